@@ -1,0 +1,276 @@
+// oracle/dslabs_oracle.cpp -- TEST INFRASTRUCTURE ONLY (see oracle_core.hpp header).
+//
+// Command-line front end of the CPU oracle. Prints one JSON object on stdout.
+//
+//   dslabs_oracle bfs --proto pingpong --clients 1 --pings 10 --inv RESULTS_OK --prune CLIENTS_DONE
+//   dslabs_oracle bfs --proto sipaxos --proposers 2 --acceptors 3 --values a,b --max-depth 9
+//   dslabs_oracle replay --proto pingpong ... --trace-file events.txt
+//   dslabs_oracle timerqueue        (TimerQueueTest.randomTimers truth table)
+//
+// Options common to bfs/replay:
+//   --inv NAME / --goal NAME / --prune NAME   (repeatable, insertion order kept; prefix "!" = negate)
+//   --max-depth N, --finish-level (level-synchronous terminal rule), --max-secs S,
+//   --no-timers ADDR, --partition a,b|c (link filter), --print-states
+#include <cstring>
+#include <fstream>
+#include <iostream>
+
+#include "oracle_core.hpp"
+#include "proto_pingpong.hpp"
+#include "proto_sipaxos.hpp"
+
+using namespace oracle;
+
+static std::string jsonEsc(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += c;
+    } else if (c == '\n') {
+      o += "\\n";
+    } else {
+      o += c;
+    }
+  }
+  return o;
+}
+
+struct Args {
+  std::string mode, proto = "pingpong";
+  std::map<std::string, std::vector<std::string>> kv;
+  bool has(const std::string& k) const { return kv.count(k) > 0; }
+  std::string get(const std::string& k, const std::string& d = "") const {
+    auto it = kv.find(k);
+    return it == kv.end() ? d : it->second.back();
+  }
+  int geti(const std::string& k, int d) const { return has(k) ? std::stoi(get(k)) : d; }
+  std::vector<std::string> all(const std::string& k) const {
+    auto it = kv.find(k);
+    return it == kv.end() ? std::vector<std::string>{} : it->second;
+  }
+};
+
+static std::vector<std::string> split(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (char c : s) {
+    if (c == sep) {
+      out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += c;
+    }
+  }
+  out.push_back(cur);
+  return out;
+}
+
+struct Scenario {
+  std::shared_ptr<State> init;
+  Names names;
+  std::function<Predicate(const std::string&)> pred;  // protocol predicate registry
+};
+
+static int addrOf(const Names& n, const std::string& s) {
+  for (size_t i = 0; i < n.addr.size(); i++)
+    if (n.addr[i] == s) return (int)i;
+  throw std::runtime_error("unknown address " + s);
+}
+
+static Scenario build(const Args& a) {
+  Scenario sc;
+  auto common = [&sc](const std::string& name) -> std::optional<Predicate> {
+    if (name == "RESULTS_OK") return RESULTS_OK(sc.names);
+    if (name == "CLIENTS_DONE") return CLIENTS_DONE();
+    if (name == "NONE_DECIDED") return NONE_DECIDED();
+    if (name.rfind("clientDone:", 0) == 0) return clientDone(sc.names, addrOf(sc.names, name.substr(11)));
+    return std::nullopt;
+  };
+  if (a.proto == "pingpong") {
+    sc.init = pingpong::initial(a.geti("clients", 1), a.geti("pings", 10), !a.has("mutant-no-check"),
+                                !a.has("mutant-no-reset"), sc.names);
+    sc.pred = [common](const std::string& n) {
+      auto p = common(n);
+      if (!p) throw std::runtime_error("unknown predicate " + n);
+      return *p;
+    };
+  } else if (a.proto == "sipaxos") {
+    int P = a.geti("proposers", 2), A = a.geti("acceptors", 3);
+    auto values = split(a.get("values", "a,b"), ',');
+    sc.init = sipaxos::initial(P, A, values, a.has("incorrect"), sc.names);
+    sc.pred = [P, values](const std::string& n) -> Predicate {
+      if (n == "Agreement") return sipaxos::agreement(P);
+      if (n == "Integrity") return sipaxos::integrity(P, values);
+      if (n == "Termination") return sipaxos::termination(P);
+      throw std::runtime_error("unknown predicate " + n);
+    };
+  } else {
+    throw std::runtime_error("unknown protocol " + a.proto);
+  }
+  return sc;
+}
+
+static Settings settingsFrom(const Args& a, Scenario& sc) {
+  Settings st;
+  auto mk = [&](const std::string& raw) {
+    if (!raw.empty() && raw[0] == '!') return sc.pred(raw.substr(1)).negate();
+    return sc.pred(raw);
+  };
+  for (auto& n : a.all("inv")) st.invariants.push_back(mk(n));
+  for (auto& n : a.all("goal")) st.goals.push_back(mk(n));
+  for (auto& n : a.all("prune")) st.prunes.push_back(mk(n));
+  st.maxDepth = a.geti("max-depth", -1);
+  for (auto& n : a.all("no-timers")) st.timersActive[addrOf(sc.names, n)] = false;
+  if (a.has("partition")) {  // TestSettings.partition: network off, links inside each group on
+    st.networkActive = false;
+    for (auto& group : split(a.get("partition"), '|')) {
+      auto members = split(group, ',');
+      for (auto& x : members)
+        for (auto& y : members)
+          if (x != y) st.linkActive[{addrOf(sc.names, x), addrOf(sc.names, y)}] = true;
+    }
+  }
+  return st;
+}
+
+static void printTerminal(const Terminal& t, const Names& names, bool printStates) {
+  std::cout << "{\"kind\":\"" << endName(t.kind) << "\",\"depth\":" << t.state->depth << ",\"predicate\":\""
+            << jsonEsc(t.predicate) << "\",\"detail\":\"" << jsonEsc(t.detail) << "\",\"trace\":[";
+  auto tr = trace(t.state);
+  bool first = true;
+  for (auto& s : tr) {
+    if (!s->previousEvent) continue;
+    std::cout << (first ? "" : ",") << "\"" << jsonEsc(eventStr(*s->previousEvent, names)) << "\"";
+    first = false;
+  }
+  std::cout << "]";
+  if (printStates) {
+    std::cout << ",\"state\":\"" << jsonEsc(t.state->key()) << "\"";
+  }
+  std::cout << "}";
+}
+
+static int runBfs(const Args& a) {
+  Scenario sc = build(a);
+  Settings st = settingsFrom(a, sc);
+  int reps = a.geti("repeat", 1);
+  Results R;
+  for (int r = 0; r < reps; r++) R = bfs(sc.init, st, a.has("finish-level"), a.has("max-secs") ? std::stod(a.get("max-secs")) : -1);
+  std::cout << "{\"end\":\"" << endName(R.end) << "\",\"states\":" << R.states << ",\"max_depth\":" << R.maxDepth
+            << ",\"successors\":" << R.successorsGenerated << ",\"elapsed_s\":" << R.elapsed << ",\"per_depth\":[";
+  for (size_t d = 0; d < R.perDepth.size(); d++) std::cout << (d ? "," : "") << R.perDepth[d];
+  std::cout << "],\"terminals\":[";
+  size_t lim = std::min<size_t>(R.terminals.size(), (size_t)a.geti("max-terminals", 64));
+  for (size_t i = 0; i < lim; i++) {
+    if (i) std::cout << ",";
+    printTerminal(R.terminals[i], sc.names, a.has("print-states"));
+  }
+  std::cout << "],\"num_terminals\":" << R.terminals.size() << "}" << std::endl;
+  return 0;
+}
+
+// Replays a list of event strings from the initial state (TraceReplaySearch.java:76-101 /
+// stepEvent(skipChecks=false): every event must be enabled in the state it is applied to).
+static int runReplay(const Args& a) {
+  Scenario sc = build(a);
+  Settings st = settingsFrom(a, sc);
+  std::ifstream in(a.get("trace-file"));
+  std::string line;
+  std::shared_ptr<const State> s = sc.init;
+  int step = 0;
+  bool ok = true;
+  std::string err;
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    bool found = false;
+    for (auto& ev : events(*s, st)) {
+      if (eventStr(ev, sc.names) == line) {
+        s = stepEvent(s, ev);
+        found = true;
+        break;
+      }
+    }
+    if (!found) {
+      ok = false;
+      err = "event " + std::to_string(step) + " not enabled: " + line;
+      break;
+    }
+    step++;
+  }
+  std::cout << "{\"ok\":" << (ok ? "true" : "false") << ",\"error\":\"" << jsonEsc(err) << "\",\"depth\":" << s->depth
+            << ",\"exception\":" << (s->exception ? "true" : "false") << ",\"invariants\":[";
+  bool first = true;
+  for (auto& p : st.invariants) {
+    PredResult r = p.test(*s);
+    std::cout << (first ? "" : ",") << "{\"name\":\"" << jsonEsc(p.name) << "\",\"value\":" << (r.value ? "true" : "false")
+              << ",\"threw\":" << (r.threw ? "true" : "false") << ",\"detail\":\"" << jsonEsc(r.detail) << "\"}";
+    first = false;
+  }
+  std::cout << "],\"goals\":[";
+  first = true;
+  for (auto& p : st.goals) {
+    PredResult r = p.test(*s);
+    std::cout << (first ? "" : ",") << "{\"name\":\"" << jsonEsc(p.name) << "\",\"value\":" << (r.value ? "true" : "false")
+              << ",\"threw\":" << (r.threw ? "true" : "false") << "}";
+    first = false;
+  }
+  std::cout << "],\"state\":\"" << jsonEsc(s->key()) << "\"}" << std::endl;
+  return 0;
+}
+
+// TimerQueueTest.randomTimers (framework/tst-self/.../search/TimerQueueTest.java:153-175) as a
+// truth table: for te1=(i,j), te2=(k,l) added in order, is te2 deliverable?
+static int runTimerQueue() {
+  std::cout << "{\"cases\":[";
+  bool first = true;
+  for (int i = 1; i <= 4; i++)
+    for (int j = i; j <= 4; j++)
+      for (int k = 1; k <= 4; k++)
+        for (int l = k; l <= 4; l++) {
+          TimerQueue tq;
+          TimerEnv t1{1, Rec{"T", {}}, i, j}, t2{2, Rec{"T", {}}, k, l};
+          tq.add(t1);
+          tq.add(t2);
+          auto d = tq.deliverable();
+          bool d1 = std::find(d.begin(), d.end(), t1) != d.end() && tq.isDeliverable(t1);
+          bool d2l = std::find(d.begin(), d.end(), t2) != d.end();
+          bool d2i = tq.isDeliverable(t2);
+          std::cout << (first ? "" : ",") << "[" << i << "," << j << "," << k << "," << l << "," << d1 << "," << d2l
+                    << "," << d2i << "]";
+          first = false;
+        }
+  std::cout << "]}" << std::endl;
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::cerr << "usage: dslabs_oracle bfs|replay|timerqueue [--opts]\n";
+    return 2;
+  }
+  Args a;
+  a.mode = argv[1];
+  for (int i = 2; i < argc; i++) {
+    std::string k = argv[i];
+    if (k.rfind("--", 0) != 0) {
+      std::cerr << "bad arg " << k << "\n";
+      return 2;
+    }
+    k = k.substr(2);
+    std::string v = "1";
+    if (i + 1 < argc && std::strncmp(argv[i + 1], "--", 2) != 0) v = argv[++i];
+    a.kv[k].push_back(v);
+  }
+  a.proto = a.get("proto", "pingpong");
+  try {
+    if (a.mode == "bfs") return runBfs(a);
+    if (a.mode == "replay") return runReplay(a);
+    if (a.mode == "timerqueue") return runTimerQueue();
+  } catch (const std::exception& e) {
+    std::cout << "{\"error\":\"" << jsonEsc(e.what()) << "\"}" << std::endl;
+    return 1;
+  }
+  std::cerr << "unknown mode\n";
+  return 2;
+}
