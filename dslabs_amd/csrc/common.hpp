@@ -1,0 +1,101 @@
+// common.hpp -- shared device/host types of the MI355X BFS engine.
+//
+// Every protocol is a struct with static __host__ __device__ transition functions over a
+// fixed-width packed State (uint32 words). The engine (engine.hip) is templated on it.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dslabs_hip.h"
+
+#define DSL_HD __host__ __device__ __forceinline__
+
+namespace dsl {
+
+// Outcome of applying the k-th enabled event to a state.
+enum StepRc : int {
+  STEP_OK = 0,
+  STEP_NULL = 1,       // destination node missing (SearchState.stepMessage returns null)
+  STEP_EXCEPTION = 2,  // handler "threw": exceptional, terminal, never equal to another state
+  STEP_OVERFLOW = 3    // bounded container exceeded: hard engine error, never truncated
+};
+
+// Predicate value (StatePredicate.test): false / true / threw.
+enum PredVal : int { PV_FALSE = 0, PV_TRUE = 1, PV_THREW = 2 };
+
+struct DevPred {
+  int32_t id;
+  int32_t negate;
+  int64_t arg0, arg1;
+};
+
+// Device form of SearchSettings/TestSettings. The tri-state precedence of
+// TestSettings.shouldDeliver (TestSettings.java:224-245) is resolved on the host into a
+// boolean matrix deliver[from] bit `to`; timers into timer_mask bit a = deliverTimers(a).
+struct DevSettings {
+  uint32_t deliver[DSL_MAX_NODES];
+  uint32_t timer_mask;
+  int32_t max_depth;
+  int32_t n_inv, n_goal, n_prune;
+  DevPred inv[DSL_MAX_PREDICATES];
+  DevPred goal[DSL_MAX_PREDICATES];
+  DevPred prune[DSL_MAX_PREDICATES];
+};
+
+DSL_HD bool should_deliver(const DevSettings& s, int from, int to) {
+  return (s.deliver[from] >> to) & 1u;
+}
+DSL_HD bool deliver_timers(const DevSettings& s, int a) { return (s.timer_mask >> a) & 1u; }
+
+// Bit-field access into a packed state. Fields never straddle a 32-bit word.
+template <int W>
+struct Packed {
+  uint32_t w[W];
+  DSL_HD uint32_t get(int bitoff, int width) const {
+    return (w[bitoff >> 5] >> (bitoff & 31)) & ((width == 32) ? 0xffffffffu : ((1u << width) - 1u));
+  }
+  DSL_HD void set(int bitoff, int width, uint32_t v) {
+    uint32_t m = ((width == 32) ? 0xffffffffu : ((1u << width) - 1u)) << (bitoff & 31);
+    uint32_t& x = w[bitoff >> 5];
+    x = (x & ~m) | ((v << (bitoff & 31)) & m);
+  }
+  DSL_HD bool bit(int b) const { return (w[b >> 5] >> (b & 31)) & 1u; }
+  DSL_HD void setbit(int b) { w[b >> 5] |= 1u << (b & 31); }
+};
+
+// How a successor is judged (Search.checkState, Search.java:162-231).
+enum Verdict : int { V_VALID = 0, V_PRUNED = 1, V_TERM_EXCEPTION = 2, V_TERM_INVARIANT = 3, V_TERM_GOAL = 4 };
+
+// Evaluates the settings' predicate programs in the reference order:
+// invariants (first violated or throwing, insertion order) -> goals (first true, throwing
+// ignored) -> prunes (any true or throwing) -> absolute depth >= maxDepth.
+template <class P>
+DSL_HD Verdict judge(const typename P::State& s, const typename P::Params& prm, const DevSettings& set,
+                     int depth, int* pred_index) {
+  for (int i = 0; i < set.n_inv; i++) {
+    int v = P::eval(set.inv[i], s, prm);
+    if (v != PV_THREW && set.inv[i].negate) v = !v;
+    if (v != PV_TRUE) {
+      *pred_index = i;
+      return V_TERM_INVARIANT;
+    }
+  }
+  for (int i = 0; i < set.n_goal; i++) {
+    int v = P::eval(set.goal[i], s, prm);
+    if (v == PV_THREW) continue;
+    if (set.goal[i].negate) v = !v;
+    if (v == PV_TRUE) {
+      *pred_index = i;
+      return V_TERM_GOAL;
+    }
+  }
+  for (int i = 0; i < set.n_prune; i++) {
+    int v = P::eval(set.prune[i], s, prm);
+    if (v != PV_THREW && set.prune[i].negate) v = !v;
+    if (v != PV_FALSE) return V_PRUNED;
+  }
+  if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
+  return V_VALID;
+}
+
+}  // namespace dsl

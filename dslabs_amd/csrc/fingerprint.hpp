@@ -1,0 +1,105 @@
+// fingerprint.hpp -- 128-bit state fingerprint and the HBM-resident visited table.
+//
+// Fingerprint: MurmurHash3_x64_128 block/finalizer structure over the canonical packed
+// state (16-byte blocks, the state width is a multiple of 16 bytes). Unused bits of a
+// packed state are always zero, so equal canonical states have equal fingerprints.
+//
+// Visited table: open addressing over 64-byte buckets of eight 8-byte slots. A slot holds
+// the fingerprint's high word (forced non-zero); the home bucket is taken from the low word
+// and the owner shard (multi-GPU) from the low word's top bits, so a stored key pins
+// 64 + log2(buckets) + log2(shards) bits of the 128-bit fingerprint. Slots are write-once
+// (0 -> key with one 64-bit CAS), which makes a plain (possibly stale) read of a bucket safe:
+// a key seen is really there, and a slot seen empty is settled by the CAS. No two-phase
+// publish, no spinning on another lane's store.
+#pragma once
+#include "common.hpp"
+
+namespace dsl {
+
+struct Fp {
+  uint64_t hi, lo;
+};
+
+DSL_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+DSL_HD uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+template <int W>
+DSL_HD Fp fingerprint(const uint32_t (&w)[W]) {
+  static_assert(W % 4 == 0, "packed state must be a multiple of 16 bytes");
+  const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+  uint64_t h1 = 0x9368e53c2f6af274ULL, h2 = 0x586dcd208f7cd3fdULL;
+#pragma unroll
+  for (int i = 0; i < W; i += 4) {
+    uint64_t k1 = (uint64_t)w[i] | ((uint64_t)w[i + 1] << 32);
+    uint64_t k2 = (uint64_t)w[i + 2] | ((uint64_t)w[i + 3] << 32);
+    k1 *= c1;
+    k1 = rotl64(k1, 31);
+    k1 *= c2;
+    h1 ^= k1;
+    h1 = rotl64(h1, 27);
+    h1 += h2;
+    h1 = h1 * 5 + 0x52dce729;
+    k2 *= c2;
+    k2 = rotl64(k2, 33);
+    k2 *= c1;
+    h2 ^= k2;
+    h2 = rotl64(h2, 31);
+    h2 += h1;
+    h2 = h2 * 5 + 0x38495ab5;
+  }
+  h1 ^= (uint64_t)(W * 4);
+  h2 ^= (uint64_t)(W * 4);
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  h2 += h1;
+  return Fp{h1, h2};
+}
+
+// Owner shard of a fingerprint: multiply-shift on the top 32 bits of the low word.
+DSL_HD int owner_of(const Fp& f, int world) {
+  return (int)(((f.lo >> 32) * (uint64_t)world) >> 32);
+}
+
+enum InsertRc : int { INS_NEW = 0, INS_EXISTS = 1, INS_FULL = 2 };
+
+struct Table {
+  unsigned long long* slots;  // nbuckets * 8
+  uint64_t bucket_mask;       // nbuckets - 1 (power of two)
+  int max_probes;             // buckets visited before declaring the table full
+};
+
+__device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
+  const unsigned long long key = (unsigned long long)(f.hi | 1ull);
+  uint64_t b = f.lo & t.bucket_mask;
+  for (int probe = 0; probe < t.max_probes; probe++) {
+    unsigned long long* B = t.slots + ((b + (uint64_t)probe) & t.bucket_mask) * 8;
+    // One 64-byte line: four 16-byte loads.
+    const ulonglong2* B2 = reinterpret_cast<const ulonglong2*>(B);
+    ulonglong2 q0 = B2[0], q1 = B2[1], q2 = B2[2], q3 = B2[3];
+    unsigned long long s[8] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y, q3.x, q3.y};
+    bool hit = false;
+#pragma unroll
+    for (int j = 0; j < 8; j++) hit |= (s[j] == key);
+    if (hit) return INS_EXISTS;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (s[j] != 0) continue;  // occupied by another key (write-once)
+      unsigned long long old = atomicCAS(B + j, 0ull, key);
+      if (old == 0ull) return INS_NEW;
+      if (old == key) return INS_EXISTS;
+    }
+  }
+  return INS_FULL;
+}
+
+}  // namespace dsl

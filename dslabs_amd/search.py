@@ -1,0 +1,416 @@
+"""Host-side mirror of the reference's search API, running the MI355X engine.
+
+Mirrors (names, argument meaning, error behaviour) of, relative to
+/root/reference/framework/tst/dslabs/framework/testing:
+  * search/Search.java:390-395            ``Search.bfs(initialState, settings)``
+  * search/SearchSettings.java:43-199     ``SearchSettings`` (maxDepth, addGoal/addPrune, ...)
+  * TestSettings.java:46-245              invariants, maxTimeSecs, link/sender/receiver filters,
+                                          partition, deliverTimers
+  * search/SearchResults.java:34-88       ``SearchResults`` / ``EndCondition``
+  * StatePredicate.java:52-83, :382-396   standard predicates and ``negate()``
+
+Every search runs on the GPU through libdslabs_hip.so; there is no CPU fallback.
+Method names keep the reference's camelCase so that tests read like the reference's tests.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+from . import _lib
+from ._lib import check
+
+
+class EndCondition(enum.IntEnum):
+    EXCEPTION_THROWN = 0
+    INVARIANT_VIOLATED = 1
+    GOAL_FOUND = 2
+    SPACE_EXHAUSTED = 3
+    TIME_EXHAUSTED = 4
+
+
+# dsl_predicate_id
+PRED_RESULTS_OK = 1
+PRED_CLIENTS_DONE = 2
+PRED_CLIENT_DONE = 3
+PRED_NONE_DECIDED = 4
+PRED_CLIENT_HAS_RESULTS = 5
+
+
+class StatePredicate:
+    """A named state predicate evaluated on the device (StatePredicate.java).
+
+    ``address_args`` names the positional args that are node addresses; they are resolved
+    to node indices against the search state's address table when the search starts.
+    """
+
+    def __init__(self, name: str, pred_id: int, arg0=0, arg1=0, negated: bool = False,
+                 address_args: Sequence[int] = ()):
+        self.name = name
+        self.pred_id = pred_id
+        self.arg0 = arg0
+        self.arg1 = arg1
+        self.negated = negated
+        self.address_args = tuple(address_args)
+
+    def negate(self) -> "StatePredicate":
+        # StatePredicate.negate(): "¬(name)" or strip an existing "¬(...)".
+        if self.name.startswith("¬(") and self.name.endswith(")"):
+            name = self.name[2:-1]
+        else:
+            name = f"¬({self.name})"
+        return StatePredicate(name, self.pred_id, self.arg0, self.arg1, not self.negated, self.address_args)
+
+    def _encode(self, state: "SearchState") -> _lib.dsl_predicate:
+        args = [self.arg0, self.arg1]
+        for i in self.address_args:
+            args[i] = state.protocol.address_index(args[i])
+        return _lib.dsl_predicate(self.pred_id, 1 if self.negated else 0, int(args[0]), int(args[1]))
+
+    def __repr__(self) -> str:
+        return self.name
+
+
+RESULTS_OK = StatePredicate("Clients got expected results", PRED_RESULTS_OK)
+CLIENTS_DONE = StatePredicate("All clients' workloads finished", PRED_CLIENTS_DONE)
+NONE_DECIDED = StatePredicate("No results returned", PRED_NONE_DECIDED)
+
+
+def clientDone(address: str) -> StatePredicate:
+    return StatePredicate(f"{address}'s workload finished", PRED_CLIENT_DONE, address, address_args=(0,))
+
+
+def clientHasResults(address: str, numResults: int) -> StatePredicate:
+    return StatePredicate(f"{address} received {numResults} results", PRED_CLIENT_HAS_RESULTS, address,
+                          numResults, address_args=(0,))
+
+
+@dataclass
+class PredicateResult:
+    """StatePredicate.PredicateResult: which predicate fired and its value."""
+    predicate: StatePredicate
+    value: Optional[bool]
+
+    def errorMessage(self) -> str:
+        verb = "matches" if self.value else "violates"
+        return f'State {verb} "{self.predicate.name}"'
+
+
+class SearchSettings:
+    """SearchSettings + TestSettings (fluent setters return self)."""
+
+    def __init__(self):
+        self._invariants: List[StatePredicate] = []
+        self._goals: List[StatePredicate] = []
+        self._prunes: List[StatePredicate] = []
+        self._max_depth = -1
+        self._max_time_secs = -1
+        self._network_active = True
+        self._link = {}
+        self._sender = {}
+        self._receiver = {}
+        self._deliver_timers = True
+        self._timers_active = {}
+        self.table_log2_slots = 0
+        self.max_frontier_states = 0
+
+    # TestSettings -------------------------------------------------------------------------
+    def addInvariant(self, p: StatePredicate) -> "SearchSettings":
+        self._invariants.append(p)
+        return self
+
+    def clearInvariants(self) -> "SearchSettings":
+        self._invariants.clear()
+        return self
+
+    def invariants(self) -> List[StatePredicate]:
+        return list(self._invariants)
+
+    def maxTimeSecs(self, secs: int) -> "SearchSettings":
+        self._max_time_secs = secs
+        return self
+
+    def timeLimited(self) -> bool:
+        return self._max_time_secs > 0
+
+    def linkActive(self, frm: str, to: str, active: bool) -> "SearchSettings":
+        self._link[(frm, to)] = active
+        return self
+
+    def senderActive(self, frm: str, active: bool) -> "SearchSettings":
+        self._sender[frm] = active
+        return self
+
+    def receiverActive(self, to: str, active: bool) -> "SearchSettings":
+        self._receiver[to] = active
+        return self
+
+    def nodeActive(self, node: str, active: bool) -> "SearchSettings":
+        self.receiverActive(node, active)
+        return self.senderActive(node, active)
+
+    def networkActive(self, active: bool) -> "SearchSettings":
+        self._network_active = active
+        return self
+
+    def partition(self, *groups) -> "SearchSettings":
+        """TestSettings.partition: network off, links inside each group on.
+        Accepts addresses (one group) or sequences of addresses (several groups)."""
+        if groups and isinstance(groups[0], str):
+            groups = (groups,)
+        self._network_active = False
+        for g in groups:
+            for a in g:
+                for b in g:
+                    if a != b:
+                        self._link[(a, b)] = True
+        return self
+
+    def reconnect(self) -> "SearchSettings":
+        self._network_active = True
+        self._link.clear()
+        self._sender.clear()
+        self._receiver.clear()
+        return self
+
+    def deliverTimers(self, *args) -> "SearchSettings":
+        if len(args) == 1:
+            self._deliver_timers = bool(args[0])
+        else:
+            self._timers_active[args[0]] = bool(args[1])
+        return self
+
+    def clearDeliverTimers(self) -> "SearchSettings":
+        self._deliver_timers = True
+        self._timers_active.clear()
+        return self
+
+    # SearchSettings ------------------------------------------------------------------------
+    def maxDepth(self, depth: int) -> "SearchSettings":
+        self._max_depth = depth
+        return self
+
+    def depthLimited(self) -> bool:
+        return self._max_depth >= 0
+
+    def addGoal(self, p: StatePredicate) -> "SearchSettings":
+        self._goals.append(p)
+        return self
+
+    def clearGoals(self) -> "SearchSettings":
+        self._goals.clear()
+        return self
+
+    def goals(self) -> List[StatePredicate]:
+        return list(self._goals)
+
+    def addPrune(self, p: StatePredicate) -> "SearchSettings":
+        self._prunes.append(p)
+        return self
+
+    def clearPrunes(self) -> "SearchSettings":
+        self._prunes.clear()
+        return self
+
+    def prunes(self) -> List[StatePredicate]:
+        return list(self._prunes)
+
+    def clone(self) -> "SearchSettings":
+        s = SearchSettings()
+        s.__dict__.update({k: (v.copy() if isinstance(v, (list, dict)) else v) for k, v in self.__dict__.items()})
+        return s
+
+    # encoding -------------------------------------------------------------------------------
+    def _encode(self, state: "SearchState") -> _lib.dsl_settings:
+        proto = state.protocol
+        s = _lib.dsl_settings()
+        s.max_depth = self._max_depth
+        s.max_time_ms = self._max_time_secs * 1000 if self._max_time_secs > 0 else -1
+        s.network_active = 1 if self._network_active else 0
+        s.deliver_timers = 1 if self._deliver_timers else 0
+        ctypes.memset(ctypes.addressof(s.link_active), 0xFF, ctypes.sizeof(s.link_active))
+        ctypes.memset(ctypes.addressof(s.sender_active), 0xFF, ctypes.sizeof(s.sender_active))
+        ctypes.memset(ctypes.addressof(s.receiver_active), 0xFF, ctypes.sizeof(s.receiver_active))
+        ctypes.memset(ctypes.addressof(s.timers_active), 0xFF, ctypes.sizeof(s.timers_active))
+        for (a, b), v in self._link.items():
+            s.link_active[proto.address_index(a)][proto.address_index(b)] = 1 if v else 0
+        for a, v in self._sender.items():
+            s.sender_active[proto.address_index(a)] = 1 if v else 0
+        for a, v in self._receiver.items():
+            s.receiver_active[proto.address_index(a)] = 1 if v else 0
+        for a, v in self._timers_active.items():
+            s.timers_active[proto.address_index(a)] = 1 if v else 0
+        for name, lst, arr in (("n_invariants", self._invariants, s.invariants),
+                               ("n_goals", self._goals, s.goals), ("n_prunes", self._prunes, s.prunes)):
+            if len(lst) > _lib.DSL_MAX_PREDICATES:
+                raise ValueError("too many predicates")
+            setattr(s, name, len(lst))
+            for i, p in enumerate(lst):
+                arr[i] = p._encode(state)
+        s.table_log2_slots = self.table_log2_slots
+        s.max_frontier_states = self.max_frontier_states
+        return s
+
+
+class SearchState:
+    """A search state handle: the protocol configuration plus (optionally) a packed state.
+
+    ``SearchState`` objects for the initial state are made by the protocol builders in
+    ``dslabs_amd.protocols``; terminal states come back from a search with their event trace
+    (``trace()``), the analogue of the reference's ``previous`` chain.
+    """
+
+    def __init__(self, protocol, packed: Optional[bytes] = None, depth: int = 0,
+                 events: Optional[List[str]] = None, raw_events=None):
+        self.protocol = protocol
+        self.packed = packed
+        self._depth = depth
+        self._events = events or []
+        self._raw_events = raw_events or []
+
+    def depth(self) -> int:
+        return self._depth
+
+    def trace(self) -> List[str]:
+        """Events from the search's initial state to this state (SearchState.trace())."""
+        return list(self._events)
+
+    def addresses(self) -> List[str]:
+        return list(self.protocol.addresses)
+
+
+class SearchResults:
+    def __init__(self, end, states, per_depth, initial_depth, max_depth, terminal: Optional[SearchState],
+                 predicate: Optional[PredicateResult], elapsed_s: float, successors: int):
+        self._end = end
+        self.states = states
+        self.per_depth = per_depth
+        self.initial_depth = initial_depth
+        self.max_depth = max_depth
+        self._terminal = terminal
+        self._predicate = predicate
+        self.elapsed_s = elapsed_s
+        self.successors = successors
+
+    def endCondition(self) -> EndCondition:
+        return self._end
+
+    def invariantViolatingState(self) -> Optional[SearchState]:
+        return self._terminal if self._end == EndCondition.INVARIANT_VIOLATED else None
+
+    def invariantViolated(self) -> Optional[PredicateResult]:
+        return self._predicate if self._end == EndCondition.INVARIANT_VIOLATED else None
+
+    def goalMatchingState(self) -> Optional[SearchState]:
+        return self._terminal if self._end == EndCondition.GOAL_FOUND else None
+
+    def goalMatched(self) -> Optional[PredicateResult]:
+        return self._predicate if self._end == EndCondition.GOAL_FOUND else None
+
+    def exceptionalState(self) -> Optional[SearchState]:
+        return self._terminal if self._end == EndCondition.EXCEPTION_THROWN else None
+
+    def exceptionThrown(self) -> bool:
+        return self._end == EndCondition.EXCEPTION_THROWN
+
+    def statesPerSecond(self) -> float:
+        return self.states / self.elapsed_s if self.elapsed_s > 0 else float("inf")
+
+    def status(self) -> str:
+        # BFS.status() line (Search.java:426-431)
+        return "Explored: %d, Depth: %d (%.2fs, %.2fK states/s)" % (
+            self.states, self.max_depth, self.elapsed_s, self.statesPerSecond() / 1000.0)
+
+
+class Engine:
+    """One engine (one GPU, or one shard of a multi-GPU search)."""
+
+    def __init__(self, protocol, device: int = -1, rank: int = 0, world_size: int = 1,
+                 virtual_shards: int = 0, comm_id: Optional[bytes] = None):
+        lib = _lib.load()
+        self.lib = lib
+        self.protocol = protocol
+        cfg = _lib.dsl_engine_config()
+        cfg.device = device
+        cfg.rank = rank
+        cfg.world_size = world_size
+        cfg.virtual_shards = virtual_shards
+        if comm_id is not None:
+            ctypes.memmove(cfg.comm_id, comm_id, 128)
+        handle = ctypes.c_void_p()
+        check(lib.dsl_create(ctypes.byref(protocol.desc()), ctypes.byref(cfg), ctypes.byref(handle)), "dsl_create")
+        self.handle = handle
+
+    def close(self):
+        if self.handle:
+            self.lib.dsl_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def state_bytes(self) -> int:
+        return self.lib.dsl_state_bytes(ctypes.byref(self.protocol.desc()))
+
+    def initial_packed(self) -> bytes:
+        n = self.state_bytes()
+        buf = (ctypes.c_uint8 * n)()
+        check(self.lib.dsl_get_initial(self.handle, buf, n), "dsl_get_initial")
+        return bytes(buf)
+
+    def kernel_stats(self):
+        ms = ctypes.c_double()
+        launches = ctypes.c_uint64()
+        items = ctypes.c_uint64()
+        check(self.lib.dsl_kernel_stats(self.handle, ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(items)),
+              "dsl_kernel_stats")
+        return ms.value, launches.value, items.value
+
+    def bfs(self, state: SearchState, settings: Optional[SearchSettings] = None) -> SearchResults:
+        if settings is None:
+            settings = SearchSettings()
+        lib = self.lib
+        enc = settings._encode(state)
+        check(lib.dsl_set_settings(self.handle, ctypes.byref(enc)), "dsl_set_settings")
+        if state.packed is not None:
+            buf = (ctypes.c_uint8 * len(state.packed)).from_buffer_copy(state.packed)
+            check(lib.dsl_set_initial(self.handle, buf, len(state.packed), state.depth()), "dsl_set_initial")
+        res_p = ctypes.POINTER(_lib.dsl_result)()
+        check(lib.dsl_run(self.handle, ctypes.byref(res_p)), "dsl_run")
+        try:
+            r = res_p.contents
+            per_depth = [r.per_depth[i] for i in range(r.n_levels)]
+            end = EndCondition(r.end_condition)
+            terminal = None
+            pred = None
+            if r.terminal_depth >= 0 and r.terminal_state:
+                raw = [r.trace[i] for i in range(r.trace_len)]
+                events = [self.protocol.render_event(e) for e in raw]
+                packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
+                base_events = state.trace() if state.packed is not None else []
+                terminal = SearchState(self.protocol, packed, r.terminal_depth, base_events + events,
+                                       [(e.is_timer, e.from_, e.to, e.type, tuple(e.fields[:e.n_fields])) for e in raw])
+                if end == EndCondition.INVARIANT_VIOLATED:
+                    pred = PredicateResult(settings.invariants()[r.predicate_index], False)
+                elif end == EndCondition.GOAL_FOUND:
+                    pred = PredicateResult(settings.goals()[r.predicate_index], True)
+            return SearchResults(end, r.states, per_depth, r.initial_depth, r.max_depth, terminal, pred,
+                                 r.elapsed_s, r.successors)
+        finally:
+            lib.dsl_result_free(res_p)
+
+
+class Search:
+    @staticmethod
+    def bfs(initialState: SearchState, settings: Optional[SearchSettings] = None, device: int = -1) -> SearchResults:
+        """Search.bfs (Search.java:390-395) on the MI355X engine."""
+        eng = Engine(initialState.protocol, device=device)
+        try:
+            return eng.bfs(initialState, settings)
+        finally:
+            eng.close()

@@ -1,0 +1,186 @@
+/*
+ * dslabs_hip.h -- C ABI of libdslabs_hip.so, the MI355X breadth-first model-checking engine.
+ *
+ * This ABI is the drop-in boundary for the reference's BFS strategy. The reference has no
+ * FFI (it is pure Java); each entry point below replaces a piece of the Java search and is what a
+ * `GpuBFS extends Search` strategy binds through JNI / Panama FFM.
+ * Paths are relative to the reference root, T = framework/tst/dslabs/framework/testing.
+ *
+ *   dsl_create          <- `new BFS(settings)` + the NodeGenerator / addServer / addClientWorker
+ *                          calls that build the initial SearchState
+ *                          (T/search/Search.java:390-395, T/AbstractState.java:207-241)
+ *   dsl_set_settings    <- SearchSettings / TestSettings: maxDepth, maxTimeSecs, invariants,
+ *                          goals, prunes, link/sender/receiver filters, timer masks
+ *                          (T/search/SearchSettings.java:43-135, T/TestSettings.java:46-245)
+ *   dsl_set_initial     <- starting a search from a non-initial SearchState (a goal state of an
+ *                          earlier search, depth > 0), e.g. PaxosTest.java:898-910
+ *   dsl_run             <- Search.run(initialState) for BFS (T/search/Search.java:233-388,
+ *                          :405-505): returns the SearchResults equivalent
+ *   dsl_result_free     <- (GC in Java)
+ *   dsl_progress        <- BFS.status() "Explored: N, Depth: D" (T/search/Search.java:426-431)
+ *   dsl_last_error      <- Java exceptions on infrastructure errors
+ *
+ * Conventions: every function returning int returns DSL_OK (0) or a negative dsl_status.
+ * Caller-owned input buffers are copied during the call. dsl_result is library-allocated and
+ * released with dsl_result_free. One engine per calling thread; dsl_run blocks.
+ */
+#ifndef DSLABS_HIP_H_
+#define DSLABS_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSL_ABI_VERSION 1
+#define DSL_MAX_NODES 32
+#define DSL_MAX_PREDICATES 16
+#define DSL_MAX_PARAMS 64
+#define DSL_MAX_EVENT_FIELDS 8
+
+typedef enum {
+  DSL_OK = 0,
+  DSL_ERR_ARG = -1,
+  DSL_ERR_HIP = -2,
+  DSL_ERR_TABLE_FULL = -3,        /* visited table capacity exhausted */
+  DSL_ERR_FRONTIER_FULL = -4,     /* next frontier exceeds its capacity */
+  DSL_ERR_STATE_OVERFLOW = -5,    /* a successor exceeded the packed state's bounded message
+                                     set / timer list / log (never silently truncated) */
+  DSL_ERR_UNKNOWN_PROTOCOL = -6,
+  DSL_ERR_UNKNOWN_PREDICATE = -7,
+  DSL_ERR_COMM = -8,
+  DSL_ERR_NO_DEVICE = -9,
+  DSL_ERR_PROBE_LIMIT = -10       /* a visited-table probe sequence did not settle */
+} dsl_status;
+
+/* SearchResults.EndCondition (T/search/SearchResults.java:35-41), same order of priority. */
+typedef enum {
+  DSL_EXCEPTION_THROWN = 0,
+  DSL_INVARIANT_VIOLATED = 1,
+  DSL_GOAL_FOUND = 2,
+  DSL_SPACE_EXHAUSTED = 3,
+  DSL_TIME_EXHAUSTED = 4
+} dsl_end_condition;
+
+/* Protocols with device transition functions. */
+typedef enum {
+  DSL_PROTO_PINGPONG = 1,   /* lab0 PingPong (labs/lab0-pingpong/src/dslabs/pingpong) */
+  DSL_PROTO_SIPAXOS = 2,    /* single-instance Paxos (T/visualization/examples/paxosmadesimple) */
+  DSL_PROTO_SYNTHETIC = 3,  /* table-driven synthetic protocol (BASELINE config C3) */
+  DSL_PROTO_AMOKV = 4,      /* lab1 at-most-once KV client/server (BASELINE config C2) */
+  DSL_PROTO_MULTIPAXOS = 5  /* lab3 Multi-Paxos (BASELINE config C5) */
+} dsl_protocol_id;
+
+typedef struct {
+  int32_t protocol;              /* dsl_protocol_id */
+  int32_t n_params;
+  int64_t params[DSL_MAX_PARAMS];/* protocol parameters, see dslabs_amd/protocols.py */
+} dsl_protocol_desc;
+
+/* Standard predicates (T/StatePredicate.java:52-83) and protocol predicates.
+ * Args are node indices / counts as documented per predicate. */
+typedef enum {
+  DSL_PRED_RESULTS_OK = 1,          /* "Clients got expected results" */
+  DSL_PRED_CLIENTS_DONE = 2,        /* "All clients' workloads finished" */
+  DSL_PRED_CLIENT_DONE = 3,         /* clientDone(addr): arg0 = node index */
+  DSL_PRED_NONE_DECIDED = 4,        /* "No results returned" */
+  DSL_PRED_CLIENT_HAS_RESULTS = 5,  /* clientHasResults(addr, n): arg0 node, arg1 n */
+  DSL_PRED_SIP_AGREEMENT = 100,     /* SingleInstancePaxos "Agreement" */
+  DSL_PRED_SIP_INTEGRITY = 101,     /* SingleInstancePaxos "Integrity" */
+  DSL_PRED_SIP_TERMINATION = 102,   /* SingleInstancePaxos "Termination" */
+  DSL_PRED_SYNTH_NOT_ALL_MAX = 200, /* synthetic: not every node word at its maximum */
+  DSL_PRED_SYNTH_COUNTER_LT = 201,  /* synthetic: node word arg0 < arg1 */
+  DSL_PRED_APPENDS_LINEARIZABLE = 300, /* KVStoreWorkload.APPENDS_LINEARIZABLE */
+  DSL_PRED_LOGS_CONSISTENT = 400    /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS */
+} dsl_predicate_id;
+
+typedef struct {
+  int32_t pred_id;   /* dsl_predicate_id */
+  int32_t negate;    /* StatePredicate.negate() */
+  int64_t arg0, arg1;
+} dsl_predicate;
+
+#define DSL_TRISTATE_UNSET (-1)
+
+typedef struct {
+  int32_t max_depth;        /* SearchSettings.maxDepth, -1 = unlimited (absolute depth) */
+  int32_t max_time_ms;      /* TestSettings.maxTimeSecs*1000, -1 = unlimited; checked per level */
+  int32_t network_active;   /* TestSettings.networkActive */
+  int32_t deliver_timers;   /* TestSettings.deliverTimers (global default) */
+  int8_t link_active[DSL_MAX_NODES][DSL_MAX_NODES]; /* [from][to]: -1 unset, 0, 1 */
+  int8_t sender_active[DSL_MAX_NODES];
+  int8_t receiver_active[DSL_MAX_NODES];
+  int8_t timers_active[DSL_MAX_NODES];
+  int32_t n_invariants, n_goals, n_prunes;          /* ordered, as inserted */
+  dsl_predicate invariants[DSL_MAX_PREDICATES];
+  dsl_predicate goals[DSL_MAX_PREDICATES];
+  dsl_predicate prunes[DSL_MAX_PREDICATES];
+  /* engine capacity knobs (0 = automatic) */
+  int32_t table_log2_slots; /* visited table = 2^k 16-byte slots (per shard) */
+  int32_t reserved0;
+  uint64_t max_frontier_states;
+  uint64_t memory_budget_bytes;
+} dsl_settings;
+
+typedef struct {
+  int32_t device;           /* HIP device ordinal, -1 = current */
+  int32_t rank, world_size; /* shard index / number of shards (one process or thread per GPU) */
+  int32_t virtual_shards;   /* >1: emulate that many hash shards on this one device (tests) */
+  uint8_t comm_id[128];     /* RCCL ncclUniqueId when world_size > 1 */
+} dsl_engine_config;
+
+/* A decoded event (MessageEnvelope / TimerEnvelope, T/MessageEnvelope.java, T/TimerEnvelope.java). */
+typedef struct {
+  int32_t is_timer;
+  int32_t from, to;         /* node indices (from == to for timers) */
+  int32_t type;             /* protocol message / timer type id */
+  int32_t n_fields;
+  int32_t timer_min, timer_max;
+  int32_t reserved;
+  int64_t fields[DSL_MAX_EVENT_FIELDS];
+} dsl_event;
+
+typedef struct {
+  int32_t end_condition;    /* dsl_end_condition */
+  int32_t terminal_depth;   /* depth of the reported terminal state, -1 if none */
+  int32_t predicate_index;  /* index in invariants[] / goals[] that fired, -1 if none */
+  int32_t max_depth;        /* deepest discovered state (BFS.depth) */
+  uint64_t states;          /* unique states, reference counting rule (Search.java:470-490) */
+  int32_t n_levels;
+  int32_t trace_len;
+  uint64_t* per_depth;      /* [n_levels]: states discovered at depth initial_depth + i */
+  dsl_event* trace;         /* [trace_len]: events from the initial state to the terminal */
+  uint8_t* terminal_state;  /* packed terminal state (state_bytes), NULL if none */
+  uint32_t state_bytes;
+  int32_t initial_depth;
+  double elapsed_s;         /* wall time of the search (excludes dsl_create) */
+  uint64_t successors;      /* successor states generated (events applied) */
+  uint64_t new_states_inserted;
+  uint64_t exchanged_states;/* states routed to another shard (multi-GPU) */
+  double level_ms_max;
+} dsl_result;
+
+typedef struct dsl_engine dsl_engine;
+
+int dsl_abi_version(void);
+int dsl_device_count(void);
+int dsl_state_bytes(const dsl_protocol_desc* proto);
+int dsl_comm_unique_id(uint8_t out[128]);
+int dsl_create(const dsl_protocol_desc* proto, const dsl_engine_config* cfg, dsl_engine** out);
+int dsl_set_settings(dsl_engine* e, const dsl_settings* s);
+int dsl_set_initial(dsl_engine* e, const uint8_t* packed, size_t len, int32_t depth);
+int dsl_get_initial(dsl_engine* e, uint8_t* packed, size_t len);
+int dsl_run(dsl_engine* e, dsl_result** out);
+int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth);
+int dsl_kernel_stats(dsl_engine* e, double* expand_ms_total, uint64_t* expand_launches,
+                     uint64_t* work_items);
+void dsl_result_free(dsl_result* r);
+void dsl_destroy(dsl_engine* e);
+const char* dsl_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DSLABS_HIP_H_ */

@@ -1,0 +1,118 @@
+"""Regenerates tests/golden/*.json from the CPU oracle (oracle/_build/dslabs_oracle).
+
+Every fixture records the oracle arguments, the oracle's output, and -- where the reference
+itself states a number -- the pinned reference fact with its source (paths relative to
+/root/reference). tests/test_oracle_golden.py checks oracle == fixture == pinned facts.
+Usage: python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import oracle_util  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+PP = ["--proto", "pingpong"]
+LAB0 = {
+    # labs/lab0-pingpong/tst/dslabs/pingpong/PingTest.java:128-140 (test04 phase 2)
+    "lab0_1c10p_exhaustive": dict(
+        args=PP + ["--clients", "1", "--pings", "10", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"],
+        pinned={"states": 120, "max_depth": 29, "end": "SPACE_EXHAUSTED",
+                "source": "labs/lab0-pingpong/README.md:282-285 (Explored: 120, Depth: 29)"}),
+    # test04 phase 1: goal CLIENTS_DONE (finish-level = level-synchronous terminal rule)
+    "lab0_1c10p_goal": dict(
+        args=PP + ["--clients", "1", "--pings", "10", "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE",
+                   "--finish-level"],
+        pinned={"terminal_depth": 20, "states": 84, "end": "GOAL_FOUND",
+                "source": "labs/lab0-pingpong/README.md:276-279 (Explored: 84, Depth: 20 -- the "
+                          "multithreaded JVM had completed the goal level)"}),
+    "lab0_1c2p_goal": dict(
+        args=PP + ["--clients", "1", "--pings", "2", "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE"],
+        pinned={"states": 6, "terminal_depth": 4, "end": "GOAL_FOUND",
+                "source": "labs/lab0-pingpong/img/state-graph.png, README.md:509-597 (6 states, goal depth 4)"}),
+    "lab0_1c2p_goal_level": dict(
+        args=PP + ["--clients", "1", "--pings", "2", "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE",
+                   "--finish-level"], pinned={"terminal_depth": 4, "end": "GOAL_FOUND", "source": "as above"}),
+    "lab0_1c2p_exhaustive": dict(
+        args=PP + ["--clients", "1", "--pings", "2", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"],
+        pinned={"states": 8, "max_depth": 5, "source": "SURVEY.md §8c derived vector (independent restatement)"}),
+    "lab0_2c10p_exhaustive": dict(
+        args=PP + ["--clients", "2", "--pings", "10", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"],
+        pinned={"states": 14640, "max_depth": 59,
+                "per_depth": [1, 2, 3, 6, 9, 12, 18, 24, 30, 40, 50, 60, 75, 90, 105, 126, 147, 168, 196, 224, 252,
+                              286, 318, 348, 383, 414, 441, 472, 497, 516, 538, 552, 560, 570, 572, 568, 565, 554,
+                              537, 520, 495, 464, 433, 396, 356, 318, 277, 236, 199, 162, 128, 100, 75, 54, 39, 26,
+                              16, 10, 5, 2],
+                "source": "SURVEY.md §8c derived vector (independent restatement), BASELINE.md C1"}),
+    # README "When Things Go Wrong": pong-value check removed (README.md:342-347)
+    "lab0_mutant_nocheck": dict(
+        args=PP + ["--clients", "1", "--pings", "10", "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE",
+                   "--mutant-no-check", "--finish-level"],
+        pinned={"terminal_depth": 3, "end": "INVARIANT_VIOLATED",
+                "trace": ["Message(client1 -> pingserver, PingRequest(ping-1))",
+                          "Message(pingserver -> client1, PongReply(ping-1))",
+                          "Message(pingserver -> client1, PongReply(ping-1))"],
+                "detail": "client1 got Pong(ping-1), expected Pong(ping-2)",
+                "source": "labs/lab0-pingpong/README.md:366-423 (3-event trace; 'client1 got "
+                          "PingApplication.Pong(value=ping-1), expected PingApplication.Pong(value=ping-2)')"}),
+    # 1 client, 3 pings, partitioned (no messages): only timers fire; exhausted immediately
+    "lab0_1c3p_partition": dict(
+        args=PP + ["--clients", "1", "--pings", "3", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE",
+                   "--partition", "pingserver|client1"], pinned={}),
+    "lab0_2c4p_maxdepth7": dict(
+        args=PP + ["--clients", "2", "--pings", "4", "--inv", "RESULTS_OK", "--max-depth", "7"], pinned={}),
+    "lab0_2c3p_notimers": dict(
+        args=PP + ["--clients", "2", "--pings", "3", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE",
+                   "--no-timers", "client2"], pinned={}),
+    "lab0_3c3p_exhaustive": dict(
+        args=PP + ["--clients", "3", "--pings", "3", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"], pinned={}),
+    "lab0_mutant_noreset": dict(
+        args=PP + ["--clients", "2", "--pings", "3", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE",
+                   "--mutant-no-reset"], pinned={}),
+}
+
+
+def gen(cases, fname):
+    out = {}
+    for name, c in cases.items():
+        r = oracle_util.run("bfs", c["args"], timeout=600)
+        if r.get("terminals"):
+            t = r["terminals"]
+            r["terminal_depth"] = t[0]["depth"]
+        out[name] = {"args": c["args"], "pinned": c["pinned"], "end": r["end"], "states": r["states"],
+                     "max_depth": r["max_depth"], "per_depth": r["per_depth"],
+                     "terminal_depth": r.get("terminal_depth", -1),
+                     "terminal_kinds": sorted({t["kind"] for t in r.get("terminals", [])}),
+                     "terminals": r.get("terminals", [])[:8]}
+        print(name, r["end"], r["states"], r["max_depth"])
+    with open(os.path.join(HERE, fname), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    gen(LAB0, "lab0.json")
+    SIP = {
+        "sipaxos_2p3a_d9": dict(
+            args=["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
+                  "Integrity", "--inv", "Agreement", "--max-depth", "9"],
+            pinned={"per_depth": [1, 2, 9, 34, 112, 360, 1143, 3556, 10884, 32981],
+                    "source": "SURVEY.md §8c derived vector (independent restatement)"}),
+        "sipaxos_2p3a_d6": dict(
+            args=["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
+                  "Integrity", "--inv", "Agreement", "--max-depth", "6"], pinned={}),
+        "sipaxos_incorrect_2p3a": dict(
+            args=["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
+                  "Integrity", "--inv", "Agreement", "--incorrect", "--max-depth", "11", "--finish-level"],
+            pinned={}),
+        "sipaxos_3p3a_d6": dict(
+            args=["--proto", "sipaxos", "--proposers", "3", "--acceptors", "3", "--values", "a,b,c", "--inv",
+                  "Integrity", "--inv", "Agreement", "--max-depth", "6"], pinned={}),
+    }
+    gen(SIP, "sipaxos.json")
+    tq = oracle_util.run("timerqueue", [])
+    with open(os.path.join(HERE, "timerqueue.json"), "w") as f:
+        json.dump({"source": "framework/tst-self/dslabs/framework/testing/search/TimerQueueTest.java:153-175",
+                   "columns": ["min1", "max1", "min2", "max2", "te1_deliverable", "te2_in_deliverable",
+                               "te2_isDeliverable"], "cases": tq["cases"]}, f)

@@ -1,0 +1,68 @@
+"""The CPU oracle against the reference's own numbers (pinned) and the committed fixtures."""
+import json
+import os
+
+import pytest
+
+import oracle_util
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+LAB0 = _load("lab0.json")
+SIP = _load("sipaxos.json")
+
+
+@pytest.mark.parametrize("name", sorted(LAB0))
+def test_lab0_oracle_matches_fixture_and_pins(name):
+    case = LAB0[name]
+    r = oracle_util.run("bfs", case["args"], timeout=300)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
+    assert r["states"] == case["states"] and r["max_depth"] == case["max_depth"]
+    pin = case["pinned"]
+    for k in ("states", "max_depth", "per_depth", "end"):
+        if k in pin:
+            assert {"states": r["states"], "max_depth": r["max_depth"], "per_depth": r["per_depth"],
+                    "end": r["end"]}[k] == pin[k], (k, pin["source"])
+    if "terminal_depth" in pin:
+        assert r["terminals"][0]["depth"] == pin["terminal_depth"]
+    if "trace" in pin:
+        assert r["terminals"][0]["trace"] == pin["trace"]
+    if "detail" in pin:
+        assert r["terminals"][0]["detail"] == pin["detail"]
+
+
+@pytest.mark.parametrize("name", ["sipaxos_2p3a_d6", "sipaxos_3p3a_d6", "sipaxos_2p3a_d9"])
+def test_sipaxos_oracle(name):
+    case = SIP[name]
+    r = oracle_util.run("bfs", case["args"], timeout=300)
+    assert r["per_depth"] == case["per_depth"]
+    if "per_depth" in case["pinned"]:
+        assert r["per_depth"] == case["pinned"]["per_depth"]
+
+
+def test_timerqueue_truth_table():
+    """TimerQueueTest.randomTimers: te1 always deliverable; te2 deliverable iff te2.min < te1.max."""
+    tq = _load("timerqueue.json")
+    r = oracle_util.run("timerqueue", [])
+    assert r["cases"] == tq["cases"]
+    assert len(r["cases"]) == 100
+    for i, j, k, l, d1, d2l, d2i in r["cases"]:
+        assert d1 == 1
+        expect = 1 if k < j else 0
+        assert d2l == expect and d2i == expect
+
+
+def test_oracle_replay_readme_trace():
+    """The README's mutant trace replays on the oracle and ends in the RESULTS_OK violation."""
+    case = LAB0["lab0_mutant_nocheck"]
+    args = [a for a in case["args"] if a != "--finish-level"]
+    r = oracle_util.replay(args, case["pinned"]["trace"])
+    assert r["ok"] and r["depth"] == 3
+    assert r["invariants"][0]["value"] is False
