@@ -6,7 +6,7 @@
 #include <string>
 
 #include "engine.hpp"
-#include "protocols/pingpong.hpp"
+#include "protocols/all.hpp"
 
 namespace dsl {
 
@@ -82,6 +82,7 @@ static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg,
 static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, EngineBase** out) {
   switch (d.protocol) {
     case DSL_PROTO_PINGPONG: return make_engine<PingPong>(d, cfg, out);
+    case DSL_PROTO_SIPAXOS: return make_engine<SIPaxos>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -110,6 +111,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
   if (!proto) return DSL_ERR_ARG;
   switch (proto->protocol) {
     case DSL_PROTO_PINGPONG: return (int)sizeof(dsl::PingPong::State);
+    case DSL_PROTO_SIPAXOS: return (int)sizeof(dsl::SIPaxos::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }

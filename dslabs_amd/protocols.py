@@ -78,3 +78,41 @@ class PingPong(Protocol):
 def pingpong_state(clients: int = 1, pings: int = 10, **kw) -> SearchState:
     """initSearchState.addServer(sa); addClientWorker(client(i), repeatedPings(pings)) for i."""
     return PingPong(clients, pings, **kw).initial_state()
+
+
+class SIPaxos(Protocol):
+    """Single-instance Paxos Made Simple (SingleInstancePaxos.java:50-127): proposers
+    "proposer1..P" with initial values, acceptors "acceptor1..A"."""
+
+    proto_id = DSL_PROTO_SIPAXOS
+    PREDICATES = {"Agreement": 100, "Integrity": 101, "Termination": 102}
+
+    def __init__(self, proposers: int = 2, acceptors: int = 3, values=("a", "b"), incorrect: bool = False):
+        assert len(values) == proposers
+        self.proposers = proposers
+        self.acceptors = acceptors
+        self.values = list(values)
+        self.incorrect = incorrect
+        self.addresses = [f"proposer{i}" for i in range(1, proposers + 1)] + \
+                         [f"acceptor{i}" for i in range(1, acceptors + 1)]
+
+    def params(self):
+        return [self.proposers, self.acceptors, int(self.incorrect)]
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        return StatePredicate(name, self.PREDICATES[name])
+
+    def render_event(self, e) -> str:
+        if e.is_timer:
+            return f"Timer(-> {self.addresses[e.to]}, Propose())"
+        n, an, av = e.fields[0], e.fields[1], e.fields[2]
+        if e.type == 0:
+            body = f"Prepare({n})"
+        elif e.type == 1:
+            body = f"PrepareAck({n}, null, )" if an == 0 else f"PrepareAck({n}, {an}, {self.values[av - 1]})"
+        elif e.type == 2:
+            body = f"Accept({n}, {self.values[av - 1]})"
+        else:
+            body = f"AcceptAck({n})"
+        return f"Message({self.addresses[e.from_]} -> {self.addresses[e.to]}, {body})"

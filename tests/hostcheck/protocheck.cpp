@@ -1,0 +1,138 @@
+// tests/hostcheck/protocheck.cpp -- TEST TOOL, not part of the product.
+//
+// Runs a protocol's packed-state transition functions (the same __host__ __device__ code the
+// HIP kernels execute) in a plain host BFS with EXACT state equality (no fingerprints), so a
+// protocol encoding can be checked against the oracle's per-depth vectors on a machine with no
+// GPU. It never stands in for the engine: the Search API only runs libdslabs_hip.so kernels.
+//
+// usage: protocheck <proto> <params...> -- <inv ids> / <goal ids> / <prune ids> maxdepth
+//   e.g. protocheck 1 1 10 1 1 -- 1 / / 2 -1
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../dslabs_amd/csrc/common.hpp"
+#include "../../dslabs_amd/csrc/protocols/all.hpp"
+
+using namespace dsl;
+
+template <class P>
+static int run(const dsl_protocol_desc& d, DevSettings set) {
+  typename P::Params prm = P::from_desc(d);
+  if (!P::valid(prm)) {
+    printf("{\"error\":\"invalid params\"}\n");
+    return 1;
+  }
+  using S = typename P::State;
+  struct Node {
+    S s;
+    int depth;
+  };
+  auto key = [](const S& s) { return std::string((const char*)s.w, sizeof(S)); };
+  S init;
+  P::init(init, prm);
+  std::unordered_set<std::string> seen;
+  std::deque<Node> q;
+  std::vector<unsigned long long> per;
+  seen.insert(key(init));
+  per.push_back(1);
+  int pi = -1;
+  int v0 = judge<P>(init, prm, set, 0, &pi);
+  const char* end = "SPACE_EXHAUSTED";
+  int tdepth = -1;
+  if (v0 >= V_TERM_EXCEPTION) {
+    end = v0 == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
+    tdepth = 0;
+  } else {
+    q.push_back({init, 0});
+  }
+  int best = 99;
+  while (!q.empty()) {
+    Node n = q.front();
+    if (tdepth >= 0 && n.depth + 1 > tdepth) break;
+    q.pop_front();
+    int ne = P::num_events(n.s, prm, set);
+    for (int k = 0; k < ne; k++) {
+      S t;
+      int rc = P::step(n.s, k, t, prm, set);
+      if (rc == STEP_NULL) continue;
+      if (rc == STEP_OVERFLOW) {
+        printf("{\"error\":\"overflow\"}\n");
+        return 1;
+      }
+      int d = n.depth + 1;
+      if (rc == STEP_EXCEPTION) {
+        if ((int)per.size() <= d) per.resize(d + 1, 0);
+        per[d]++;
+        if (tdepth < 0) tdepth = d;
+        best = std::min(best, (int)V_TERM_EXCEPTION);
+        continue;
+      }
+      if (!seen.insert(key(t)).second) continue;
+      if ((int)per.size() <= d) per.resize(d + 1, 0);
+      per[d]++;
+      int v = judge<P>(t, prm, set, d, &pi);
+      if (v >= V_TERM_EXCEPTION) {
+        if (tdepth < 0) tdepth = d;
+        best = std::min(best, v);
+        continue;
+      }
+      if (v == V_PRUNED) continue;
+      q.push_back({t, d});
+    }
+  }
+  if (best != 99)
+    end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
+  unsigned long long total = 0;
+  printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"per_depth\":[", end, tdepth, (int)sizeof(S));
+  for (size_t i = 0; i < per.size(); i++) {
+    printf("%s%llu", i ? "," : "", per[i]);
+    total += per[i];
+  }
+  printf("],\"states\":%llu}\n", total);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  dsl_protocol_desc d{};
+  int i = 1;
+  d.protocol = atoi(argv[i++]);
+  while (i < argc && strcmp(argv[i], "--") != 0) d.params[d.n_params++] = atoll(argv[i++]);
+  i++;
+  DevSettings set{};
+  for (int a = 0; a < DSL_MAX_NODES; a++) set.deliver[a] = 0xffffffffu;
+  set.timer_mask = 0xffffffffu;
+  DevPred* lists[3] = {set.inv, set.goal, set.prune};
+  int* counts[3] = {&set.n_inv, &set.n_goal, &set.n_prune};
+  int which = 0;
+  for (; i < argc - 1; i++) {
+    if (strcmp(argv[i], "/") == 0) {
+      which++;
+      continue;
+    }
+    int id = atoi(argv[i]);
+    DevPred p{};
+    p.negate = id < 0;
+    p.id = id < 0 ? -id : id;
+    lists[which][(*counts[which])++] = p;
+  }
+  set.max_depth = atoi(argv[argc - 1]);
+  switch (d.protocol) {
+    case DSL_PROTO_PINGPONG: return run<PingPong>(d, set);
+    case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, set);
+#ifdef DSL_HAVE_SYNTHETIC
+    case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
+#endif
+#ifdef DSL_HAVE_AMOKV
+    case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
+#endif
+#ifdef DSL_HAVE_MULTIPAXOS
+    case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, set);
+#endif
+  }
+  return 2;
+}

@@ -1,0 +1,69 @@
+"""Protocol ENCODINGS (packed-state transition functions, host-compiled) vs the oracle.
+
+This checks the device protocols' semantics on CPU; the kernels themselves are checked by the
+-m gpu tests. tests/hostcheck/protocheck.cpp is a test tool, never part of the product."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import oracle_util
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "hostcheck", "protocheck.cpp")
+BIN = os.path.join(ROOT, "tests", "hostcheck", "_build", "protocheck")
+
+
+@pytest.fixture(scope="module")
+def protocheck():
+    os.makedirs(os.path.dirname(BIN), exist_ok=True)
+    deps = [SRC] + [os.path.join(dp, f) for dp, _, fs in os.walk(os.path.join(ROOT, "dslabs_amd", "csrc"))
+                    for f in fs]
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(d) for d in deps):
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-Wno-unused-result", "-o", BIN, SRC],
+                       check=True)
+    return BIN
+
+
+def run(bin_, args):
+    out = subprocess.run([bin_] + [str(a) for a in args], check=True, capture_output=True, text=True, timeout=600)
+    return json.loads(out.stdout)
+
+
+# (protocheck args, oracle args)
+CASES = {
+    "pp_1c10p": ([1, 1, 10, 1, 1, "--", 1, "/", "/", 2, -1],
+                 ["--proto", "pingpong", "--clients", "1", "--pings", "10", "--inv", "RESULTS_OK", "--prune",
+                  "CLIENTS_DONE"]),
+    "pp_3c3p": ([1, 3, 3, 1, 1, "--", 1, "/", "/", 2, -1],
+                ["--proto", "pingpong", "--clients", "3", "--pings", "3", "--inv", "RESULTS_OK", "--prune",
+                 "CLIENTS_DONE"]),
+    "pp_mutant_noreset": ([1, 2, 3, 1, 0, "--", 1, "/", "/", 2, -1],
+                          ["--proto", "pingpong", "--clients", "2", "--pings", "3", "--inv", "RESULTS_OK",
+                           "--prune", "CLIENTS_DONE", "--mutant-no-reset"]),
+    "pp_mutant_nocheck": ([1, 1, 10, 0, 1, "--", 1, "/", 2, "/", -1],
+                          ["--proto", "pingpong", "--clients", "1", "--pings", "10", "--inv", "RESULTS_OK",
+                           "--goal", "CLIENTS_DONE", "--mutant-no-check", "--finish-level"]),
+    "sip_2p3a_d7": ([2, 2, 3, 0, "--", 101, 100, "/", "/", 7],
+                    ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
+                     "Integrity", "--inv", "Agreement", "--max-depth", "7"]),
+    "sip_3p3a_d6": ([2, 3, 3, 0, "--", 101, 100, "/", "/", 6],
+                    ["--proto", "sipaxos", "--proposers", "3", "--acceptors", "3", "--values", "a,b,c", "--inv",
+                     "Integrity", "--inv", "Agreement", "--max-depth", "6"]),
+    "sip_incorrect_2p3a_d9": ([2, 2, 3, 1, "--", 101, 100, "/", "/", 9],
+                              ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b",
+                               "--inv", "Integrity", "--inv", "Agreement", "--incorrect", "--max-depth", "9"]),
+    "sip_2p5a_d6": ([2, 2, 5, 0, "--", 101, 100, "/", "/", 6],
+                    ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "5", "--values", "a,b", "--inv",
+                     "Integrity", "--inv", "Agreement", "--max-depth", "6"]),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_encoding_matches_oracle(protocheck, name):
+    pargs, oargs = CASES[name]
+    got = run(protocheck, pargs)
+    want = oracle_util.run("bfs", oargs, timeout=600)
+    assert got["end"] == want["end"]
+    assert got["per_depth"] == want["per_depth"]
