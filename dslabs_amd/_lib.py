@@ -84,6 +84,14 @@ class dsl_result(ctypes.Structure):
     ]
 
 
+class dsl_stats(ctypes.Structure):
+    _fields_ = [("expand_ms", ctypes.c_double), ("count_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
+                ("expand_launches", ctypes.c_uint64), ("parents", ctypes.c_uint64),
+                ("work_items", ctypes.c_uint64), ("new_states", ctypes.c_uint64), ("appended", ctypes.c_uint64),
+                ("exchanged", ctypes.c_uint64), ("state_bytes", ctypes.c_uint32), ("world_size", ctypes.c_uint32),
+                ("table_slots", ctypes.c_uint64)]
+
+
 _lib = None
 
 
@@ -108,7 +116,7 @@ def load() -> ctypes.CDLL:
     lib.dsl_get_initial.argtypes = [ctypes.c_void_p, P(ctypes.c_uint8), ctypes.c_size_t]
     lib.dsl_run.argtypes = [ctypes.c_void_p, P(P(dsl_result))]
     lib.dsl_progress.argtypes = [ctypes.c_void_p, P(ctypes.c_uint64), P(ctypes.c_int32)]
-    lib.dsl_kernel_stats.argtypes = [ctypes.c_void_p, P(ctypes.c_double), P(ctypes.c_uint64), P(ctypes.c_uint64)]
+    lib.dsl_kernel_stats.argtypes = [ctypes.c_void_p, P(dsl_stats)]
     lib.dsl_result_free.argtypes = [P(dsl_result)]
     lib.dsl_result_free.restype = None
     lib.dsl_destroy.argtypes = [ctypes.c_void_p]

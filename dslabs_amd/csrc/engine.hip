@@ -169,11 +169,9 @@ int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth) {
   return DSL_OK;
 }
 
-int dsl_kernel_stats(dsl_engine* e, double* expand_ms_total, uint64_t* expand_launches, uint64_t* work_items) {
-  if (!e) return DSL_ERR_ARG;
-  if (expand_ms_total) *expand_ms_total = e->impl->expand_ms_total;
-  if (expand_launches) *expand_launches = e->impl->expand_launches;
-  if (work_items) *work_items = e->impl->work_items;
+int dsl_kernel_stats(dsl_engine* e, dsl_stats* out) {
+  if (!e || !out) return DSL_ERR_ARG;
+  *out = e->impl->stats;
   return DSL_OK;
 }
 

@@ -206,9 +206,7 @@ struct EngineBase {
   virtual int state_bytes() const = 0;
   volatile unsigned long long progress_states = 0;
   volatile int progress_depth = 0;
-  double expand_ms_total = 0;
-  uint64_t expand_launches = 0;
-  uint64_t work_items = 0;
+  dsl_stats stats{};
 };
 
 int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)(int), DevSettings* out);
@@ -224,7 +222,7 @@ struct Engine : EngineBase {
   int init_depth = 0;
   bool have_init = false;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evc0 = nullptr, evc1 = nullptr;
 
   // device memory
   unsigned long long* d_table = nullptr;
@@ -274,6 +272,8 @@ struct Engine : EngineBase {
     hipFree(d_seed);
     if (ev0) hipEventDestroy(ev0);
     if (ev1) hipEventDestroy(ev1);
+    if (evc0) hipEventDestroy(evc0);
+    if (evc1) hipEventDestroy(evc1);
     if (stream) hipStreamDestroy(stream);
     d_table = nullptr;
     d_cur = d_next = nullptr;
@@ -285,7 +285,7 @@ struct Engine : EngineBase {
     d_terms = nullptr;
     d_seed = nullptr;
     stream = nullptr;
-    ev0 = ev1 = nullptr;
+    ev0 = ev1 = evc0 = evc1 = nullptr;
   }
 
   int state_bytes() const override { return (int)sizeof(State); }
@@ -321,6 +321,8 @@ struct Engine : EngineBase {
       DSL_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
       DSL_HIP(hipEventCreate(&ev0));
       DSL_HIP(hipEventCreate(&ev1));
+      DSL_HIP(hipEventCreate(&evc0));
+      DSL_HIP(hipEventCreate(&evc1));
     }
     return DSL_OK;
   }
@@ -358,6 +360,9 @@ struct Engine : EngineBase {
     int rc = ensure_stream();
     if (rc) return rc;
     auto t_start = std::chrono::steady_clock::now();
+    stats = dsl_stats{};
+    stats.state_bytes = sizeof(State);
+    stats.world_size = 1;
     if (!have_init) {
       uint8_t tmp[sizeof(State)];
       get_initial(tmp, sizeof(State));
@@ -371,6 +376,7 @@ struct Engine : EngineBase {
     if ((rc = grow(&d_hist_parent, &hist_parent_cap, 1024, false, 0))) return rc;
     if ((rc = grow(&d_hist_event, &hist_event_cap, 1024, false, 0))) return rc;
     Table table{d_table, table_buckets - 1, 64};
+    stats.table_slots = table_buckets * 8;
 
     DSL_HIP(hipMemcpyAsync(d_cur, &init, sizeof(State), hipMemcpyHostToDevice, stream));
     hipLaunchKernelGGL(k_seed<P>, dim3(1), dim3(64), 0, stream, d_cur, prm, dset, table, init_depth, d_seed);
@@ -415,6 +421,7 @@ struct Engine : EngineBase {
         if ((rc = grow(&d_counts, &counts_cap, F, false, 0))) return rc;
         if ((rc = grow(&d_offsets, &offsets_cap, F, false, 0))) return rc;
         const int cblocks = (int)std::min<uint64_t>((F + kBlock - 1) / kBlock, 8192);
+        DSL_HIP(hipEventRecord(evc0, stream));
         hipLaunchKernelGGL(k_count<P>, dim3(cblocks), dim3(kBlock), 0, stream, d_cur, F, prm, dset, d_counts);
         // 2. exclusive scan
         size_t need = 0;
@@ -426,6 +433,7 @@ struct Engine : EngineBase {
           scan_tmp_bytes = need;
         }
         DSL_HIP(scan(F));
+        DSL_HIP(hipEventRecord(evc1, stream));
         unsigned long long last[2];
         DSL_HIP(hipMemcpyAsync(&last[0], d_offsets + F - 1, 8, hipMemcpyDeviceToHost, stream));
         DSL_HIP(hipMemcpyAsync(&last[1], d_counts + F - 1, 8, hipMemcpyDeviceToHost, stream));
@@ -463,11 +471,16 @@ struct Engine : EngineBase {
         LevelCounters ctr;
         DSL_HIP(hipMemcpyAsync(&ctr, d_ctr, sizeof(ctr), hipMemcpyDeviceToHost, stream));
         DSL_HIP(hipStreamSynchronize(stream));
-        float kms = 0;
+        float kms = 0, cms = 0;
         hipEventElapsedTime(&kms, ev0, ev1);
-        expand_ms_total += kms;
-        expand_launches++;
-        work_items += total;
+        hipEventElapsedTime(&cms, evc0, evc1);
+        stats.expand_ms += kms;
+        stats.scan_ms += cms;
+        stats.expand_launches++;
+        stats.parents += F;
+        stats.work_items += total;
+        stats.new_states += ctr.new_states;
+        stats.appended += ctr.next_size;
         if (ctr.err_overflow) {
           set_error("a successor exceeded the packed state's bounds (" + std::to_string(ctr.err_overflow) + " times)");
           return DSL_ERR_STATE_OVERFLOW;

@@ -363,13 +363,10 @@ class Engine:
         check(self.lib.dsl_get_initial(self.handle, buf, n), "dsl_get_initial")
         return bytes(buf)
 
-    def kernel_stats(self):
-        ms = ctypes.c_double()
-        launches = ctypes.c_uint64()
-        items = ctypes.c_uint64()
-        check(self.lib.dsl_kernel_stats(self.handle, ctypes.byref(ms), ctypes.byref(launches), ctypes.byref(items)),
-              "dsl_kernel_stats")
-        return ms.value, launches.value, items.value
+    def kernel_stats(self) -> dict:
+        st = _lib.dsl_stats()
+        check(self.lib.dsl_kernel_stats(self.handle, ctypes.byref(st)), "dsl_kernel_stats")
+        return {name: getattr(st, name) for name, _ in st._fields_}
 
     def bfs(self, state: SearchState, settings: Optional[SearchSettings] = None) -> SearchResults:
         if settings is None:

@@ -118,7 +118,7 @@ typedef struct {
   dsl_predicate goals[DSL_MAX_PREDICATES];
   dsl_predicate prunes[DSL_MAX_PREDICATES];
   /* engine capacity knobs (0 = automatic) */
-  int32_t table_log2_slots; /* visited table = 2^k 16-byte slots (per shard) */
+  int32_t table_log2_slots; /* visited table = 2^k 8-byte slots (per shard) */
   int32_t reserved0;
   uint64_t max_frontier_states;
   uint64_t memory_budget_bytes;
@@ -174,8 +174,25 @@ int dsl_set_initial(dsl_engine* e, const uint8_t* packed, size_t len, int32_t de
 int dsl_get_initial(dsl_engine* e, uint8_t* packed, size_t len);
 int dsl_run(dsl_engine* e, dsl_result** out);
 int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth);
-int dsl_kernel_stats(dsl_engine* e, double* expand_ms_total, uint64_t* expand_launches,
-                     uint64_t* work_items);
+/* Cumulative kernel statistics of the last dsl_run (HIP events on the engine's stream). The
+ * byte model of the expand kernel: parents read once (S bytes each), one 64-byte
+ * visited-table bucket line per successor probe, one bucket line written back + 12 bytes of
+ * parent/event per newly discovered state, S bytes per successor appended to the next frontier. */
+typedef struct {
+  double expand_ms;          /* sum of k_expand durations */
+  double count_ms, scan_ms;  /* sum of k_count / scan durations */
+  uint64_t expand_launches;
+  uint64_t parents;          /* frontier states expanded */
+  uint64_t work_items;       /* (state, event) pairs = successors generated */
+  uint64_t new_states;       /* newly discovered successors */
+  uint64_t appended;         /* VALID successors written to the next frontier */
+  uint64_t exchanged;        /* successors routed to another shard */
+  uint32_t state_bytes;
+  uint32_t world_size;
+  uint64_t table_slots;
+} dsl_stats;
+
+int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);
 void dsl_result_free(dsl_result* r);
 void dsl_destroy(dsl_engine* e);
 const char* dsl_last_error(void);
