@@ -1,0 +1,169 @@
+"""bench.py -- unique states explored / sec of the MI355X BFS engine (BASELINE.json metric).
+
+A "step" is one complete BFS over the workload (Search.bfs from the initial state to the end
+condition), timed with the search resident on the GPU; value = unique states (reference
+counting rule, Search.java:470-490) x steps / wall time, whole job.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME] [--depth D]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N ...
+
+Multi-GPU: one process per GPU; the visited set and frontier are hash-partitioned by
+fingerprint, successors routed to their owner shard per level (RCCL all-to-all over xGMI).
+Per-depth counts are shard-count invariant; `value` = global unique states / max-rank time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # The reference's own Paxos ("Paxos Made Simple", SingleInstancePaxos.java:50-127): 2
+    # proposers, 3 acceptors, invariants Integrity + Agreement, exhaustive to maxDepth.
+    "sipaxos": dict(depth=15, cpu_depth=10,
+                    desc="reference SingleInstancePaxos (2 proposers, 3 acceptors), invariants "
+                         "Integrity+Agreement, BFS to maxDepth"),
+}
+
+
+def build_search(name: str, depth: int):
+    from dslabs_amd import SearchSettings
+    from dslabs_amd.protocols import SIPaxos
+    if name == "sipaxos":
+        proto = SIPaxos(2, 3, ("a", "b"))
+        s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
+        s.maxDepth(depth)
+        s.table_log2_slots = 28
+        return proto, s, ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b",
+                          "--inv", "Integrity", "--inv", "Agreement"]
+    raise SystemExit(f"unknown workload {name}")
+
+
+def cpu_baseline(oracle_args, depth: int) -> dict:
+    """The CPU oracle (a scalar C++ restatement of the reference BFS, oracle/) on the GPU box's
+    host, one thread, on a bounded sample of the same workload (smaller maxDepth)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    exe = os.path.join(ROOT, "oracle", "_build", "dslabs_oracle")
+    out = subprocess.run([exe, "bfs"] + oracle_args + ["--max-depth", str(depth)], check=True,
+                         capture_output=True, text=True, timeout=300)
+    r = json.loads(out.stdout)
+    return {"value": r["states"] / r["elapsed_s"], "unit": "states/s", "cores": 1, "kind": "port",
+            "sample": f"same workload, maxDepth {depth} ({r['states']} states, {r['elapsed_s']:.2f} s, "
+                      f"oracle/dslabs_oracle single-threaded)"}
+
+
+def roofline(stats: dict) -> dict:
+    """Algorithmic bytes of k_expand per launch (SURVEY.md §8d byte model):
+    parents read once (S B), one 64-B bucket line probed per successor, one bucket line written
+    back + 12 B parent/event per new state, S B per successor appended to the next frontier."""
+    S = stats["state_bytes"]
+    alg = stats["parents"] * S + stats["work_items"] * 64 + stats["new_states"] * (64 + 12) + stats["appended"] * S
+    t = stats["expand_ms"] / 1e3
+    achieved = alg / t / 1e9 if t > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_expand", "launches": stats["expand_launches"],
+            "avg_launch_ms": round(stats["expand_ms"] / max(1, stats["expand_launches"]), 4),
+            "alg_bytes_per_launch": int(alg / max(1, stats["expand_launches"]))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="sipaxos")
+    ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dist = None
+    comm_id = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        from dslabs_amd import _lib
+        lib = _lib.load()
+        import ctypes
+        buf = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            _lib.check(lib.dsl_comm_unique_id(buf), "dsl_comm_unique_id")
+        obj = [bytes(buf)]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+
+    from dslabs_amd import Engine
+    wl = WORKLOADS[args.workload]
+    depth = args.depth if args.depth is not None else wl["depth"]
+    proto, settings, oracle_args = build_search(args.workload, depth)
+    eng = Engine(proto, device=local_rank, rank=rank, world_size=world, comm_id=comm_id)
+    state = proto.initial_state()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.bfs(state, settings)
+    barrier()
+    t0 = time.perf_counter()
+    total_states = 0
+    res = None
+    for _ in range(args.steps):
+        res = eng.bfs(state, settings)
+        total_states += res.states
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = eng.kernel_stats()
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(total_states / elapsed, 1),
+            "unit": "states/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (model-checking state space generated from the protocol's initial state)",
+            "config": {"workload": args.workload, "description": wl["desc"], "max_depth": depth,
+                       "unique_states_per_step": res.states, "per_depth": res.per_depth,
+                       "end_condition": res.endCondition().name, "state_bytes": stats["state_bytes"],
+                       "successors_per_step": res.successors, "parallelism": f"hash-sharded x{world}"},
+            "roofline": roofline(stats),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(oracle_args, wl["cpu_depth"])
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
