@@ -28,7 +28,7 @@ STATUS_NAMES = {
 EXPORTED = [
     "dsl_abi_version", "dsl_device_count", "dsl_state_bytes", "dsl_comm_unique_id", "dsl_create",
     "dsl_set_settings", "dsl_set_initial", "dsl_get_initial", "dsl_run", "dsl_progress",
-    "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error",
+    "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
 ]
 
 
@@ -117,6 +117,8 @@ def load() -> ctypes.CDLL:
     lib.dsl_run.argtypes = [ctypes.c_void_p, P(P(dsl_result))]
     lib.dsl_progress.argtypes = [ctypes.c_void_p, P(ctypes.c_uint64), P(ctypes.c_int32)]
     lib.dsl_kernel_stats.argtypes = [ctypes.c_void_p, P(dsl_stats)]
+    lib.dsl_create_with_host_comm.argtypes = [P(dsl_protocol_desc), P(dsl_engine_config), ctypes.c_void_p,
+                                              P(ctypes.c_void_p)]
     lib.dsl_result_free.argtypes = [P(dsl_result)]
     lib.dsl_result_free.restype = None
     lib.dsl_destroy.argtypes = [ctypes.c_void_p]

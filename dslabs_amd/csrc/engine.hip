@@ -7,8 +7,163 @@
 
 #include "engine.hpp"
 #include "protocols/all.hpp"
+#include "sharded_engine.hpp"
+
+#ifdef DSL_WITH_RCCL
+#include <rccl/rccl.h>
+#endif
 
 namespace dsl {
+
+#ifdef DSL_WITH_RCCL
+// One communicator per engine (one rank per GPU). Small host-visible collectives are staged
+// through a device scratch buffer on the engine's stream.
+struct RcclComm : Comm {
+  ncclComm_t c = nullptr;
+  int r = 0, n = 1;
+  uint64_t* dbuf = nullptr;  // 2 * (kMaxShards * 64) u64
+  static constexpr int kScratch = 2 * kMaxShards * 64;
+  ~RcclComm() override {
+    if (c) ncclCommDestroy(c);
+    hipFree(dbuf);
+  }
+  int rank() const override { return r; }
+  int size() const override { return n; }
+  static int ck(ncclResult_t e, const char* what) {
+    if (e != ncclSuccess) {
+      set_error(std::string("RCCL ") + what + ": " + ncclGetErrorString(e));
+      return DSL_ERR_COMM;
+    }
+    return DSL_OK;
+  }
+  int allgather_u64(const uint64_t* in, int k, uint64_t* out, hipStream_t st) override {
+    if (k * (n + 1) > kScratch) return DSL_ERR_ARG;
+    DSL_HIP(hipMemcpyAsync(dbuf, in, k * 8, hipMemcpyHostToDevice, st));
+    int rc = ck(ncclAllGather(dbuf, dbuf + k, k, ncclUint64, c, st), "allgather");
+    if (rc) return rc;
+    DSL_HIP(hipMemcpyAsync(out, dbuf + k, (size_t)k * n * 8, hipMemcpyDeviceToHost, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    return DSL_OK;
+  }
+  int allreduce_u64(uint64_t* v, int k, bool min, hipStream_t st) override {
+    if (k > kScratch) return DSL_ERR_ARG;
+    DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
+    int rc = ck(ncclAllReduce(dbuf, dbuf, k, ncclUint64, min ? ncclMin : ncclSum, c, st), "allreduce");
+    if (rc) return rc;
+    DSL_HIP(hipMemcpyAsync(v, dbuf, k * 8, hipMemcpyDeviceToHost, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    return DSL_OK;
+  }
+  int bcast_u64(uint64_t* v, int k, int root, hipStream_t st) override {
+    if (k > kScratch) return DSL_ERR_ARG;
+    DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
+    int rc = ck(ncclBroadcast(dbuf, dbuf, k, ncclUint64, root, c, st), "broadcast");
+    if (rc) return rc;
+    DSL_HIP(hipMemcpyAsync(v, dbuf, k * 8, hipMemcpyDeviceToHost, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    return DSL_OK;
+  }
+  int alltoallv(const uint8_t* send, const uint64_t* so, const uint64_t* sb, uint8_t* recv, const uint64_t* ro,
+                const uint64_t* rb, hipStream_t st) override {
+    int rc = ck(ncclGroupStart(), "group start");
+    if (rc) return rc;
+    for (int p = 0; p < n; p++) {
+      if (p == r) continue;
+      if (sb[p]) {
+        rc = ck(ncclSend(send + so[p], sb[p], ncclUint8, p, c, st), "send");
+        if (rc) break;
+      }
+      if (rb[p]) {
+        rc = ck(ncclRecv(recv + ro[p], rb[p], ncclUint8, p, c, st), "recv");
+        if (rc) break;
+      }
+    }
+    int rc2 = ck(ncclGroupEnd(), "group end");
+    return rc ? rc : rc2;
+  }
+};
+
+static int make_comm(const dsl_engine_config& cfg, Comm** out) {
+  auto* cm = new RcclComm();
+  cm->r = cfg.rank;
+  cm->n = cfg.world_size;
+  if (cfg.device >= 0) {
+    hipError_t e = hipSetDevice(cfg.device);
+    if (e != hipSuccess) {
+      delete cm;
+      set_error("hipSetDevice failed");
+      return DSL_ERR_HIP;
+    }
+  }
+  if (hipMalloc(&cm->dbuf, RcclComm::kScratch * 8) != hipSuccess) {
+    delete cm;
+    set_error("hipMalloc failed");
+    return DSL_ERR_HIP;
+  }
+  ncclUniqueId id;
+  std::memcpy(&id, cfg.comm_id, sizeof(id));
+  int rc = RcclComm::ck(ncclCommInitRank(&cm->c, cfg.world_size, id, cfg.rank), "comm init");
+  if (rc) {
+    delete cm;
+    return rc;
+  }
+  *out = cm;
+  return DSL_OK;
+}
+#else
+static int make_comm(const dsl_engine_config&, Comm**) {
+  set_error("built without RCCL: multi-GPU unavailable");
+  return DSL_ERR_COMM;
+}
+#endif
+
+// Transport provided by the caller through dsl_host_comm (host buffers).
+struct HostComm : Comm {
+  dsl_host_comm h;
+  std::vector<uint8_t> sbuf, rbuf;
+  explicit HostComm(const dsl_host_comm& x) : h(x) {}
+  int rank() const override { return h.rank; }
+  int size() const override { return h.size; }
+  int allgather_u64(const uint64_t* in, int n, uint64_t* out, hipStream_t) override {
+    return h.allgather_u64(h.ctx, in, n, out) ? DSL_ERR_COMM : DSL_OK;
+  }
+  int allreduce_u64(uint64_t* v, int n, bool min, hipStream_t) override {
+    return h.allreduce_u64(h.ctx, v, n, min ? 1 : 0) ? DSL_ERR_COMM : DSL_OK;
+  }
+  int bcast_u64(uint64_t* v, int n, int root, hipStream_t) override {
+    return h.bcast_u64(h.ctx, v, n, root) ? DSL_ERR_COMM : DSL_OK;
+  }
+  int alltoallv(const uint8_t* send, const uint64_t* so, const uint64_t* sb, uint8_t* recv, const uint64_t* ro,
+                const uint64_t* rb, hipStream_t st) override {
+    const int n = h.size;
+    std::vector<uint64_t> hso(n), hro(n);
+    uint64_t stot = 0, rtot = 0;
+    for (int p = 0; p < n; p++) {
+      hso[p] = stot;
+      stot += sb[p];
+      hro[p] = rtot;
+      rtot += rb[p];
+    }
+    sbuf.resize(stot + 1);
+    rbuf.resize(rtot + 1);
+    for (int p = 0; p < n; p++)
+      if (sb[p]) DSL_HIP(hipMemcpyAsync(sbuf.data() + hso[p], send + so[p], sb[p], hipMemcpyDeviceToHost, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    if (h.alltoallv(h.ctx, sbuf.data(), hso.data(), sb, rbuf.data(), hro.data(), rb)) return DSL_ERR_COMM;
+    for (int p = 0; p < n; p++)
+      if (rb[p]) DSL_HIP(hipMemcpyAsync(recv + ro[p], rbuf.data() + hro[p], rb[p], hipMemcpyHostToDevice, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    return DSL_OK;
+  }
+};
+
+static thread_local const dsl_host_comm* g_pending_host_comm = nullptr;
+
+template <class P>
+hipError_t ShardedEngine<P>::hipcub_scan(void* tmp, size_t& bytes, unsigned long long* in, unsigned long long* out,
+                                         uint64_t n) {
+  return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, n, stream);
+}
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
@@ -75,7 +230,22 @@ static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg,
     set_error("invalid protocol parameters");
     return DSL_ERR_ARG;
   }
-  *out = new Engine<P>(prm, cfg);
+  if (cfg.world_size > 1) {
+    if (cfg.world_size > kMaxShards || cfg.rank < 0 || cfg.rank >= cfg.world_size) return DSL_ERR_ARG;
+    Comm* cm = nullptr;
+    if (g_pending_host_comm) {
+      cm = new HostComm(*g_pending_host_comm);
+    } else {
+      int rc = make_comm(cfg, &cm);
+      if (rc) return rc;
+    }
+    *out = new ShardedEngine<P>(prm, cfg, cfg.world_size, cm);
+  } else if (cfg.virtual_shards > 1) {
+    if (cfg.virtual_shards > kMaxShards) return DSL_ERR_ARG;
+    *out = new ShardedEngine<P>(prm, cfg, cfg.virtual_shards, nullptr);
+  } else {
+    *out = new Engine<P>(prm, cfg);
+  }
   return DSL_OK;
 }
 
@@ -117,9 +287,19 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
 }
 
 int dsl_comm_unique_id(uint8_t out[128]) {
-  (void)out;
-  dsl::set_error("multi-GPU communicator not built in this library version");
+  if (!out) return DSL_ERR_ARG;
+#ifdef DSL_WITH_RCCL
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) {
+    dsl::set_error("ncclGetUniqueId failed");
+    return DSL_ERR_COMM;
+  }
+  std::memcpy(out, &id, sizeof(id));
+  return DSL_OK;
+#else
+  dsl::set_error("built without RCCL");
   return DSL_ERR_COMM;
+#endif
 }
 
 int dsl_create(const dsl_protocol_desc* proto, const dsl_engine_config* cfg, dsl_engine** out) {
@@ -139,6 +319,17 @@ int dsl_create(const dsl_protocol_desc* proto, const dsl_engine_config* cfg, dsl
   if (rc) return rc;
   *out = new dsl_engine{impl};
   return DSL_OK;
+}
+
+int dsl_create_with_host_comm(const dsl_protocol_desc* proto, const dsl_engine_config* cfg,
+                              const dsl_host_comm* comm, dsl_engine** out) {
+  if (!proto || !cfg || !comm || !out || comm->size != cfg->world_size || comm->rank != cfg->rank ||
+      !comm->allgather_u64 || !comm->allreduce_u64 || !comm->bcast_u64 || !comm->alltoallv)
+    return DSL_ERR_ARG;
+  dsl::g_pending_host_comm = comm;
+  int rc = dsl_create(proto, cfg, out);
+  dsl::g_pending_host_comm = nullptr;
+  return rc;
 }
 
 int dsl_set_settings(dsl_engine* e, const dsl_settings* s) {

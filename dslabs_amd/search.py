@@ -328,10 +328,11 @@ class Engine:
     """One engine (one GPU, or one shard of a multi-GPU search)."""
 
     def __init__(self, protocol, device: int = -1, rank: int = 0, world_size: int = 1,
-                 virtual_shards: int = 0, comm_id: Optional[bytes] = None):
+                 virtual_shards: int = 0, comm_id: Optional[bytes] = None, host_comm=None):
         lib = _lib.load()
         self.lib = lib
         self.protocol = protocol
+        self.host_comm = host_comm  # keeps the ctypes callbacks alive
         cfg = _lib.dsl_engine_config()
         cfg.device = device
         cfg.rank = rank
@@ -340,7 +341,13 @@ class Engine:
         if comm_id is not None:
             ctypes.memmove(cfg.comm_id, comm_id, 128)
         handle = ctypes.c_void_p()
-        check(lib.dsl_create(ctypes.byref(protocol.desc()), ctypes.byref(cfg), ctypes.byref(handle)), "dsl_create")
+        if host_comm is not None:
+            rc = lib.dsl_create_with_host_comm(ctypes.byref(protocol.desc()), ctypes.byref(cfg),
+                                               ctypes.byref(host_comm.struct), ctypes.byref(handle))
+            check(rc, "dsl_create_with_host_comm")
+        else:
+            check(lib.dsl_create(ctypes.byref(protocol.desc()), ctypes.byref(cfg), ctypes.byref(handle)),
+                  "dsl_create")
         self.handle = handle
 
     def close(self):

@@ -193,6 +193,24 @@ typedef struct {
 } dsl_stats;
 
 int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);
+
+/* Caller-provided transport for a multi-process search (one shard per process), used instead
+ * of RCCL: e.g. MPI, a JVM-side transport, or torch.distributed/gloo in tests. All buffers are
+ * HOST memory; every callback is collective (all ranks call it in the same order) and returns 0
+ * on success. alltoallv: send_bytes[d] bytes at send + send_off[d] go to rank d; recv_bytes[s]
+ * bytes from rank s land at recv + recv_off[s]. */
+typedef struct {
+  void* ctx;
+  int32_t rank, size;
+  int (*allgather_u64)(void* ctx, const uint64_t* in, int32_t n, uint64_t* out /* size*n */);
+  int (*allreduce_u64)(void* ctx, uint64_t* v, int32_t n, int32_t is_min);
+  int (*bcast_u64)(void* ctx, uint64_t* v, int32_t n, int32_t root);
+  int (*alltoallv)(void* ctx, const uint8_t* send, const uint64_t* send_off, const uint64_t* send_bytes,
+                   uint8_t* recv, const uint64_t* recv_off, const uint64_t* recv_bytes);
+} dsl_host_comm;
+
+int dsl_create_with_host_comm(const dsl_protocol_desc* proto, const dsl_engine_config* cfg,
+                              const dsl_host_comm* comm, dsl_engine** out);
 void dsl_result_free(dsl_result* r);
 void dsl_destroy(dsl_engine* e);
 const char* dsl_last_error(void);

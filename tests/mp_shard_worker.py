@@ -1,0 +1,83 @@
+"""Worker for tests: one shard of a multi-process search (gloo host transport).
+
+env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT; argv: <mode> <out.json>
+mode 'collectives' runs the dsl_host_comm callbacks directly (CPU only);
+mode 'lab0' / 'sipaxos' / 'mutant' runs a sharded search on cuda:0 through the engine."""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch.distributed as dist
+    mode, out = sys.argv[1], sys.argv[2]
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    from dslabs_amd.distributed import TorchHostComm
+    hc = TorchHostComm()
+    res = {"rank": rank}
+    if mode == "collectives":
+        U = ctypes.POINTER(ctypes.c_uint64)
+        inp = np.array([rank + 1, 10 * (rank + 1)], dtype=np.uint64)
+        outa = np.zeros(2 * world, dtype=np.uint64)
+        hc.allgather(None, inp.ctypes.data_as(U), 2, outa.ctypes.data_as(U))
+        res["allgather"] = outa.tolist()
+        v = np.array([rank + 5, ~np.uint64(0) if rank == 0 else np.uint64(7)], dtype=np.uint64)
+        hc.allreduce(None, v.ctypes.data_as(U), 2, 1)
+        res["allreduce_min"] = [int(x) for x in v]
+        v = np.array([rank + 5, 1 << 40], dtype=np.uint64)
+        hc.allreduce(None, v.ctypes.data_as(U), 2, 0)
+        res["allreduce_sum"] = [int(x) for x in v]
+        b = np.array([rank * 3 + 1, rank], dtype=np.uint64)
+        hc.bcast(None, b.ctypes.data_as(U), 2, world - 1)
+        res["bcast"] = [int(x) for x in b]
+        # alltoallv: rank r sends (r*16 + d) repeated (r + d + 1) times to rank d, region stride 64
+        so = np.array([64 * d for d in range(world)], dtype=np.uint64)
+        sb = np.array([0 if d == rank else rank + d + 1 for d in range(world)], dtype=np.uint64)
+        send = np.zeros(64 * world, dtype=np.uint8)
+        for d in range(world):
+            send[64 * d: 64 * d + int(sb[d])] = rank * 16 + d
+        rb = np.array([0 if s == rank else s + rank + 1 for s in range(world)], dtype=np.uint64)
+        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.uint64)
+        recv = np.zeros(int(rb.sum()) + 1, dtype=np.uint8)
+        U8 = ctypes.POINTER(ctypes.c_uint8)
+        hc.alltoallv(None, send.ctypes.data_as(U8), so.ctypes.data_as(U), sb.ctypes.data_as(U),
+                     recv.ctypes.data_as(U8), ro.ctypes.data_as(U), rb.ctypes.data_as(U))
+        res["alltoallv"] = recv[:int(rb.sum())].tolist()
+    else:
+        from dslabs_amd import CLIENTS_DONE, RESULTS_OK, Engine, SearchSettings
+        from dslabs_amd.protocols import PingPong, SIPaxos
+        if mode == "lab0":
+            proto = PingPong(2, 10)
+            s = SearchSettings().addInvariant(RESULTS_OK).addPrune(CLIENTS_DONE)
+        elif mode == "mutant":
+            proto = PingPong(1, 10, check_value=False)
+            s = SearchSettings().addInvariant(RESULTS_OK).addGoal(CLIENTS_DONE)
+        else:
+            proto = SIPaxos(2, 3, ("a", "b"))
+            s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
+            s.maxDepth(9)
+        s.table_log2_slots = 22
+        eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc)
+        r = eng.bfs(proto.initial_state(), s)
+        res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states,
+                   exchanged=eng.kernel_stats()["exchanged"])
+        t = r.invariantViolatingState() or r.goalMatchingState()
+        if t is not None:
+            res["trace"] = t.trace()
+            res["depth"] = t.depth()
+        eng.close()
+    res["errors"] = hc.errors
+    with open(out, "w") as f:
+        json.dump(res, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
