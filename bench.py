@@ -28,6 +28,12 @@ METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 WORKLOADS = {
+    # BASELINE config C5: lab3 Multi-Paxos (builder-authored), 3 servers, 2 clients
+    # appending X / Y to one key, invariants RESULTS_OK + LOGS_CONSISTENT_ALL_SLOTS +
+    # APPENDS_LINEARIZABLE, timers on, BFS to maxDepth 12 (1,110,019 unique states).
+    "multipaxos": dict(depth=12, cpu_depth=10,
+                       desc="lab3 Multi-Paxos, 3 servers + 2 clients (append X / append Y), invariants "
+                            "RESULTS_OK, LOGS_CONSISTENT_ALL_SLOTS, APPENDS_LINEARIZABLE, timers on, BFS to maxDepth"),
     # The reference's own Paxos ("Paxos Made Simple", SingleInstancePaxos.java:50-127): 2
     # proposers, 3 acceptors, invariants Integrity + Agreement, exhaustive to maxDepth.
     "sipaxos": dict(depth=15, cpu_depth=10,
@@ -38,7 +44,16 @@ WORKLOADS = {
 
 def build_search(name: str, depth: int):
     from dslabs_amd import SearchSettings
-    from dslabs_amd.protocols import SIPaxos
+    from dslabs_amd import RESULTS_OK
+    from dslabs_amd.protocols import MultiPaxos, SIPaxos
+    if name == "multipaxos":
+        proto = MultiPaxos(3, 2, "append-xy")
+        s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
+        s.addInvariant(proto.predicate("APPENDS_LINEARIZABLE"))
+        s.maxDepth(depth)
+        s.table_log2_slots = 28
+        return proto, s, ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
+                          "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
     if name == "sipaxos":
         proto = SIPaxos(2, 3, ("a", "b"))
         s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
@@ -82,7 +97,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="sipaxos")
+    ap.add_argument("--workload", default="multipaxos")
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()

@@ -1,4 +1,6 @@
 // all.hpp -- every protocol with device transition functions.
 #pragma once
+#include "multipaxos.hpp"
 #include "pingpong.hpp"
 #include "sipaxos.hpp"
+#define DSL_HAVE_MULTIPAXOS 1

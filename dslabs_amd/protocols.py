@@ -116,3 +116,105 @@ class SIPaxos(Protocol):
         else:
             body = f"AcceptAck({n})"
         return f"Message({self.addresses[e.from_]} -> {self.addresses[e.to]}, {body})"
+
+
+class MultiPaxos(Protocol):
+    """lab3 Multi-Paxos (builder-authored): servers "server1..n", clients
+    "client1..c"; each client appends single-character values to key "foo"
+    (KVStoreWorkload.append, labs/lab1-clientserver/tst/dslabs/kvstore/KVStoreWorkload.java:52)."""
+
+    proto_id = DSL_PROTO_MULTIPAXOS
+    VALUES = ["X", "Y", "Z"]
+    PREDICATES = {"LOGS_CONSISTENT_ALL_SLOTS": (400, "Non-empty log slots consistent"),
+                  "APPENDS_LINEARIZABLE": (300, "Sequence of appends to the same key is linearizable")}
+    WORKLOADS = {  # same names as the oracle's --workload
+        "append-xy": ([["X"], ["Y"]], [[], []]),
+        "append-xy-expect": ([["X"], ["Y"]], [["X"], ["XY"]]),
+        "append-x": ([["X"]], [["X"]]),
+        "append-xz": ([["X", "Z"], ["Y"]], [[], []]),
+    }
+
+    def __init__(self, servers: int = 3, clients: int = 2, workload: str = "append-xy"):
+        vals, exp = self.WORKLOADS[workload]
+        self.workload = workload
+        self.servers = servers
+        self.clients = clients
+        self.values = vals[:clients]
+        self.expected = exp[:clients]
+        self.addresses = [f"server{i}" for i in range(1, servers + 1)] + [f"client{i}" for i in range(1, clients + 1)]
+
+    @staticmethod
+    def encode_result(s: str) -> int:
+        r = len(s)
+        for i, ch in enumerate(s):
+            r |= (MultiPaxos.VALUES.index(ch) + 1) << (3 + 2 * i)
+        return r
+
+    @staticmethod
+    def decode_result(r: int) -> str:
+        return "".join(MultiPaxos.VALUES[((r >> (3 + 2 * i)) & 3) - 1] for i in range(r & 7))
+
+    def params(self):
+        ps = [self.servers, self.clients]
+        for c in range(2):
+            vals = self.values[c] if c < self.clients else []
+            exp = self.expected[c] if c < self.clients else []
+            v = [self.VALUES.index(x) + 1 for x in vals] + [0] * (2 - len(vals))
+            e = [self.encode_result(x) for x in exp] + [-1] * (2 - len(exp))
+            ps += [len(vals)] + v + e
+        return ps
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        pid, full = self.PREDICATES[name]
+        return StatePredicate(full, pid)
+
+    # ---- rendering in the oracle's toString form ------------------------------------------------
+    def _cmd(self, cmd: int) -> str:
+        if cmd == 0:
+            return "noop"
+        c, q = (cmd - 1) >> 1, ((cmd - 1) & 1) + 1
+        return f"{self.servers + c}#{q}:{self.values[c][q - 1]}"
+
+    @staticmethod
+    def _ballot(cb: int) -> str:
+        return f"({cb >> 2},{cb & 3})"
+
+    @staticmethod
+    def _mballot(m: int) -> int:
+        return ((m & 0xF) << 2) | ((m >> 4) & 3)
+
+    def _entry(self, e: int) -> str:
+        st, b, cmd = e & 3, (e >> 2) & 0x3F, (e >> 8) & 7
+        if st == 0:
+            return "E"
+        if st == 2:
+            return "C:" + self._cmd(cmd)
+        return "A" + self._ballot(b) + ":" + self._cmd(cmd)
+
+    def render_event(self, e) -> str:
+        a = self.addresses
+        if e.is_timer:
+            if e.type == 8:
+                return f"Timer(-> {a[e.to]}, TickTimer())"
+            return f"Timer(-> {a[e.to]}, ClientTimer({e.fields[0]}))"
+        m = e.fields[0]
+        t = e.type
+        if t == 0:
+            body = f"PaxosRequest({self._cmd(m & 7)})"
+        elif t == 1:
+            body = f"PaxosReply({m & 3}, {self.decode_result((m >> 2) & 0xFFF)})"
+        elif t == 2:
+            body = f"P1a({self._ballot(self._mballot(m))})"
+        elif t == 3:
+            log = ";".join(self._entry((m >> (6 + 11 * i)) & 0x7FF) for i in range(4))
+            body = f"P1b({self._ballot(self._mballot(m))}, {log})"
+        elif t == 4:
+            body = f"P2a({self._ballot(self._mballot(m))}, {(m >> 6) & 7}, {self._cmd((m >> 9) & 7)})"
+        elif t == 5:
+            body = f"P2b({self._ballot(self._mballot(m))}, {(m >> 6) & 7})"
+        elif t == 6:
+            body = f"Decision({m & 7}, {self._cmd((m >> 3) & 7)})"
+        else:
+            body = f"Heartbeat({self._ballot(self._mballot(m))})"
+        return f"Message({a[e.from_]} -> {a[e.to]}, {body})"

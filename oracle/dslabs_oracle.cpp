@@ -16,6 +16,7 @@
 #include <iostream>
 
 #include "oracle_core.hpp"
+#include "proto_multipaxos.hpp"
 #include "proto_pingpong.hpp"
 #include "proto_sipaxos.hpp"
 
@@ -105,6 +106,17 @@ static Scenario build(const Args& a) {
       if (n == "Termination") return sipaxos::termination(P);
       throw std::runtime_error("unknown predicate " + n);
     };
+  } else if (a.proto == "multipaxos") {
+    multipaxos::Config cfg = multipaxos::Config::fromArgs(a.geti("servers", 3), a.geti("clients", 2),
+                                                          a.get("workload", "append-xy"), false);
+    sc.init = multipaxos::initial(cfg, sc.names);
+    sc.pred = [common, cfg](const std::string& n) -> Predicate {
+      auto p = common(n);
+      if (p) return *p;
+      if (n == "LOGS_CONSISTENT_ALL_SLOTS") return multipaxos::logsConsistent(cfg);
+      if (n == "APPENDS_LINEARIZABLE") return multipaxos::appendsLinearizable(cfg);
+      throw std::runtime_error("unknown predicate " + n);
+    };
   } else {
     throw std::runtime_error("unknown protocol " + a.proto);
   }
@@ -151,12 +163,36 @@ static void printTerminal(const Terminal& t, const Names& names, bool printState
   std::cout << "}";
 }
 
+// --start-trace FILE: replay the events (one per line, unfiltered) from the initial state and
+// start the search there (bfs(goalStateOfAnEarlierSearch), e.g. PaxosTest.java:898-910).
+static std::shared_ptr<const State> replayStart(const Args& a, Scenario& sc) {
+  std::shared_ptr<const State> s = sc.init;
+  if (!a.has("start-trace")) return s;
+  Settings all;  // events are matched without delivery filters
+  std::ifstream in(a.get("start-trace"));
+  std::string line;
+  while (std::getline(in, line)) {
+    if (line.empty()) continue;
+    bool found = false;
+    for (auto& ev : events(*s, all))
+      if (eventStr(ev, sc.names) == line) {
+        s = stepEvent(s, ev);
+        found = true;
+        break;
+      }
+    if (!found) throw std::runtime_error("start trace event not enabled: " + line);
+  }
+  auto fresh = std::make_shared<State>(*s);  // the start state keeps its depth
+  return fresh;
+}
+
 static int runBfs(const Args& a) {
   Scenario sc = build(a);
   Settings st = settingsFrom(a, sc);
+  std::shared_ptr<const State> start = replayStart(a, sc);
   int reps = a.geti("repeat", 1);
   Results R;
-  for (int r = 0; r < reps; r++) R = bfs(sc.init, st, a.has("finish-level"), a.has("max-secs") ? std::stod(a.get("max-secs")) : -1);
+  for (int r = 0; r < reps; r++) R = bfs(start, st, a.has("finish-level"), a.has("max-secs") ? std::stod(a.get("max-secs")) : -1);
   std::cout << "{\"end\":\"" << endName(R.end) << "\",\"states\":" << R.states << ",\"max_depth\":" << R.maxDepth
             << ",\"successors\":" << R.successorsGenerated << ",\"elapsed_s\":" << R.elapsed << ",\"per_depth\":[";
   for (size_t d = 0; d < R.perDepth.size(); d++) std::cout << (d ? "," : "") << R.perDepth[d];
@@ -270,6 +306,9 @@ int main(int argc, char** argv) {
   } catch (const std::exception& e) {
     std::cout << "{\"error\":\"" << jsonEsc(e.what()) << "\"}" << std::endl;
     return 1;
+  } catch (const Overflow& o) {
+    std::cout << "{\"error\":\"overflow: " << jsonEsc(o.msg) << "\"}" << std::endl;
+    return 3;
   }
   std::cerr << "unknown mode\n";
   return 2;

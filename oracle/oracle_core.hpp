@@ -82,6 +82,13 @@ struct TimerEnv {  // TimerEnvelope, equality {to, timer, min, max} (TimerEnvelo
   }
 };
 
+// A bounded container of a restated protocol overflowed: a hard error of the oracle run (the
+// engine reports DSL_ERR_STATE_OVERFLOW for the same situation). Deliberately NOT a
+// std::exception, so stepEvent does not capture it as a handler exception.
+struct Overflow {
+  std::string msg;
+};
+
 // Exceptions thrown by handlers (captured into the state, SearchState.java:218-222).
 struct HandlerException : std::runtime_error {
   using std::runtime_error::runtime_error;

@@ -1,0 +1,59 @@
+"""Maps oracle CLI arguments (tests/golden/*.json "args") onto the engine's Python API, so each
+committed oracle fixture is replayed on the GPU with the same meaning."""
+from dslabs_amd import CLIENTS_DONE, NONE_DECIDED, RESULTS_OK, SearchSettings, clientDone
+from dslabs_amd.protocols import MultiPaxos, PingPong, SIPaxos
+
+
+def _opt(args, name, default=None):
+    return args[args.index(name) + 1] if name in args else default
+
+
+def protocol(args):
+    p = _opt(args, "--proto", "pingpong")
+    if p == "pingpong":
+        return PingPong(int(_opt(args, "--clients", 1)), int(_opt(args, "--pings", 10)),
+                        check_value="--mutant-no-check" not in args, reset_timer="--mutant-no-reset" not in args)
+    if p == "sipaxos":
+        vals = _opt(args, "--values", "a,b").split(",")
+        return SIPaxos(int(_opt(args, "--proposers", 2)), int(_opt(args, "--acceptors", 3)), vals,
+                       incorrect="--incorrect" in args)
+    if p == "multipaxos":
+        return MultiPaxos(int(_opt(args, "--servers", 3)), int(_opt(args, "--clients", 2)),
+                          _opt(args, "--workload", "append-xy"))
+    raise ValueError(p)
+
+
+def predicate(proto, name):
+    neg = name.startswith("!")
+    name = name.lstrip("!")
+    std = {"RESULTS_OK": RESULTS_OK, "CLIENTS_DONE": CLIENTS_DONE, "NONE_DECIDED": NONE_DECIDED}
+    if name in std:
+        p = std[name]
+    elif name.startswith("clientDone:"):
+        p = clientDone(name.split(":", 1)[1])
+    else:
+        p = proto.predicate(name)
+    return p.negate() if neg else p
+
+
+def settings(args, proto, table_log2=24):
+    s = SearchSettings()
+    s.table_log2_slots = table_log2
+    i = 0
+    while i < len(args):
+        a = args[i]
+        v = args[i + 1] if i + 1 < len(args) else None
+        if a == "--inv":
+            s.addInvariant(predicate(proto, v))
+        elif a == "--goal":
+            s.addGoal(predicate(proto, v))
+        elif a == "--prune":
+            s.addPrune(predicate(proto, v))
+        elif a == "--max-depth":
+            s.maxDepth(int(v))
+        elif a == "--no-timers":
+            s.deliverTimers(v, False)
+        elif a == "--partition":
+            s.partition(*[g.split(",") for g in v.split("|")])
+        i += 1
+    return s

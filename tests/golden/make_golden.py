@@ -116,3 +116,37 @@ if __name__ == "__main__":
         json.dump({"source": "framework/tst-self/dslabs/framework/testing/search/TimerQueueTest.java:153-175",
                    "columns": ["min1", "max1", "min2", "max2", "te1_deliverable", "te2_in_deliverable",
                                "te2_isDeliverable"], "cases": tq["cases"]}, f)
+
+
+MP = ["--proto", "multipaxos"]
+INV3 = ["--inv", "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
+MULTIPAXOS = {
+    # BASELINE C5: 3 servers, 2 clients (append(foo,X) / append(foo,Y)), maxDepth 12, timers on
+    "mp_c5_d12": dict(args=MP + ["--workload", "append-xy"] + INV3 + ["--max-depth", "12"], pinned={}),
+    "mp_c5_d8": dict(args=MP + ["--workload", "append-xy"] + INV3 + ["--max-depth", "8"], pinned={}),
+    "mp_c5_notimers_d10": dict(args=MP + ["--workload", "append-xy"] + INV3 + ["--max-depth", "10", "--no-timers",
+                                                                                "server1", "--no-timers", "server2",
+                                                                                "--no-timers", "server3",
+                                                                                "--no-timers", "client1",
+                                                                                "--no-timers", "client2"], pinned={}),
+    # PaxosTest.test22 phase 1: partition(server1, server2, client1), goal !NONE_DECIDED
+    "mp_test22_phase1": dict(args=MP + ["--workload", "append-xy-expect", "--inv", "RESULTS_OK", "--inv",
+                                        "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "!NONE_DECIDED", "--partition",
+                                        "server1,server2,client1", "--finish-level"], pinned={}),
+    # full network with expected results X / XY: client2 can be ordered first -> violation
+    "mp_expect_violation": dict(args=MP + ["--workload", "append-xy-expect", "--inv", "RESULTS_OK", "--inv",
+                                           "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "CLIENTS_DONE", "--finish-level"],
+                                pinned={}),
+    # PaxosTest.test27-style singleton group: CLIENTS_DONE after 2 steps per command
+    "mp_singleton": dict(args=MP + ["--servers", "1", "--clients", "1", "--workload", "append-x"] + INV3 +
+                         ["--goal", "CLIENTS_DONE", "--finish-level"],
+                         pinned={"terminal_depth": 2,
+                                 "source": "PaxosTest.java:1214-1228 (singleton reaches CLIENTS_DONE at 2 steps per "
+                                           "command; its 3-command workload at depth 6)"}),
+    "mp_2s1c_prune": dict(args=MP + ["--servers", "2", "--clients", "1", "--workload", "append-x"] + INV3 +
+                          ["--prune", "CLIENTS_DONE", "--max-depth", "11"], pinned={}),
+    "mp_xz_d8": dict(args=MP + ["--workload", "append-xz"] + INV3 + ["--max-depth", "8"], pinned={}),
+}
+
+if __name__ == "__main__":
+    gen(MULTIPAXOS, "multipaxos.json")

@@ -31,7 +31,12 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   struct Node {
     S s;
     int depth;
+    long long id;
   };
+  // parent pointers (for printing the first terminal's trace)
+  std::vector<std::pair<long long, int>> parent{{-1, -1}};
+  long long first_term_parent = -2;
+  int first_term_event = -1;
   auto key = [](const S& s) { return std::string((const char*)s.w, sizeof(S)); };
   S init;
   P::init(init, prm);
@@ -48,7 +53,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     end = v0 == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
   } else {
-    q.push_back({init, 0});
+    q.push_back({init, 0, 0});
   }
   int best = 99;
   while (!q.empty()) {
@@ -78,11 +83,13 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       int v = judge<P>(t, prm, set, d, &pi);
       if (v >= V_TERM_EXCEPTION) {
         if (tdepth < 0) tdepth = d;
+        if (first_term_parent == -2) first_term_parent = n.id, first_term_event = k;
         best = std::min(best, v);
         continue;
       }
       if (v == V_PRUNED) continue;
-      q.push_back({t, d});
+      parent.push_back({n.id, k});
+      q.push_back({t, d, (long long)parent.size() - 1});
     }
   }
   if (best != 99)
@@ -93,7 +100,24 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
   }
-  printf("],\"states\":%llu}\n", total);
+  printf("],\"states\":%llu", total);
+  if (first_term_parent >= 0) {
+    // trace of the first terminal: replay the event indices from the initial state
+    std::vector<int> evs{first_term_event};
+    for (long long id = first_term_parent; id > 0; id = parent[id].first) evs.push_back(parent[id].second);
+    std::reverse(evs.begin(), evs.end());
+    printf(",\"trace\":[");
+    S s = init, t;
+    for (size_t i = 0; i < evs.size(); i++) {
+      dsl_event e;
+      P::describe(s, prm, set, evs[i], &e);
+      printf("%s[%d,%d,%d,%d,%lld]", i ? "," : "", e.is_timer, e.from, e.to, e.type, (long long)e.fields[0]);
+      P::step(s, evs[i], t, prm, set);
+      s = t;
+    }
+    printf("]");
+  }
+  printf("}\n");
   return 0;
 }
 

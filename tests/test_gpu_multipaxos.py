@@ -1,0 +1,83 @@
+"""lab3 Multi-Paxos (BASELINE C5) on the MI355X engine vs the oracle's golden vectors."""
+import json
+import os
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import EndCondition, Engine, Search
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "multipaxos.json")))
+
+
+def _run(case, **eng):
+    proto = argmap.protocol(case["args"])
+    s = argmap.settings(case["args"], proto)
+    e = Engine(proto, **eng)
+    try:
+        return e.bfs(proto.initial_state(), s)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("name", sorted(GOLD))
+def test_multipaxos_parity(name):
+    case = GOLD[name]
+    r = _run(case)
+    assert r.endCondition().name == case["end"]
+    assert r.per_depth == case["per_depth"], name
+    assert r.states == case["states"]
+    if case["terminal_depth"] >= 0:
+        assert r.max_depth == case["terminal_depth"]
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_multipaxos_c5_sharded(shards):
+    case = GOLD["mp_c5_d12"]
+    r = _run(case, virtual_shards=shards)
+    assert r.per_depth == case["per_depth"]
+
+
+@pytest.mark.parametrize("name", ["mp_expect_violation", "mp_test22_phase1", "mp_singleton"])
+def test_multipaxos_trace_replays(name):
+    case = GOLD[name]
+    r = _run(case)
+    st = r.invariantViolatingState() or r.goalMatchingState()
+    args = [a for a in case["args"] if a != "--finish-level"]
+    rep = oracle_util.replay(args, st.trace())
+    assert rep["ok"], rep["error"]
+    assert rep["depth"] == st.depth()
+    if r.endCondition() == EndCondition.INVARIANT_VIOLATED:
+        assert not all(i["value"] for i in rep["invariants"])
+    else:
+        assert rep["goals"][0]["value"]
+
+
+def test_test22_two_phase_search():
+    """PaxosTest.test22: goal in partition {server1, server2, client1}, then from that state
+    CLIENTS_DONE must be reachable in partition {server1, server3, client2}; the second search
+    starts from the GPU's own goal state and is checked against the oracle started from the
+    same (replayed) state."""
+    case = GOLD["mp_test22_phase1"]
+    r1 = _run(case)
+    assert r1.endCondition() == EndCondition.GOAL_FOUND
+    first = r1.goalMatchingState()
+    proto = first.protocol
+    args2 = ["--proto", "multipaxos", "--workload", "append-xy-expect", "--inv", "RESULTS_OK", "--inv",
+             "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "CLIENTS_DONE", "--partition", "server1,server3,client2",
+             "--finish-level"]
+    r2 = Search.bfs(first, argmap.settings(args2, proto))
+    assert r2.endCondition() == EndCondition.GOAL_FOUND
+    import tempfile
+    with tempfile.NamedTemporaryFile("w", suffix=".trace", delete=False) as f:
+        f.write("\n".join(first.trace()) + "\n")
+    try:
+        want = oracle_util.run("bfs", args2 + ["--start-trace", f.name], timeout=300)
+    finally:
+        os.unlink(f.name)
+    assert r2.per_depth == want["per_depth"]
+    assert r2.initial_depth == first.depth()
+    rep = oracle_util.replay(args2[:-1], r2.goalMatchingState().trace())
+    assert rep["ok"] and rep["goals"][0]["value"]

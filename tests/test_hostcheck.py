@@ -57,6 +57,16 @@ CASES = {
     "sip_2p5a_d6": ([2, 2, 5, 0, "--", 101, 100, "/", "/", 6],
                     ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "5", "--values", "a,b", "--inv",
                      "Integrity", "--inv", "Agreement", "--max-depth", "6"]),
+    "mp_c5_d10": ([5, 3, 2, 1, 1, 0, -1, -1, 1, 2, 0, -1, -1, "--", 1, 400, 300, "/", "/", 10],
+                  ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
+                   "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--max-depth", "10"]),
+    "mp_xz_d8": ([5, 3, 2, 2, 1, 3, -1, -1, 1, 2, 0, -1, -1, "--", 1, 400, 300, "/", "/", 8],
+                 ["--proto", "multipaxos", "--workload", "append-xz", "--inv", "RESULTS_OK", "--inv",
+                  "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--max-depth", "8"]),
+    "mp_2s1c_d11": ([5, 2, 1, 1, 1, 0, 9, -1, 0, 0, 0, -1, -1, "--", 1, 400, 300, "/", "/", 2, 11],
+                    ["--proto", "multipaxos", "--servers", "2", "--clients", "1", "--workload", "append-x", "--inv",
+                     "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--prune",
+                     "CLIENTS_DONE", "--max-depth", "11"]),
 }
 
 
