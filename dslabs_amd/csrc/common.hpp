@@ -35,6 +35,7 @@ struct DevPred {
 struct DevSettings {
   uint32_t deliver[DSL_MAX_NODES];
   uint32_t timer_mask;
+  int32_t all_deliver;  // every (from, to) pair of the protocol's nodes delivers
   int32_t max_depth;
   int32_t n_inv, n_goal, n_prune;
   DevPred inv[DSL_MAX_PREDICATES];
@@ -65,37 +66,5 @@ struct Packed {
 
 // How a successor is judged (Search.checkState, Search.java:162-231).
 enum Verdict : int { V_VALID = 0, V_PRUNED = 1, V_TERM_EXCEPTION = 2, V_TERM_INVARIANT = 3, V_TERM_GOAL = 4 };
-
-// Evaluates the settings' predicate programs in the reference order:
-// invariants (first violated or throwing, insertion order) -> goals (first true, throwing
-// ignored) -> prunes (any true or throwing) -> absolute depth >= maxDepth.
-template <class P>
-DSL_HD Verdict judge(const typename P::State& s, const typename P::Params& prm, const DevSettings& set,
-                     int depth, int* pred_index) {
-  for (int i = 0; i < set.n_inv; i++) {
-    int v = P::eval(set.inv[i], s, prm);
-    if (v != PV_THREW && set.inv[i].negate) v = !v;
-    if (v != PV_TRUE) {
-      *pred_index = i;
-      return V_TERM_INVARIANT;
-    }
-  }
-  for (int i = 0; i < set.n_goal; i++) {
-    int v = P::eval(set.goal[i], s, prm);
-    if (v == PV_THREW) continue;
-    if (set.goal[i].negate) v = !v;
-    if (v == PV_TRUE) {
-      *pred_index = i;
-      return V_TERM_GOAL;
-    }
-  }
-  for (int i = 0; i < set.n_prune; i++) {
-    int v = P::eval(set.prune[i], s, prm);
-    if (v != PV_THREW && set.prune[i].negate) v = !v;
-    if (v != PV_FALSE) return V_PRUNED;
-  }
-  if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
-  return V_VALID;
-}
 
 }  // namespace dsl

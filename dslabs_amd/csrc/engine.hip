@@ -1,13 +1,10 @@
 // engine.hip -- libdslabs_hip.so: C ABI (include/dslabs_hip.h) over the templated engine.
 #include <hip/hip_runtime.h>
 
-#include <hipcub/hipcub.hpp>
-#include <mutex>
 #include <string>
 
-#include "engine.hpp"
+#include "bfs_engine.hpp"
 #include "protocols/all.hpp"
-#include "sharded_engine.hpp"
 
 #ifdef DSL_WITH_RCCL
 #include <rccl/rccl.h>
@@ -159,11 +156,6 @@ struct HostComm : Comm {
 
 static thread_local const dsl_host_comm* g_pending_host_comm = nullptr;
 
-template <class P>
-hipError_t ShardedEngine<P>::hipcub_scan(void* tmp, size_t& bytes, unsigned long long* in, unsigned long long* out,
-                                         uint64_t n) {
-  return hipcub::DeviceScan::ExclusiveSum(tmp, bytes, in, out, n, stream);
-}
 
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
@@ -187,6 +179,10 @@ int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)(int), 
     }
     d.deliver[f] = row;
   }
+  d.all_deliver = 1;
+  for (int f = 0; f < num_nodes; f++)
+    if ((d.deliver[f] & ((num_nodes >= 32 ? 0u : (1u << num_nodes)) - 1u)) != ((num_nodes >= 32 ? 0u : (1u << num_nodes)) - 1u))
+      d.all_deliver = 0;
   for (int a = 0; a < num_nodes; a++) {
     bool ok = in.timers_active[a] >= 0 ? in.timers_active[a] != 0 : in.deliver_timers != 0;
     if (ok) d.timer_mask |= 1u << a;
@@ -215,15 +211,6 @@ int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)(int), 
 }
 
 template <class P>
-hipError_t Engine<P>::scan_bytes(uint64_t n, size_t* bytes) {
-  return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, d_counts, d_offsets, n, stream);
-}
-template <class P>
-hipError_t Engine<P>::scan(uint64_t n) {
-  return hipcub::DeviceScan::ExclusiveSum(d_scan_tmp, scan_tmp_bytes, d_counts, d_offsets, n, stream);
-}
-
-template <class P>
 static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg, EngineBase** out) {
   typename P::Params prm = P::from_desc(d);
   if (!P::valid(prm)) {
@@ -239,12 +226,12 @@ static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg,
       int rc = make_comm(cfg, &cm);
       if (rc) return rc;
     }
-    *out = new ShardedEngine<P>(prm, cfg, cfg.world_size, cm);
+    *out = new BfsEngine<P>(prm, cfg, cfg.world_size, cm);
   } else if (cfg.virtual_shards > 1) {
     if (cfg.virtual_shards > kMaxShards) return DSL_ERR_ARG;
-    *out = new ShardedEngine<P>(prm, cfg, cfg.virtual_shards, nullptr);
+    *out = new BfsEngine<P>(prm, cfg, cfg.virtual_shards, nullptr);
   } else {
-    *out = new Engine<P>(prm, cfg);
+    *out = new BfsEngine<P>(prm, cfg, 1, nullptr);
   }
   return DSL_OK;
 }

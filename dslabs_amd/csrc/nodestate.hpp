@@ -1,0 +1,343 @@
+// nodestate.hpp -- generic packed search state + incremental set fingerprint.
+//
+// A packed state is [kNodes x kNodeWords node words][net count][records, sorted, distinct].
+// Node words hold a node's fields and its timer queue; the network is the SET of sent messages
+// (delivery never removes, duplicates collapse: SearchState.java:71, :300-301).
+//
+// Protocols are node-local, as DSLabs handlers are (F/Node.java:387-562): a handler sees only
+// its node's words and the delivered message / fired timer, updates the words and emits sends.
+// A successor is therefore a DELTA of its parent: one node's new words + a short send list.
+//
+// Fingerprint (128 bit): the XOR over nodes i of H_node(i, words_i) and over the network's
+// records r of H_msg(r), with H = MurmurHash3_x64_128 block/finalizer structure under domain
+// seeds. It is order-independent over the record set, so
+//     fp(successor) = fp(parent) ^ H_node(i, old) ^ H_node(i, new) ^ XOR_{r new to the set} H_msg(r)
+// is computed without materializing the successor. For n distinct states the chance that two
+// share a fingerprint is ~ n^2 / 2^129 (each pair of distinct states differs in a non-empty
+// set of hashed components).
+#pragma once
+#include "common.hpp"
+#include "fingerprint.hpp"
+
+namespace dsl {
+
+template <class P>
+struct Layout {
+  using Rec = typename P::Rec;
+  static constexpr int kRecWords = (int)(sizeof(Rec) / 4);
+  static constexpr int kNetCount = P::kNodes * P::kNodeWords;
+  static constexpr int kRecBase = ((kNetCount + 1 + kRecWords - 1) / kRecWords) * kRecWords;
+  static constexpr int kWords = ((kRecBase + P::kNetCap * kRecWords) + 3) / 4 * 4;
+};
+
+template <class P>
+using StateOf = Packed<Layout<P>::kWords>;
+
+template <class P>
+struct Net {
+  using L = Layout<P>;
+  using Rec = typename P::Rec;
+  static DSL_HD int size(const uint32_t* w) { return (int)w[L::kNetCount]; }
+  static DSL_HD Rec at(const uint32_t* w, int i) {
+    if constexpr (sizeof(Rec) == 8) {
+      return (Rec)w[L::kRecBase + 2 * i] | ((Rec)w[L::kRecBase + 2 * i + 1] << 32);
+    } else {
+      return (Rec)w[L::kRecBase + i];
+    }
+  }
+  static DSL_HD void put(uint32_t* w, int i, Rec r) {
+    if constexpr (sizeof(Rec) == 8) {
+      w[L::kRecBase + 2 * i] = (uint32_t)r;
+      w[L::kRecBase + 2 * i + 1] = (uint32_t)((uint64_t)r >> 32);
+    } else {
+      w[L::kRecBase + i] = (uint32_t)r;
+    }
+  }
+  static DSL_HD bool contains(const uint32_t* w, Rec r) {
+    int lo = 0, hi = size(w);
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      Rec x = at(w, mid);
+      if (x == r) return true;
+      if (x < r) lo = mid + 1; else hi = mid;
+    }
+    return false;
+  }
+  // 0 inserted, 1 present, -1 overflow
+  static DSL_HD int insert(uint32_t* w, Rec r) {
+    int n = size(w), lo = 0, hi = n;
+    while (lo < hi) {
+      int mid = (lo + hi) >> 1;
+      if (at(w, mid) < r) lo = mid + 1; else hi = mid;
+    }
+    if (lo < n && at(w, lo) == r) return 1;
+    if (n >= P::kNetCap) return -1;
+    for (int j = n; j > lo; j--) put(w, j, at(w, j - 1));
+    put(w, lo, r);
+    w[L::kNetCount] = (uint32_t)(n + 1);
+    return 0;
+  }
+};
+
+// Sends emitted by one handler invocation (duplicates collapse, as in the network set).
+template <class P>
+struct Sender {
+  using Rec = typename P::Rec;
+  int n = 0;
+  bool overflow = false;
+  Rec r[P::kMaxSends];
+  DSL_HD void send(Rec x) {
+    for (int i = 0; i < n; i++)
+      if (r[i] == x) return;
+    if (n >= P::kMaxSends) {
+      overflow = true;
+      return;
+    }
+    r[n++] = x;
+  }
+};
+
+// Read access to a state's node words (what predicates and handlers see).
+struct NodeView {
+  const uint32_t* base;     // node words of the parent state
+  int nw;                   // words per node
+  int changed;              // node replaced by `over` (-1: none)
+  const uint32_t* over;
+  DSL_HD const uint32_t* node(int i) const { return i == changed ? over : base + i * nw; }
+};
+
+// ---- fingerprint ------------------------------------------------------------------------------
+DSL_HD Fp fp_xor(Fp a, Fp b) { return Fp{a.hi ^ b.hi, a.lo ^ b.lo}; }
+
+template <int NW>
+DSL_HD Fp hash_words(const uint32_t* w, uint64_t seed) {
+  const uint64_t c1 = 0x87c37b91114253d5ULL, c2 = 0x4cf5ad432745937fULL;
+  uint64_t h1 = seed ^ 0x9368e53c2f6af274ULL, h2 = seed ^ 0x586dcd208f7cd3fdULL;
+#pragma unroll
+  for (int i = 0; i < NW; i += 4) {
+    const uint64_t k1 = (uint64_t)w[i] | ((uint64_t)(i + 1 < NW ? w[i + 1] : 0u) << 32);
+    const uint64_t k2 = (uint64_t)(i + 2 < NW ? w[i + 2] : 0u) | ((uint64_t)(i + 3 < NW ? w[i + 3] : 0u) << 32);
+    uint64_t a = k1 * c1;
+    a = rotl64(a, 31) * c2;
+    h1 ^= a;
+    h1 = rotl64(h1, 27) + h2;
+    h1 = h1 * 5 + 0x52dce729;
+    uint64_t b = k2 * c2;
+    b = rotl64(b, 33) * c1;
+    h2 ^= b;
+    h2 = rotl64(h2, 31) + h1;
+    h2 = h2 * 5 + 0x38495ab5;
+  }
+  h1 ^= (uint64_t)(NW * 4);
+  h2 ^= (uint64_t)(NW * 4);
+  h1 += h2;
+  h2 += h1;
+  h1 = fmix64(h1);
+  h2 = fmix64(h2);
+  h1 += h2;
+  h2 += h1;
+  return Fp{h1, h2};
+}
+
+template <class P>
+DSL_HD Fp node_hash(int i, const uint32_t* w) {
+  return hash_words<P::kNodeWords>(w, 0x5EED00000000ull + (uint64_t)i);
+}
+
+template <class P>
+DSL_HD Fp msg_hash(typename P::Rec r) {
+  uint32_t w[2] = {(uint32_t)(uint64_t)r, (uint32_t)((uint64_t)r >> 32)};
+  return hash_words<2>(w, 0x0E7A5E7ull);
+}
+
+template <class P>
+DSL_HD Fp full_fingerprint(const uint32_t* w) {
+  Fp f{0, 0};
+  for (int i = 0; i < P::kNodes; i++) f = fp_xor(f, node_hash<P>(i, w + i * P::kNodeWords));
+  const int n = Net<P>::size(w);
+  for (int j = 0; j < n; j++) f = fp_xor(f, msg_hash<P>(Net<P>::at(w, j)));
+  return f;
+}
+
+// ---- events -------------------------------------------------------------------------------------
+// Enabled events of a state (SearchState.events, SearchState.java:226-252): every network record
+// whose (from, to) passes shouldDeliver and whose destination exists, in record order; then for
+// every node with deliverTimers(node), its deliverable timers (TimerQueue.deliverable()).
+template <class P>
+DSL_HD int count_events(const uint32_t* w, const typename P::Params& prm, const DevSettings& set) {
+  int n = 0;
+  const int cnt = Net<P>::size(w);
+  const int nodes = P::num_nodes(prm);
+  if (set.all_deliver) {
+    n = cnt;
+  } else {
+    for (int j = 0; j < cnt; j++) {
+      const auto r = Net<P>::at(w, j);
+      n += should_deliver(set, P::rec_from(r), P::rec_to(r));
+    }
+  }
+  for (int i = 0; i < nodes; i++)
+    if (deliver_timers(set, i)) n += P::num_timer_events(i, w + i * P::kNodeWords, prm);
+  return n;
+}
+
+// Locates event k: returns >= 0 = record index, or -1 - (node * 256 + j) for timer j of node.
+template <class P>
+DSL_HD int locate_event(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
+  const int cnt = Net<P>::size(w);
+  if (set.all_deliver) {
+    if (k < cnt) return k;
+    k -= cnt;
+  } else {
+    for (int j = 0; j < cnt; j++) {
+      const auto r = Net<P>::at(w, j);
+      if (should_deliver(set, P::rec_from(r), P::rec_to(r)) && k-- == 0) return j;
+    }
+  }
+  const int nodes = P::num_nodes(prm);
+  for (int i = 0; i < nodes; i++) {
+    if (!deliver_timers(set, i)) continue;
+    const int t = P::num_timer_events(i, w + i * P::kNodeWords, prm);
+    if (k < t) return -1 - (i * 256 + k);
+    k -= t;
+  }
+  return INT32_MIN;
+}
+
+// A successor as a delta of its parent.
+template <class P>
+struct Delta {
+  int node;
+  uint32_t nw[P::kNodeWords];
+  Sender<P> out;
+};
+
+// Applies event k of parent w: fills the delta; returns a StepRc.
+template <class P>
+DSL_HD int delta_step(const uint32_t* w, int k, Delta<P>& d, const typename P::Params& prm, const DevSettings& set) {
+  const int e = locate_event<P>(w, prm, set, k);
+  if (e == INT32_MIN) return STEP_NULL;
+  d.out.n = 0;
+  d.out.overflow = false;
+  int rc;
+  if (e >= 0) {
+    const auto r = Net<P>::at(w, e);
+    d.node = P::rec_to(r);
+    if (d.node >= P::num_nodes(prm)) return STEP_NULL;
+    for (int i = 0; i < P::kNodeWords; i++) d.nw[i] = w[d.node * P::kNodeWords + i];
+    rc = P::on_message(d.node, d.nw, r, d.out, prm);
+  } else {
+    const int x = -1 - e;
+    d.node = x >> 8;
+    for (int i = 0; i < P::kNodeWords; i++) d.nw[i] = w[d.node * P::kNodeWords + i];
+    rc = P::on_timer(d.node, d.nw, x & 255, d.out, prm);
+  }
+  if (d.out.overflow && rc == STEP_OK) rc = STEP_OVERFLOW;
+  return rc;
+}
+
+// Successor fingerprint from the parent's: node delta + the sends not already in the set.
+template <class P>
+DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
+  Fp f = fp_xor(parent, node_hash<P>(d.node, w + d.node * P::kNodeWords));
+  f = fp_xor(f, node_hash<P>(d.node, d.nw));
+  for (int j = 0; j < d.out.n; j++)
+    if (!Net<P>::contains(w, d.out.r[j])) f = fp_xor(f, msg_hash<P>(d.out.r[j]));
+  return f;
+}
+
+// Enabled events of the successor, from the parent's count and the delta: the changed node's
+// timer events are replaced, records new to the set add their deliverable ones.
+template <class P>
+DSL_HD int delta_event_count(const uint32_t* w, int parent_events, const Delta<P>& d, const typename P::Params& prm,
+                             const DevSettings& set) {
+  int n = parent_events;
+  if (deliver_timers(set, d.node))
+    n += P::num_timer_events(d.node, d.nw, prm) - P::num_timer_events(d.node, w + d.node * P::kNodeWords, prm);
+  for (int j = 0; j < d.out.n; j++) {
+    const auto r = d.out.r[j];
+    if (!Net<P>::contains(w, r) && (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))))
+      n++;
+  }
+  return n;
+}
+
+// Materializes the successor (parent w + delta) into out; false on network overflow.
+template <class P>
+DSL_HD bool materialize(const uint32_t* w, const Delta<P>& d, uint32_t* out) {
+  for (int i = 0; i < Layout<P>::kWords; i++) out[i] = w[i];
+  for (int i = 0; i < P::kNodeWords; i++) out[d.node * P::kNodeWords + i] = d.nw[i];
+  for (int j = 0; j < d.out.n; j++)
+    if (Net<P>::insert(out, d.out.r[j]) < 0) return false;
+  return true;
+}
+
+// Whole-state step (host-side trace replay, initial states).
+template <class P>
+DSL_HD int full_step(const uint32_t* w, int k, uint32_t* out, const typename P::Params& prm, const DevSettings& set) {
+  Delta<P> d;
+  int rc = delta_step<P>(w, k, d, prm, set);
+  if (rc == STEP_NULL) return rc;
+  if (!materialize<P>(w, d, out)) return STEP_OVERFLOW;
+  return rc;
+}
+
+// Initial state: every node added and init()-ed in address order (SearchState.setupNode).
+template <class P>
+DSL_HD bool init_state(uint32_t* w, const typename P::Params& prm) {
+  for (int i = 0; i < Layout<P>::kWords; i++) w[i] = 0;
+  for (int i = 0; i < P::num_nodes(prm); i++) {
+    Sender<P> out;
+    P::init_node(i, w + i * P::kNodeWords, out, prm);
+    if (out.overflow) return false;
+    for (int j = 0; j < out.n; j++)
+      if (Net<P>::insert(w, out.r[j]) < 0) return false;
+  }
+  return true;
+}
+
+// Decodes event k of state w for traces (MessageEnvelope / TimerEnvelope fields).
+template <class P>
+void describe_event(const uint32_t* w, int k, const typename P::Params& prm, const DevSettings& set, dsl_event* e) {
+  *e = dsl_event{};
+  const int x = locate_event<P>(w, prm, set, k);
+  if (x == INT32_MIN) return;
+  if (x >= 0) {
+    P::describe_message(Net<P>::at(w, x), e);
+  } else {
+    const int y = -1 - x, node = y >> 8;
+    P::describe_timer(node, w + node * P::kNodeWords, y & 255, prm, e);
+  }
+}
+
+// checkState order over a node view (Search.java:162-231).
+template <class P>
+DSL_HD Verdict judge_view(const NodeView& v, const typename P::Params& prm, const DevSettings& set, int depth,
+                          int* pred_index) {
+  for (int i = 0; i < set.n_inv; i++) {
+    int x = P::eval(set.inv[i], v, prm);
+    if (x != PV_THREW && set.inv[i].negate) x = !x;
+    if (x != PV_TRUE) {
+      *pred_index = i;
+      return V_TERM_INVARIANT;
+    }
+  }
+  for (int i = 0; i < set.n_goal; i++) {
+    int x = P::eval(set.goal[i], v, prm);
+    if (x == PV_THREW) continue;
+    if (set.goal[i].negate) x = !x;
+    if (x == PV_TRUE) {
+      *pred_index = i;
+      return V_TERM_GOAL;
+    }
+  }
+  for (int i = 0; i < set.n_prune; i++) {
+    int x = P::eval(set.prune[i], v, prm);
+    if (x != PV_THREW && set.prune[i].negate) x = !x;
+    if (x != PV_FALSE) return V_PRUNED;
+  }
+  if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
+  return V_VALID;
+}
+
+}  // namespace dsl

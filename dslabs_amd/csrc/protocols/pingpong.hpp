@@ -1,188 +1,148 @@
-// pingpong.hpp -- lab0 PingPong as device transition functions over a packed state.
+// pingpong.hpp -- lab0 PingPong as node-local device handlers.
 //
 // Re-expresses (not translates) labs/lab0-pingpong/src/dslabs/pingpong/PingServer.java:29-32,
 // PingClient.java:41-87 (sendCommand / handlePongReply / onPingTimer), Timers.java:7-11
 // (PingTimer, 10 ms), wrapped in the ClientWorker command loop
-// (framework/tst/dslabs/framework/testing/ClientWorker.java:174-251) with the
-// repeatedPings workload (labs/lab0-pingpong/tst/dslabs/pingpong/PingTest.java:44-51).
+// (framework/tst/dslabs/framework/testing/ClientWorker.java:174-251) with the repeatedPings
+// workload (labs/lab0-pingpong/tst/dslabs/pingpong/PingTest.java:44-51). README mutants:
+// no pong-value check (README.md:342-347), no timer re-set (README.md:299-306).
 //
-// Nodes: 0 = pingserver, 1..C = client1..clientC. Ping values are interned as 1..N
-// ("ping-i" -> i); 0 encodes null.
-//
-// Packed state (24 words = 96 B):
-//   w[0..1]  network bitmap, PingRequest(client c, value v): bit (c-1)*N + (v-1)   (<= 60 bits)
-//   w[2..3]  network bitmap, PongReply(to client c, value v): bit 64 + (c-1)*N + (v-1)
-//   per client c (5 words at w[4 + 5(c-1)]):
-//     word 0: ping:4 | pong:4 | nres:4 | ntim:4     (PingClient.ping/pong, |results|, |timers|)
-//     words 1-2: results[15] as nibbles            (ClientWorker.results, in order)
-//     words 3-4: timer queue[15] as nibbles        (PingTimer(ping) values, insertion order)
-// Canonical by construction: the network is a set bitmap; lists keep order; unused nibbles 0.
-// The ClientWorker bookkeeping (waitingOnResult, workload index, resultsOk) is a function of
-// nres (ClientWorker equality is {client, results}: ClientWorker.java:49-51), so it is not stored.
+// Nodes: 0 = pingserver (no fields: PingApplication has none), 1..C = client1..clientC.
+// Ping values are interned as 1..N ("ping-i" -> i); 0 encodes null.
+// Client node words (5):
+//   w0: ping:4 | pong:4 | nres:4 | ntim:4     (PingClient.ping/pong, |results|, |timer queue|)
+//   w1-w2: results[15] as nibbles            (ClientWorker.results, in order)
+//   w3-w4: timer queue[15] as nibbles        (PingTimer(ping) values, insertion order)
+// ClientWorker bookkeeping (waitingOnResult, workload index, resultsOk) is a function of nres
+// (its equality is {client, results}: ClientWorker.java:49-51), so it is not stored.
+// Records (32 bit): type:1 @31 | client:3 @28 | value:4 @24
+//   type 0 PingRequest(ping-v) client -> server, type 1 PongReply(ping-v) server -> client.
 #pragma once
-#include "../common.hpp"
+#include "../nodestate.hpp"
 
 namespace dsl {
 
 struct PingPong {
-  static constexpr int kWords = 24;
-  static constexpr int kMaxClients = 4;
-  static constexpr int kMaxPings = 15;
-  static constexpr int kRetryMillis = 10;
-  using State = Packed<kWords>;
+  static constexpr int kMaxClients = 4, kMaxPings = 15, kRetryMillis = 10;
+  static constexpr int kNodes = 1 + kMaxClients, kNodeWords = 5;
+  static constexpr int kNetCap = 2 * kMaxClients * kMaxPings, kMaxSends = 2;
+  using Rec = uint32_t;
+  using State = StateOf<PingPong>;
 
   struct Params {
-    int32_t clients;      // 1..4
-    int32_t pings;        // workload length per client, 1..15
-    int32_t check_value;  // 0 = README mutant (no pong value check)
-    int32_t reset_timer;  // 0 = README mutant (no PingTimer re-set)
+    int32_t clients, pings, check_value, reset_timer;
   };
-
-  // message / timer type ids for decoded events
   enum { T_PING_REQUEST = 0, T_PONG_REPLY = 1, T_PING_TIMER = 2 };
 
-  static DSL_HD int cbase(int c) { return (4 + 5 * (c - 1)) * 32; }  // bit offset of client c
-  static DSL_HD int ping(const State& s, int c) { return s.get(cbase(c), 4); }
-  static DSL_HD int pong(const State& s, int c) { return s.get(cbase(c) + 4, 4); }
-  static DSL_HD int nres(const State& s, int c) { return s.get(cbase(c) + 8, 4); }
-  static DSL_HD int ntim(const State& s, int c) { return s.get(cbase(c) + 12, 4); }
-  static DSL_HD int result(const State& s, int c, int j) { return s.get(cbase(c) + 32 + 4 * j, 4); }
-  static DSL_HD int timer(const State& s, int c, int j) { return s.get(cbase(c) + 96 + 4 * j, 4); }
-  static DSL_HD int req_bit(const Params& p, int c, int v) { return (c - 1) * p.pings + (v - 1); }
-  static DSL_HD int rep_bit(const Params& p, int c, int v) { return 64 + (c - 1) * p.pings + (v - 1); }
+  static DSL_HD Rec rec(int type, int c, int v) { return ((Rec)type << 31) | ((Rec)c << 28) | ((Rec)v << 24); }
+  static DSL_HD int rec_type(Rec r) { return (int)(r >> 31); }
+  static DSL_HD int rec_client(Rec r) { return (int)((r >> 28) & 7); }
+  static DSL_HD int rec_value(Rec r) { return (int)((r >> 24) & 15); }
+  static DSL_HD int rec_from(Rec r) { return rec_type(r) ? 0 : rec_client(r); }
+  static DSL_HD int rec_to(Rec r) { return rec_type(r) ? rec_client(r) : 0; }
 
-  // PingClient.sendCommand: ping = p, pong = null, send PingRequest, set PingTimer(10ms).
-  static DSL_HD bool send_command(State& s, const Params& p, int c, int v) {
-    const int b = cbase(c);
-    s.set(b, 4, v);
-    s.set(b + 4, 4, 0);
-    s.setbit(req_bit(p, c, v));
-    int n = ntim(s, c);
-    if (n >= kMaxPings) return false;
-    s.set(b + 96 + 4 * n, 4, v);
-    s.set(b + 12, 4, n + 1);
-    return true;
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return (w[bit >> 5] >> (bit & 31)) & ((1 << width) - 1); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) {
+    uint32_t m = ((1u << width) - 1) << (bit & 31);
+    w[bit >> 5] = (w[bit >> 5] & ~m) | (((uint32_t)v << (bit & 31)) & m);
   }
+  static DSL_HD int ping(const uint32_t* w) { return get(w, 0, 4); }
+  static DSL_HD int pong(const uint32_t* w) { return get(w, 4, 4); }
+  static DSL_HD int nres(const uint32_t* w) { return get(w, 8, 4); }
+  static DSL_HD int ntim(const uint32_t* w) { return get(w, 12, 4); }
+  static DSL_HD int result(const uint32_t* w, int j) { return get(w, 32 + 4 * j, 4); }
+  static DSL_HD int timer(const uint32_t* w, int j) { return get(w, 96 + 4 * j, 4); }
 
-  // ClientWorker.sendNextCommandWhilePossible: harvest a result, then send the next command.
-  // waitingOnResult == (nres < pings) for this workload (one command in flight until done).
-  static DSL_HD bool client_worker_continue(State& s, const Params& p, int c) {
-    const int b = cbase(c);
-    int n = nres(s, c);
-    if (n < p.pings && pong(s, c) != 0) {
-      s.set(b + 32 + 4 * n, 4, pong(s, c));
+  static DSL_HD void push_timer(uint32_t* w, int v, Sender<PingPong>& out) {
+    const int n = ntim(w);
+    if (n >= kMaxPings) {
+      out.overflow = true;
+      return;
+    }
+    put(w, 96 + 4 * n, 4, v);
+    put(w, 12, 4, n + 1);
+  }
+  // PingClient.sendCommand: ping = p, pong = null, send PingRequest, set PingTimer(10 ms).
+  static DSL_HD void send_command(int c, uint32_t* w, int v, Sender<PingPong>& out) {
+    put(w, 0, 4, v);
+    put(w, 4, 4, 0);
+    out.send(rec(0, c, v));
+    push_timer(w, v, out);
+  }
+  // ClientWorker.sendNextCommandWhilePossible; waitingOnResult == (nres < pings).
+  static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, Sender<PingPong>& out) {
+    int n = nres(w);
+    if (n < p.pings && pong(w) != 0) {
+      put(w, 32 + 4 * n, 4, pong(w));
       n++;
-      s.set(b + 8, 4, n);
-      if (n < p.pings) return send_command(s, p, c, n + 1);
+      put(w, 8, 4, n);
+      if (n < p.pings) send_command(c, w, n + 1, out);
     }
-    return true;
   }
 
-  static DSL_HD void init(State& s, const Params& p) {
-    for (int i = 0; i < kWords; i++) s.w[i] = 0;
-    for (int c = 1; c <= p.clients; c++) send_command(s, p, c, 1);  // ClientWorker.init
+  static DSL_HD int num_nodes(const Params& p) { return 1 + p.clients; }
+  static DSL_HD void init_node(int i, uint32_t* w, Sender<PingPong>& out, const Params& p) {
+    if (i > 0) send_command(i, w, 1, out);  // ClientWorker.init -> first command
   }
+  // TimerQueue.deliverable(): all PingTimers are (10,10): only the head is deliverable.
+  static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params&) { return i > 0 && ntim(w) > 0; }
 
-  // Number of enabled events (SearchState.events): deliverable messages, then timers.
-  static DSL_HD int num_events(const State& s, const Params& p, const DevSettings& set) {
-    int n = 0;
-    for (int c = 1; c <= p.clients; c++) {
-      bool to_srv = should_deliver(set, c, 0), to_cli = should_deliver(set, 0, c);
-      for (int v = 1; v <= p.pings; v++) {
-        n += (to_srv && s.bit(req_bit(p, c, v)));
-        n += (to_cli && s.bit(rep_bit(p, c, v)));
-      }
-      // TimerQueue.deliverable(): every PingTimer is (10,10), so only the head is deliverable.
-      n += (deliver_timers(set, c) && ntim(s, c) > 0);
-    }
-    return n;
-  }
-
-  // Locates the k-th enabled event. kind: 0 request, 1 reply, 2 timer.
-  static DSL_HD bool locate(const State& s, const Params& p, const DevSettings& set, int k, int* kind, int* c_out,
-                            int* v_out) {
-    for (int c = 1; c <= p.clients; c++) {
-      bool to_srv = should_deliver(set, c, 0), to_cli = should_deliver(set, 0, c);
-      for (int v = 1; v <= p.pings; v++) {
-        if (to_srv && s.bit(req_bit(p, c, v)) && k-- == 0) {
-          *kind = 0, *c_out = c, *v_out = v;
-          return true;
-        }
-        if (to_cli && s.bit(rep_bit(p, c, v)) && k-- == 0) {
-          *kind = 1, *c_out = c, *v_out = v;
-          return true;
-        }
-      }
-      if (deliver_timers(set, c) && ntim(s, c) > 0 && k-- == 0) {
-        *kind = 2, *c_out = c, *v_out = timer(s, c, 0);
-        return true;
-      }
-    }
-    return false;
-  }
-
-  static DSL_HD int step(const State& in, int k, State& s, const Params& p, const DevSettings& set) {
-    int kind, c, v;
-    s = in;
-    if (!locate(in, p, set, k, &kind, &c, &v)) return STEP_NULL;
-    if (kind == 0) {
-      // PingServer.handlePingRequest: reply Pong(value) to the sender.
-      s.setbit(rep_bit(p, c, v));
+  static DSL_HD int on_message(int i, uint32_t* w, Rec r, Sender<PingPong>& out, const Params& p) {
+    if (i == 0) {  // PingServer.handlePingRequest: reply Pong(value) to the sender
+      if (rec_type(r) != 0) return STEP_EXCEPTION;
+      out.send(rec(1, rec_client(r), rec_value(r)));
       return STEP_OK;
     }
-    const int b = cbase(c);
-    if (kind == 1) {
-      // PingClient.handlePongReply (value check unless mutant), then the ClientWorker loop.
-      if (!p.check_value || ping(s, c) == v) s.set(b + 4, 4, v);
-      return client_worker_continue(s, p, c) ? STEP_OK : STEP_OVERFLOW;
+    if (rec_type(r) != 1) return STEP_EXCEPTION;
+    const int v = rec_value(r);
+    if (!p.check_value || ping(w) == v) put(w, 4, 4, v);  // PingClient.handlePongReply
+    client_worker_continue(i, w, p, out);
+    return STEP_OK;
+  }
+  // PingClient.onPingTimer, the ClientWorker loop, then remove the first equal timer (the head).
+  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<PingPong>& out, const Params& p) {
+    const int v = timer(w, 0);
+    if (ping(w) == v && pong(w) == 0) {
+      out.send(rec(0, i, v));
+      if (p.reset_timer) push_timer(w, v, out);
     }
-    // PingClient.onPingTimer, ClientWorker loop, then remove the first equal timer (the head).
-    bool ok = true;
-    if (ping(s, c) == v && pong(s, c) == 0) {
-      s.setbit(req_bit(p, c, v));
-      if (p.reset_timer) {
-        int n = ntim(s, c);
-        if (n >= kMaxPings) return STEP_OVERFLOW;
-        s.set(b + 96 + 4 * n, 4, v);
-        s.set(b + 12, 4, n + 1);
-      }
-    }
-    ok = client_worker_continue(s, p, c);
-    int n = ntim(s, c);
-    for (int j = 0; j + 1 < n; j++) s.set(b + 96 + 4 * j, 4, timer(s, c, j + 1));
-    s.set(b + 96 + 4 * (n - 1), 4, 0);
-    s.set(b + 12, 4, n - 1);
-    return ok ? STEP_OK : STEP_OVERFLOW;
+    client_worker_continue(i, w, p, out);
+    const int n = ntim(w);
+    for (int j = 0; j + 1 < n; j++) put(w, 96 + 4 * j, 4, timer(w, j + 1));
+    put(w, 96 + 4 * (n - 1), 4, 0);
+    put(w, 12, 4, n - 1);
+    return STEP_OK;
   }
 
-  static DSL_HD int eval(const DevPred& pr, const State& s, const Params& p) {
+  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const Params& p) {
     switch (pr.id) {
       case DSL_PRED_RESULTS_OK:
-        for (int c = 1; c <= p.clients; c++)
-          for (int j = 0; j < nres(s, c); j++)
-            if (result(s, c, j) != j + 1) return PV_FALSE;
+        for (int c = 1; c <= p.clients; c++) {
+          const uint32_t* w = v.node(c);
+          for (int j = 0; j < nres(w); j++)
+            if (result(w, j) != j + 1) return PV_FALSE;
+        }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
         for (int c = 1; c <= p.clients; c++)
-          if (nres(s, c) < p.pings) return PV_FALSE;
+          if (nres(v.node(c)) < p.pings) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_DONE:
         if (pr.arg0 < 1 || pr.arg0 > p.clients) return PV_THREW;
-        return nres(s, (int)pr.arg0) >= p.pings ? PV_TRUE : PV_FALSE;
+        return nres(v.node((int)pr.arg0)) >= p.pings ? PV_TRUE : PV_FALSE;
       case DSL_PRED_NONE_DECIDED:
         for (int c = 1; c <= p.clients; c++)
-          if (nres(s, c) > 0) return PV_FALSE;
+          if (nres(v.node(c)) > 0) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_HAS_RESULTS:
         if (pr.arg0 < 1 || pr.arg0 > p.clients) return PV_THREW;
-        return nres(s, (int)pr.arg0) == pr.arg1 ? PV_TRUE : PV_FALSE;
+        return nres(v.node((int)pr.arg0)) == pr.arg1 ? PV_TRUE : PV_FALSE;
       default:
         return PV_THREW;
     }
   }
 
   static bool known_predicate(int id) { return id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS; }
-  static int num_nodes(const Params& p) { return 1 + p.clients; }
   static bool valid(const Params& p) {
     return p.clients >= 1 && p.clients <= kMaxClients && p.pings >= 1 && p.pings <= kMaxPings;
   }
@@ -194,21 +154,20 @@ struct PingPong {
     p.reset_timer = d.n_params > 3 ? (int32_t)d.params[3] : 1;
     return p;
   }
-
-  static void describe(const State& s, const Params& p, const DevSettings& set, int k, dsl_event* e) {
-    int kind = 0, c = 0, v = 0;
-    locate(s, p, set, k, &kind, &c, &v);
-    *e = dsl_event{};
+  static void describe_message(Rec r, dsl_event* e) {
+    e->from = rec_from(r);
+    e->to = rec_to(r);
+    e->type = rec_type(r) ? T_PONG_REPLY : T_PING_REQUEST;
     e->n_fields = 1;
-    e->fields[0] = v;
-    if (kind == 0) {
-      e->from = c, e->to = 0, e->type = T_PING_REQUEST;
-    } else if (kind == 1) {
-      e->from = 0, e->to = c, e->type = T_PONG_REPLY;
-    } else {
-      e->is_timer = 1, e->from = c, e->to = c, e->type = T_PING_TIMER;
-      e->timer_min = e->timer_max = kRetryMillis;
-    }
+    e->fields[0] = rec_value(r);
+  }
+  static void describe_timer(int i, const uint32_t* w, int, const Params&, dsl_event* e) {
+    e->is_timer = 1;
+    e->from = e->to = i;
+    e->type = T_PING_TIMER;
+    e->timer_min = e->timer_max = kRetryMillis;
+    e->n_fields = 1;
+    e->fields[0] = timer(w, 0);
   }
 };
 

@@ -3,10 +3,12 @@
 // Runs a protocol's packed-state transition functions (the same __host__ __device__ code the
 // HIP kernels execute) in a plain host BFS with EXACT state equality (no fingerprints), so a
 // protocol encoding can be checked against the oracle's per-depth vectors on a machine with no
-// GPU. It never stands in for the engine: the Search API only runs libdslabs_hip.so kernels.
+// GPU. It also cross-checks the incremental (delta) fingerprint against a full recomputation on
+// every generated successor. It never stands in for the engine: the Search API only runs the
+// libdslabs_hip.so kernels.
 //
 // usage: protocheck <proto> <params...> -- <inv ids> / <goal ids> / <prune ids> maxdepth
-//   e.g. protocheck 1 1 10 1 1 -- 1 / / 2 -1
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -15,7 +17,6 @@
 #include <unordered_set>
 #include <vector>
 
-#include "../../dslabs_amd/csrc/common.hpp"
 #include "../../dslabs_amd/csrc/protocols/all.hpp"
 
 using namespace dsl;
@@ -28,48 +29,54 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     return 1;
   }
   using S = typename P::State;
+  constexpr int NWORDS = Layout<P>::kWords;
   struct Node {
     S s;
     int depth;
     long long id;
+    Fp fp;
   };
-  // parent pointers (for printing the first terminal's trace)
   std::vector<std::pair<long long, int>> parent{{-1, -1}};
   long long first_term_parent = -2;
   int first_term_event = -1;
   auto key = [](const S& s) { return std::string((const char*)s.w, sizeof(S)); };
   S init;
-  P::init(init, prm);
+  if (!init_state<P>(init.w, prm)) {
+    printf("{\"error\":\"init overflow\"}\n");
+    return 1;
+  }
   std::unordered_set<std::string> seen;
   std::deque<Node> q;
   std::vector<unsigned long long> per;
   seen.insert(key(init));
   per.push_back(1);
   int pi = -1;
-  int v0 = judge<P>(init, prm, set, 0, &pi);
+  NodeView v0{init.w, P::kNodeWords, -1, nullptr};
+  int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
-  if (v0 >= V_TERM_EXCEPTION) {
-    end = v0 == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
+  long long fp_mismatch = 0;
+  if (v >= V_TERM_EXCEPTION) {
+    end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
   } else {
-    q.push_back({init, 0, 0});
+    q.push_back({init, 0, 0, full_fingerprint<P>(init.w)});
   }
   int best = 99;
   while (!q.empty()) {
     Node n = q.front();
     if (tdepth >= 0 && n.depth + 1 > tdepth) break;
     q.pop_front();
-    int ne = P::num_events(n.s, prm, set);
+    const int ne = count_events<P>(n.s.w, prm, set);
     for (int k = 0; k < ne; k++) {
-      S t;
-      int rc = P::step(n.s, k, t, prm, set);
+      Delta<P> dl;
+      const int rc = delta_step<P>(n.s.w, k, dl, prm, set);
       if (rc == STEP_NULL) continue;
       if (rc == STEP_OVERFLOW) {
         printf("{\"error\":\"overflow\"}\n");
         return 1;
       }
-      int d = n.depth + 1;
+      const int d = n.depth + 1;
       if (rc == STEP_EXCEPTION) {
         if ((int)per.size() <= d) per.resize(d + 1, 0);
         per[d]++;
@@ -77,10 +84,19 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         best = std::min(best, (int)V_TERM_EXCEPTION);
         continue;
       }
+      S t;
+      if (!materialize<P>(n.s.w, dl, t.w)) {
+        printf("{\"error\":\"overflow\"}\n");
+        return 1;
+      }
+      const Fp f = delta_fingerprint<P>(n.s.w, n.fp, dl);
+      const Fp g = full_fingerprint<P>(t.w);
+      if (f.hi != g.hi || f.lo != g.lo) fp_mismatch++;
       if (!seen.insert(key(t)).second) continue;
       if ((int)per.size() <= d) per.resize(d + 1, 0);
       per[d]++;
-      int v = judge<P>(t, prm, set, d, &pi);
+      NodeView view{n.s.w, P::kNodeWords, dl.node, dl.nw};
+      v = judge_view<P>(view, prm, set, d, &pi);
       if (v >= V_TERM_EXCEPTION) {
         if (tdepth < 0) tdepth = d;
         if (first_term_parent == -2) first_term_parent = n.id, first_term_event = k;
@@ -89,20 +105,20 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       }
       if (v == V_PRUNED) continue;
       parent.push_back({n.id, k});
-      q.push_back({t, d, (long long)parent.size() - 1});
+      q.push_back({t, d, (long long)parent.size() - 1, g});
     }
   }
   if (best != 99)
     end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
   unsigned long long total = 0;
-  printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"per_depth\":[", end, tdepth, (int)sizeof(S));
+  printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"per_depth\":[", end, tdepth,
+         (int)sizeof(S), fp_mismatch);
   for (size_t i = 0; i < per.size(); i++) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
   }
   printf("],\"states\":%llu", total);
   if (first_term_parent >= 0) {
-    // trace of the first terminal: replay the event indices from the initial state
     std::vector<int> evs{first_term_event};
     for (long long id = first_term_parent; id > 0; id = parent[id].first) evs.push_back(parent[id].second);
     std::reverse(evs.begin(), evs.end());
@@ -110,13 +126,14 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     S s = init, t;
     for (size_t i = 0; i < evs.size(); i++) {
       dsl_event e;
-      P::describe(s, prm, set, evs[i], &e);
+      describe_event<P>(s.w, evs[i], prm, set, &e);
       printf("%s[%d,%d,%d,%d,%lld]", i ? "," : "", e.is_timer, e.from, e.to, e.type, (long long)e.fields[0]);
-      P::step(s, evs[i], t, prm, set);
+      full_step<P>(s.w, evs[i], t.w, prm, set);
       s = t;
     }
     printf("]");
   }
+  (void)NWORDS;
   printf("}\n");
   return 0;
 }
@@ -130,6 +147,7 @@ int main(int argc, char** argv) {
   DevSettings set{};
   for (int a = 0; a < DSL_MAX_NODES; a++) set.deliver[a] = 0xffffffffu;
   set.timer_mask = 0xffffffffu;
+  set.all_deliver = 1;
   DevPred* lists[3] = {set.inv, set.goal, set.prune};
   int* counts[3] = {&set.n_inv, &set.n_goal, &set.n_prune};
   int which = 0;
@@ -148,15 +166,7 @@ int main(int argc, char** argv) {
   switch (d.protocol) {
     case DSL_PROTO_PINGPONG: return run<PingPong>(d, set);
     case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, set);
-#ifdef DSL_HAVE_SYNTHETIC
-    case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
-#endif
-#ifdef DSL_HAVE_AMOKV
-    case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
-#endif
-#ifdef DSL_HAVE_MULTIPAXOS
     case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, set);
-#endif
   }
   return 2;
 }

@@ -34,7 +34,8 @@ def test_struct_layouts(lib):
 
 def test_state_bytes_without_device(lib):
     from dslabs_amd.protocols import PingPong
-    assert lib.dsl_state_bytes(ctypes.byref(PingPong(1, 10).desc())) == 96
+    # 5 nodes x 5 words + count + 120 32-bit records, padded to 16 bytes
+    assert lib.dsl_state_bytes(ctypes.byref(PingPong(1, 10).desc())) == 592
 
 
 def test_create_fails_loudly_without_device(lib):
