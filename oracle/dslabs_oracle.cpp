@@ -213,7 +213,7 @@ static int runReplay(const Args& a) {
   Settings st = settingsFrom(a, sc);
   std::ifstream in(a.get("trace-file"));
   std::string line;
-  std::shared_ptr<const State> s = sc.init;
+  std::shared_ptr<const State> s = replayStart(a, sc);  // --start-trace: an earlier search's state
   int step = 0;
   bool ok = true;
   std::string err;

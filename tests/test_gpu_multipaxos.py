@@ -75,11 +75,16 @@ def test_test22_two_phase_search():
         f.write("\n".join(first.trace()) + "\n")
     try:
         want = oracle_util.run("bfs", args2 + ["--start-trace", f.name], timeout=300)
+        # the second trace extends the first (the previous chain crosses the start state); its
+        # suffix is replayed under the second phase's partition from the first goal state
+        full = r2.goalMatchingState().trace()
+        assert full[:first.depth()] == first.trace()
+        rep = oracle_util.replay(args2[:-1] + ["--start-trace", f.name], full[first.depth():])
     finally:
         os.unlink(f.name)
     # the oracle indexes per_depth by absolute depth (zeros before the start state's depth)
     assert want["per_depth"][:first.depth()] == [0] * first.depth()
     assert r2.per_depth == want["per_depth"][first.depth():]
     assert r2.initial_depth == first.depth()
-    rep = oracle_util.replay(args2[:-1], r2.goalMatchingState().trace())
-    assert rep["ok"] and rep["goals"][0]["value"]
+    assert rep["ok"] and rep["goals"][0]["value"], rep
+    assert rep["depth"] == r2.goalMatchingState().depth()
