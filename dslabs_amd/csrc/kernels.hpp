@@ -66,14 +66,100 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* c
   return base + (unsigned long long)__popcll(lt);
 }
 
-__device__ __forceinline__ unsigned long long wave_reserve_dest(unsigned long long* ctrs, bool pred, int dest, int W) {
-  unsigned long long idx = 0;
+// Workgroup-wide slot reservation on per-destination counters (W <= kMaxShards; W = 1 for a
+// plain append): a lane with `pred` gets a unique index in ctrs[dest]. One returning atomic per
+// destination per call per workgroup, not per wave -- a single device-scope counter word
+// saturates near 90 returning atomics/us on MI355X, so per-wave reservations from every CU
+// serialize the whole level on that word. Has barriers: every thread of the block calls it.
+struct BlockResv {
+  int cnt[kBlock / 64][kMaxShards];
+  unsigned long long off[kBlock / 64][kMaxShards];
+};
+
+__device__ __forceinline__ unsigned long long block_reserve(BlockResv& s, unsigned long long* ctrs, bool pred,
+                                                            int dest, int W) {
+  const int wid = threadIdx.x >> 6, lane = __lane_id();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  unsigned long long mine = 0;
   for (int d = 0; d < W; d++) {
-    const bool mine = pred && dest == d;
-    const unsigned long long r = wave_reserve(&ctrs[d], mine);
-    if (mine) idx = r;
+    const bool me = pred && dest == d;
+    const unsigned long long m = __ballot(me);
+    if (lane == 0) s.cnt[wid][d] = __popcll(m);
+    if (me) mine = m;
   }
-  return idx;
+  __syncthreads();
+  if ((int)threadIdx.x < W) {
+    const int d = threadIdx.x;
+    unsigned long long tot = 0;
+    for (int w = 0; w < kBlock / 64; w++) tot += (unsigned long long)s.cnt[w][d];
+    unsigned long long base = tot ? atomicAdd(&ctrs[d], tot) : 0ull;
+    for (int w = 0; w < kBlock / 64; w++) {
+      s.off[w][d] = base;
+      base += (unsigned long long)s.cnt[w][d];
+    }
+  }
+  __syncthreads();
+  return pred ? s.off[wid][dest] + (unsigned long long)__popcll(mine & lt) : 0ull;
+}
+
+// Sums a per-thread value over the workgroup and adds it to *ctr with one atomic (kernel exit).
+__device__ __forceinline__ void block_flush(unsigned long long* red, unsigned long long* ctr, unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  __syncthreads();
+  if (__lane_id() == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kBlock / 64; w++) t += red[w];
+    if (t) atomicAdd(ctr, t);
+  }
+}
+
+// Wave-cooperative row emission: every lane with `active` has a successor (its parent row
+// `base + pidx * NW`, its canonical delta `d`) to be written to `dst`. The rows are written one
+// after another by the whole wavefront, lane L producing words L, L+64, ... of the row
+// (nodestate.hpp: emit_word), so each store instruction covers 256 contiguous bytes and the
+// destination is never read back. The parent row is read with uniform addresses (LDS broadcast
+// or one cache line per 16 lanes). Must be called by all lanes of the wave.
+template <class P>
+__device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
+                                          uint32_t* dst) {
+  using L = Layout<P>;
+  using Rec = typename P::Rec;
+  constexpr int NW = L::kWords, T = (NW + 63) / 64;
+  unsigned long long mask = __ballot(active);
+  const int lane = __lane_id();
+  while (mask) {
+    const int src = __ffsll((long long)mask) - 1;
+    mask &= mask - 1;
+    const uint32_t* pw = base + (uint64_t)__shfl((unsigned long long)pidx, src) * NW;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(__shfl((unsigned long long)(uintptr_t)dst, src));
+    const int node = __shfl(d.node, src);
+    const int m = __shfl(d.out.n, src);
+    uint32_t nw[P::kNodeWords];
+#pragma unroll
+    for (int i = 0; i < P::kNodeWords; i++) nw[i] = __shfl(d.nw[i], src);
+    const int n = Net<P>::size(pw);
+    EmitAcc acc[T];
+#pragma unroll
+    for (int t = 0; t < T; t++) acc[t] = EmitAcc{0u, 0, 0};
+    for (int i = 0; i < m; i++) {
+      Rec r;
+      if constexpr (sizeof(Rec) == 8) {
+        r = (Rec)__shfl((unsigned long long)d.out.r[i], src);
+      } else {
+        r = (Rec)__shfl((unsigned)d.out.r[i], src);
+      }
+      const int pos = net_lower_bound<P>(pw, n, r) + i;
+#pragma unroll
+      for (int t = 0; t < T; t++) emit_acc_send<P>(acc[t], lane + 64 * t, r, pos);
+    }
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      const int o = lane + 64 * t;
+      if (o < NW) ow[o] = emit_word<P>(pw, n, m, node, nw, o, acc[t]);
+    }
+  }
 }
 
 template <class P>
@@ -107,6 +193,10 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // PB
   int* off = reinterpret_cast<int*>(fps + a.PB);           // PB + 1
   __shared__ int s_total;
+  __shared__ BlockResv s_resv;
+  __shared__ unsigned long long s_red[kBlock / 64];
+  // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
+  unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
 
   const uint64_t nchunks = (a.F + a.PB - 1) / a.PB;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -128,17 +218,18 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
       off[0] = 0;
       for (int j = 0; j < pb; j++) off[j + 1] += off[j];
       s_total = off[pb];
-      atomicAdd(&a.ctr->work_items, (unsigned long long)off[pb]);
+      c_work += (unsigned long long)off[pb];
     }
     __syncthreads();
     const int total = s_total;
     // 3. one lane per (parent, event)
     for (int base = 0; base < total; base += blockDim.x) {
       const int t = base + threadIdx.x;
-      bool is_new = false, is_valid = false, is_succ = false, route = false;
+      bool is_valid = false, route = false;
       int dest = 0, j = 0, k = 0;
       Fp f{0, 0};
       Delta<P> d;
+      d.out.n = 0;
       if (t < total) {
         int lo = 0, hi = pb;
         while (hi - lo > 1) {
@@ -150,7 +241,7 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
         const uint32_t* w = rows + j * NW;
         const int rc = delta_step<P>(w, k, d, prm, set);
         if (rc == STEP_OK) {
-          is_succ = true;
+          c_succ++;
           f = delta_fingerprint<P>(w, fps[j], d);
           if (ROUTE) dest = owner_of(f, a.W);
           if (ROUTE && dest != a.me) {
@@ -158,12 +249,13 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
           } else {
             const int ins = table_insert(a.table, f);
             if (ins == INS_NEW) {
-              is_new = true;
+              c_new++;
               int pi = -1;
               const NodeView view{w, P::kNodeWords, d.node, d.nw};
               const int v = judge_view<P>(view, prm, set, a.depth, &pi);
               if (v == V_VALID) {
-                is_valid = true;
+                if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = true;
+                else atomicAdd(&a.ctr->err_overflow, 1ull);
               } else if (v >= V_TERM_EXCEPTION) {
                 const unsigned long long slot = atomicAdd(&a.ctr->n_terminals, 1ull);
                 if (slot < kTermCap) a.terms[slot] = TerminalRec{v, pi, (uint32_t)k, 0u, p0 + j, f.hi};
@@ -174,52 +266,44 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
           }
         } else if (rc == STEP_EXCEPTION) {
           // exceptional states never equal another (Throwable identity): new and terminal
-          is_succ = true;
-          is_new = true;
+          c_succ++;
+          c_new++;
           const unsigned long long slot = atomicAdd(&a.ctr->n_terminals, 1ull);
           if (slot < kTermCap) a.terms[slot] = TerminalRec{V_TERM_EXCEPTION, -1, (uint32_t)k, 0u, p0 + j, fps[j].hi};
         } else if (rc == STEP_OVERFLOW) {
           atomicAdd(&a.ctr->err_overflow, 1ull);
         }
       }
-      const unsigned long long nsucc = __popcll(__ballot(is_succ));
-      const unsigned long long nnew = __popcll(__ballot(is_new));
-      if (__lane_id() == 0) {
-        if (nsucc) atomicAdd(&a.ctr->successors, nsucc);
-        if (nnew) atomicAdd(&a.ctr->new_states, nnew);
-      }
-      const unsigned long long idx = wave_reserve(&a.ctr->next_size, is_valid);
+      const unsigned long long idx = block_reserve(s_resv, &a.ctr->next_size, is_valid, 0, 1);
       const bool fits = is_valid && idx < a.next_cap;
-      unsigned long long ne = 0;
       if (fits) {
         const uint32_t* w = rows + j * NW;
-        if (materialize<P>(w, d, a.next + idx * NW)) {
-          a.next_fp[idx] = f;
-          a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
-          a.next_event[idx] = (uint32_t)k;
-          ne = (unsigned long long)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
-        } else {
-          atomicAdd(&a.ctr->err_overflow, 1ull);
+        a.next_fp[idx] = f;
+        a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
+        a.next_event[idx] = (uint32_t)k;
+        c_next_work += (unsigned long long)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
+      }
+      wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+      // beyond the estimated capacity: spill (parent, event); materialized after the level (rare)
+      const bool spill = is_valid && !fits;
+      if (__ballot(spill)) {
+        const unsigned long long sidx = wave_reserve(&a.ctr->spilled, spill);
+        if (spill) {
+          if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
+          else atomicAdd(&a.ctr->err_frontier, 1ull);
         }
       }
-      // beyond the estimated capacity: spill (parent, event); materialized after the level
-      const unsigned long long sidx = wave_reserve(&a.ctr->spilled, is_valid && !fits);
-      if (is_valid && !fits) {
-        if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
-        else atomicAdd(&a.ctr->err_frontier, 1ull);
-      }
-      {
-        unsigned long long s = ne;
-        for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-        if (__lane_id() == 0 && s) atomicAdd(&a.ctr->next_work, s);
-      }
       if (ROUTE) {
-        const unsigned long long ridx = wave_reserve_dest(a.rc->out, route, dest, a.W);
+        const unsigned long long ridx = block_reserve(s_resv, a.rc->out, route, dest, a.W);
         if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
       }
     }
     __syncthreads();  // LDS is reused by the next chunk
   }
+  block_flush(s_red, &a.ctr->successors, c_succ);
+  block_flush(s_red, &a.ctr->new_states, c_new);
+  block_flush(s_red, &a.ctr->next_work, c_next_work);
+  block_flush(s_red, &a.ctr->work_items, c_work);
 }
 
 // Materializes spilled VALID states (already inserted, counted and judged) at next_size.
@@ -230,26 +314,33 @@ __global__ void __launch_bounds__(kBlock) k_unspill(const uint64_t* items, uint6
                                                     int32_t me, LevelCounters* ctr, typename P::Params prm,
                                                     DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
+  __shared__ unsigned long long s_red[kBlock / 64];
+  unsigned long long c_next_work = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
     unsigned long long ne = 0;
+    bool ok = false;
+    uint64_t parent = 0;
+    Delta<P> d;
+    d.out.n = 0;
     if (i < n) {
-      const uint64_t parent = items[i] >> 20;
+      parent = items[i] >> 20;
       const int k = (int)(items[i] & 0xfffff);
       const uint32_t* w = cur + parent * NW;
-      Delta<P> d;
       delta_step<P>(w, k, d, prm, set);
       const uint64_t idx = base_idx + i;
-      if (!materialize<P>(w, d, next + idx * NW)) atomicAdd(&ctr->err_overflow, 1ull);
+      ok = Net<P>::size(w) + d.out.n <= P::kNetCap;
+      if (!ok) atomicAdd(&ctr->err_overflow, 1ull);
       next_fp[idx] = delta_fingerprint<P>(w, cur_fp[parent], d);
       next_parent[idx] = ((uint64_t)me << 48) | parent;
       next_event[idx] = (uint32_t)k;
       ne = (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
-    for (int o = 32; o > 0; o >>= 1) ne += __shfl_xor(ne, o);
-    if (__lane_id() == 0 && ne) atomicAdd(&ctr->next_work, ne);
+    wave_emit<P>(ok, cur, parent, d, next + (base_idx + i) * NW);
+    c_next_work += ne;
   }
+  block_flush(s_red, &ctr->next_work, c_next_work);
 }
 
 // Inserts the initial state's fingerprint and judges it (BFS.initSearch + exploreNode's
@@ -280,6 +371,9 @@ struct ProbeArgs {
 };
 
 __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
+  __shared__ BlockResv s_resv;
+  __shared__ unsigned long long s_red[kBlock / 64];
+  unsigned long long c_new = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -293,15 +387,15 @@ __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
       if (ins == INS_NEW) {
         is_new = true;
         item = r.item;
+        c_new++;
       } else if (ins == INS_FULL) {
         atomicAdd(&a.ctr->err_table, 1ull);
       }
     }
-    const unsigned long long nnew = __popcll(__ballot(is_new));
-    if (__lane_id() == 0 && nnew) atomicAdd(&a.ctr->new_states, nnew);
-    const unsigned long long idx = wave_reserve_dest(a.rc->out, is_new, src, a.W);
+    const unsigned long long idx = block_reserve(s_resv, a.rc->out, is_new, src, a.W);
     if (is_new) a.out_items[(uint64_t)src * a.cap_v + idx] = item;
   }
+  block_flush(s_red, &a.ctr->new_states, c_new);
 }
 
 // A routed VALID new state: row, fingerprint, parent pointer, event.
@@ -331,6 +425,7 @@ struct MaterializeArgs {
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
+  __shared__ BlockResv s_resv;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -357,16 +452,20 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
         if (slot < kTermCap) a.terms[slot] = TerminalRec{v, pi, (uint32_t)k, 0u, parent, f.hi};
       }
     }
-    const unsigned long long idx = wave_reserve_dest(a.rc->out, ship, dest, a.W);
+    const unsigned long long idx = block_reserve(s_resv, a.rc->out, ship, dest, a.W);
+    StateRec<P>* r = a.out + (uint64_t)dest * a.cap_s + idx;
     if (ship) {
-      StateRec<P>* r = a.out + (uint64_t)dest * a.cap_s + idx;
       const uint32_t* w = a.cur + parent * NW;
-      if (!materialize<P>(w, d, r->w)) atomicAdd(&a.ctr->err_overflow, 1ull);
+      if (Net<P>::size(w) + d.out.n > P::kNetCap) {
+        atomicAdd(&a.ctr->err_overflow, 1ull);
+        ship = false;
+      }
       r->fp = f;
       r->parent = ((uint64_t)a.me << 48) | parent;
       r->event = (uint32_t)k;
       r->pad = (uint32_t)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
+    wave_emit<P>(ship, a.cur, parent, d, r->w);
   }
 }
 
@@ -375,28 +474,37 @@ __global__ void __launch_bounds__(kBlock) k_append_received(const StateRec<P>* i
                                                             uint64_t* next_parent, uint32_t* next_event,
                                                             uint64_t next_cap, LevelCounters* ctr) {
   constexpr int NW = Layout<P>::kWords;
+  __shared__ BlockResv s_resv;
+  __shared__ unsigned long long s_red[kBlock / 64];
+  unsigned long long c_next_work = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
     const bool ok = i < n;
-    const unsigned long long idx = wave_reserve(&ctr->next_size, ok);
-    unsigned long long ne = 0;
+    const unsigned long long idx = block_reserve(s_resv, &ctr->next_size, ok, 0, 1);
+    bool copy = false;
     if (ok) {
       if (idx < next_cap) {
-        const uint4* s = reinterpret_cast<const uint4*>(in[i].w);
-        uint4* dd = reinterpret_cast<uint4*>(next + idx * NW);
-        for (int q = 0; q < NW / 4; q++) dd[q] = s[q];
+        copy = true;
         next_fp[idx] = in[i].fp;
         next_parent[idx] = in[i].parent;
         next_event[idx] = in[i].event;
-        ne = in[i].pad;  // enabled events of the state (next level's work)
+        c_next_work += in[i].pad;  // enabled events of the state (next level's work)
       } else {
         atomicAdd(&ctr->err_frontier, 1ull);
       }
     }
-    for (int o = 32; o > 0; o >>= 1) ne += __shfl_xor(ne, o);
-    if (__lane_id() == 0 && ne) atomicAdd(&ctr->next_work, ne);
+    // rows copied by the whole wave, one row at a time (coalesced)
+    unsigned long long mask = __ballot(copy);
+    while (mask) {
+      const int src = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const uint32_t* from = in[base + threadIdx.x - __lane_id() + src].w;
+      uint32_t* to = next + __shfl(idx, src) * NW;
+      for (int o = __lane_id(); o < NW; o += 64) to[o] = from[o];
+    }
   }
+  block_flush(s_red, &ctr->next_work, c_next_work);
 }
 
 }  // namespace dsl

@@ -212,7 +212,25 @@ struct Delta {
   Sender<P> out;
 };
 
-// Applies event k of parent w: fills the delta; returns a StepRc.
+// Canonical send list of a delta: drops the sends already in the parent's network set and sorts
+// the rest ascending, i.e. exactly the records the successor adds to the set, in merge order.
+template <class P>
+DSL_HD void canon_sends(const uint32_t* w, Delta<P>& d) {
+  int m = 0;
+  for (int j = 0; j < d.out.n; j++) {
+    const auto r = d.out.r[j];
+    if (Net<P>::contains(w, r)) continue;
+    int k = m++;
+    while (k > 0 && r < d.out.r[k - 1]) {
+      d.out.r[k] = d.out.r[k - 1];
+      k--;
+    }
+    d.out.r[k] = r;
+  }
+  d.out.n = m;
+}
+
+// Applies event k of parent w: fills the delta (its send list canonical); returns a StepRc.
 template <class P>
 DSL_HD int delta_step(const uint32_t* w, int k, Delta<P>& d, const typename P::Params& prm, const DevSettings& set) {
   const int e = locate_event<P>(w, prm, set, k);
@@ -233,6 +251,7 @@ DSL_HD int delta_step(const uint32_t* w, int k, Delta<P>& d, const typename P::P
     rc = P::on_timer(d.node, d.nw, x & 255, d.out, prm);
   }
   if (d.out.overflow && rc == STEP_OK) rc = STEP_OVERFLOW;
+  if (rc == STEP_OK) canon_sends<P>(w, d);
   return rc;
 }
 
@@ -241,8 +260,7 @@ template <class P>
 DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
   Fp f = fp_xor(parent, node_hash<P>(d.node, w + d.node * P::kNodeWords));
   f = fp_xor(f, node_hash<P>(d.node, d.nw));
-  for (int j = 0; j < d.out.n; j++)
-    if (!Net<P>::contains(w, d.out.r[j])) f = fp_xor(f, msg_hash<P>(d.out.r[j]));
+  for (int j = 0; j < d.out.n; j++) f = fp_xor(f, msg_hash<P>(d.out.r[j]));  // canonical: all new
   return f;
 }
 
@@ -254,12 +272,79 @@ DSL_HD int delta_event_count(const uint32_t* w, int parent_events, const Delta<P
   int n = parent_events;
   if (deliver_timers(set, d.node))
     n += P::num_timer_events(d.node, d.nw, prm) - P::num_timer_events(d.node, w + d.node * P::kNodeWords, prm);
-  for (int j = 0; j < d.out.n; j++) {
+  for (int j = 0; j < d.out.n; j++) {  // canonical: every send is new to the set
     const auto r = d.out.r[j];
-    if (!Net<P>::contains(w, r) && (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))))
-      n++;
+    if (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))) n++;
   }
   return n;
+}
+
+// ---- merged-row emission ----------------------------------------------------------------------
+// The successor row = parent row with one node's words replaced and the canonical sends merged
+// into the sorted record array. Output word o is computed independently of the others, so a
+// wavefront writes a row cooperatively (kernels.hpp: wave_emit, 64 lanes x consecutive words,
+// coalesced) and nothing is ever read back from the destination. For a record slot q the
+// accumulator collects, over the sends s_i (ascending) with merged position pos_i =
+// lower_bound(parent records, s_i) + i: whether some pos_i == q (then the word is s_i's) and how
+// many pos_i < q (then the word is parent record q - before).
+struct EmitAcc {
+  uint32_t val;
+  int before;
+  int hit;
+};
+
+template <class P>
+DSL_HD int net_lower_bound(const uint32_t* w, int n, typename P::Rec r) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (Net<P>::at(w, mid) < r) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+template <class P>
+DSL_HD void emit_acc_send(EmitAcc& a, int o, typename P::Rec s, int pos) {
+  using L = Layout<P>;
+  if (o < L::kRecBase) return;
+  const int q = (o - L::kRecBase) / L::kRecWords, half = (o - L::kRecBase) % L::kRecWords;
+  if (q == pos) {
+    a.hit = 1;
+    a.val = half ? (uint32_t)((uint64_t)s >> 32) : (uint32_t)s;
+  } else if (pos < q) {
+    a.before++;
+  }
+}
+
+template <class P>
+DSL_HD uint32_t emit_word(const uint32_t* pw, int n, int m, int node, const uint32_t* nw, int o, const EmitAcc& a) {
+  using L = Layout<P>;
+  if (o < L::kNetCount) {
+    uint32_t v = pw[o];
+#pragma unroll
+    for (int i = 0; i < P::kNodeWords; i++)
+      if (o == node * P::kNodeWords + i) v = nw[i];
+    return v;
+  }
+  if (o == L::kNetCount) return (uint32_t)(n + m);
+  if (o < L::kRecBase) return 0u;
+  if (a.hit) return a.val;
+  const int q = (o - L::kRecBase) / L::kRecWords, half = (o - L::kRecBase) % L::kRecWords;
+  const int pq = q - a.before;
+  return pq < n ? pw[L::kRecBase + pq * L::kRecWords + half] : 0u;
+}
+
+// Host/scalar form of the emission (tests/hostcheck checks it against materialize()).
+template <class P>
+DSL_HD bool emit_row(const uint32_t* pw, const Delta<P>& d, uint32_t* out) {
+  const int n = Net<P>::size(pw), m = d.out.n;
+  if (n + m > P::kNetCap) return false;
+  for (int o = 0; o < Layout<P>::kWords; o++) {
+    EmitAcc a{0u, 0, 0};
+    for (int i = 0; i < m; i++) emit_acc_send<P>(a, o, d.out.r[i], net_lower_bound<P>(pw, n, d.out.r[i]) + i);
+    out[o] = emit_word<P>(pw, n, m, d.node, d.nw, o, a);
+  }
+  return true;
 }
 
 // Materializes the successor (parent w + delta) into out; false on network overflow.

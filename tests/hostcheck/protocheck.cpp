@@ -55,7 +55,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
-  long long fp_mismatch = 0;
+  long long fp_mismatch = 0, emit_mismatch = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
@@ -89,6 +89,10 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         printf("{\"error\":\"overflow\"}\n");
         return 1;
       }
+      {  // the kernels' word-parallel merge (emit_word) must produce the same row
+        S e;
+        if (!emit_row<P>(n.s.w, dl, e.w) || std::memcmp(e.w, t.w, sizeof(S)) != 0) emit_mismatch++;
+      }
       const Fp f = delta_fingerprint<P>(n.s.w, n.fp, dl);
       const Fp g = full_fingerprint<P>(t.w);
       if (f.hi != g.hi || f.lo != g.lo) fp_mismatch++;
@@ -111,8 +115,8 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   if (best != 99)
     end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
   unsigned long long total = 0;
-  printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"per_depth\":[", end, tdepth,
-         (int)sizeof(S), fp_mismatch);
+  printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"emit_mismatch\":%lld,"
+         "\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch, emit_mismatch);
   for (size_t i = 0; i < per.size(); i++) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
