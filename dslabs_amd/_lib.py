@@ -9,7 +9,10 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdslabs_hip.so")
+# DSL_LIB_VARIANT selects an instrumented in-tree build (e.g. "phases" -> libdslabs_hip_phases.so,
+# built by tools/build_variant.sh); the default is the product library.
+_VARIANT = os.environ.get("DSL_LIB_VARIANT", "")
+LIB_PATH = os.path.join(HERE, "libdslabs_hip%s.so" % ("_" + _VARIANT if _VARIANT else ""))
 
 DSL_MAX_NODES = 32
 DSL_MAX_PREDICATES = 16

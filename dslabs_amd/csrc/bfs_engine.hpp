@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -524,6 +525,15 @@ struct BfsEngine : EngineBase {
           stats.expand_ms += kms;
           stats.expand_launches++;
         }
+#ifdef DSL_PHASES
+        for (auto& S : sh) {
+          const auto& q = S.lc.phase;
+          fprintf(stderr, "[phases] depth %d F=%llu work=%llu new=%llu cycles:", depth + 1, (unsigned long long)S.F,
+                  (unsigned long long)S.lc.work_items, (unsigned long long)S.lc.new_states);
+          for (int i = 0; i < 8; i++) fprintf(stderr, " %.3g", (double)q[i]);
+          fprintf(stderr, "\n");
+        }
+#endif
         // global counts, errors, terminal selection
         std::vector<uint64_t> gsum(8, 0);
         uint64_t enc = ~0ull;

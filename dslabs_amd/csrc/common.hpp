@@ -64,6 +64,41 @@ struct Packed {
   DSL_HD void setbit(int b) { w[b >> 5] |= 1u << (b & 31); }
 };
 
+// Word i of a node's N words for a run-time i: a select chain, so a node held in a per-lane
+// array stays in VGPRs (a dynamically indexed private array is placed in scratch, and every
+// handler access would then be a memory round trip). A constant i folds to one access.
+template <int N>
+DSL_HD uint32_t sel_word(const uint32_t* w, int i) {
+  uint32_t v = w[0];
+#pragma unroll
+  for (int k = 1; k < N; k++) {
+    uint32_t x = w[k];
+#ifdef __HIP_DEVICE_COMPILE__
+    // keeps the selection on VALUES: otherwise the optimizer folds the chain into one load
+    // from a selected address, i.e. back into a dynamically indexed (scratch) array
+    asm("" : "+v"(x));
+#endif
+    v = (i == k) ? x : v;
+  }
+  return v;
+}
+template <int N>
+DSL_HD void sel_put(uint32_t* w, int i, uint32_t v) {
+#pragma unroll
+  for (int k = 0; k < N; k++) w[k] = (i == k) ? v : w[k];
+}
+// Bit-field get/put over a node's N words (fields never straddle a word).
+template <int N>
+DSL_HD int field_get(const uint32_t* w, int bit, int width) {
+  return (int)((sel_word<N>(w, bit >> 5) >> (bit & 31)) & ((1u << width) - 1u));
+}
+template <int N>
+DSL_HD void field_put(uint32_t* w, int bit, int width, int v) {
+  const uint32_t m = ((1u << width) - 1u) << (bit & 31);
+  const int i = bit >> 5;
+  sel_put<N>(w, i, (sel_word<N>(w, i) & ~m) | (((uint32_t)v << (bit & 31)) & m));
+}
+
 // How a successor is judged (Search.checkState, Search.java:162-231).
 enum Verdict : int { V_VALID = 0, V_PRUNED = 1, V_TERM_EXCEPTION = 2, V_TERM_INVARIANT = 3, V_TERM_GOAL = 4 };
 

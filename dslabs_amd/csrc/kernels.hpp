@@ -22,6 +22,7 @@ namespace dsl {
 constexpr int kBlock = 256;
 constexpr uint32_t kTermCap = 1024;
 constexpr int kMaxShards = 16;
+constexpr int kWin = 1024;  // work items per class-sorted window of k_level
 
 struct LevelCounters {
   unsigned long long new_states;    // newly discovered successors (all verdicts)
@@ -34,7 +35,20 @@ struct LevelCounters {
   unsigned long long work_items;    // (state, event) pairs of this level
   unsigned long long next_work;     // enabled events of the appended states (= next level's work)
   unsigned long long spilled;       // VALID states beyond the next frontier's capacity (spill list)
+  unsigned long long phase[8];      // DSL_PHASES builds only: shader cycles per k_level phase
 };
+
+// Phase timing (instrumented builds, -DDSL_PHASES): wave-level shader-clock deltas per phase of
+// k_level, summed per workgroup and flushed once. Product builds compile it away.
+#ifdef DSL_PHASES
+#define PH_DECL unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long ph_t = clock64();
+#define PH_MARK(i) do { const unsigned long long ph_n = clock64(); ph_acc[i] += ph_n - ph_t; ph_t = ph_n; } while (0)
+#define PH_FLUSH(red, ctr) do { for (int ph_i = 0; ph_i < 8; ph_i++) block_flush(red, &(ctr)->phase[ph_i], __lane_id() == 0 ? ph_acc[ph_i] : 0ull); } while (0)
+#else
+#define PH_DECL
+#define PH_MARK(i) do { } while (0)
+#define PH_FLUSH(red, ctr) do { } while (0)
+#endif
 
 struct TerminalRec {
   int32_t verdict;  // V_TERM_*
@@ -143,16 +157,19 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
     EmitAcc acc[T];
 #pragma unroll
     for (int t = 0; t < T; t++) acc[t] = EmitAcc{0u, 0, 0};
-    for (int i = 0; i < m; i++) {
-      Rec r;
-      if constexpr (sizeof(Rec) == 8) {
-        r = (Rec)__shfl((unsigned long long)d.out.r[i], src);
-      } else {
-        r = (Rec)__shfl((unsigned)d.out.r[i], src);
-      }
-      const int pos = net_lower_bound<P>(pw, n, r) + i;
 #pragma unroll
-      for (int t = 0; t < T; t++) emit_acc_send<P>(acc[t], lane + 64 * t, r, pos);
+    for (int i = 0; i < P::kMaxSends; i++) {  // constant indices: the send list stays in VGPRs
+      if (i < m) {
+        Rec r;
+        if constexpr (sizeof(Rec) == 8) {
+          r = (Rec)__shfl((unsigned long long)d.out.r[i], src);
+        } else {
+          r = (Rec)__shfl((unsigned)d.out.r[i], src);
+        }
+        const int pos = net_lower_bound<P>(pw, n, r) + i;
+#pragma unroll
+        for (int t = 0; t < T; t++) emit_acc_send<P>(acc[t], lane + 64 * t, r, pos);
+      }
     }
 #pragma unroll
     for (int t = 0; t < T; t++) {
@@ -186,7 +203,12 @@ struct LevelArgs {
 };
 
 template <class P, bool ROUTE>
-__global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
+// Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel; the few values the
+// register allocator then spills are cold (measured: 2 waves/SIMD at 175 VGPRs is 1.5x slower).
+#ifndef DSL_KLEVEL_ATTR
+#define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
+__global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // PB * NW
@@ -194,9 +216,14 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
   int* off = reinterpret_cast<int*>(fps + a.PB);           // PB + 1
   __shared__ int s_total;
   __shared__ BlockResv s_resv;
+  __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   __shared__ unsigned long long s_red[kBlock / 64];
+  __shared__ int s_hist[16];
+  __shared__ uint8_t s_par[kWin], s_cls[kWin];
+  __shared__ uint16_t s_perm[kWin];
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
   unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
+  PH_DECL
 
   const uint64_t nchunks = (a.F + a.PB - 1) / a.PB;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -222,36 +249,71 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
     }
     __syncthreads();
     const int total = s_total;
-    // 3. one lane per (parent, event)
-    for (int base = 0; base < total; base += blockDim.x) {
+    PH_MARK(0);  // staging + event count + scan
+    // 3. the chunk's work items in windows of kWin: grouped by handler class (LDS counting sort),
+    //    then one lane per (parent, event), so a wavefront mostly runs one handler
+    for (int w0 = 0; w0 < total; w0 += kWin) {
+    const int wn = min(kWin, total - w0);
+    if (threadIdx.x < 16) s_hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < wn; t += blockDim.x) {
+      const int g = w0 + t;
+      int lo = 0, hi = pb;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= g) lo = mid; else hi = mid;
+      }
+      const int c = event_class<P>(rows + lo * NW, prm, set, g - off[lo]);
+      s_par[t] = (uint8_t)lo;
+      s_cls[t] = (uint8_t)c;
+      atomicAdd(&s_hist[c], 1);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int acc = 0;
+      for (int c = 0; c < 16; c++) {
+        const int h = s_hist[c];
+        s_hist[c] = acc;
+        acc += h;
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < wn; t += blockDim.x) s_perm[atomicAdd(&s_hist[s_cls[t]], 1)] = (uint16_t)t;
+    __syncthreads();
+    PH_MARK(7);  // classify + sort
+    for (int base = 0; base < wn; base += blockDim.x) {
       const int t = base + threadIdx.x;
       bool is_valid = false, route = false;
       int dest = 0, j = 0, k = 0;
       Fp f{0, 0};
       Delta<P> d;
       d.out.n = 0;
-      if (t < total) {
-        int lo = 0, hi = pb;
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (off[mid] <= t) lo = mid; else hi = mid;
-        }
-        j = lo;
-        k = t - off[lo];
+      if (t < wn) {
+        const int u = s_perm[t];
+        j = s_par[u];
+        k = w0 + u - off[j];
         const uint32_t* w = rows + j * NW;
         const int rc = delta_step<P>(w, k, d, prm, set);
+        PH_MARK(1);  // decode + handler + canonical sends
         if (rc == STEP_OK) {
           c_succ++;
           f = delta_fingerprint<P>(w, fps[j], d);
+          PH_MARK(2);  // fingerprint
           if (ROUTE) dest = owner_of(f, a.W);
           if (ROUTE && dest != a.me) {
             route = true;
           } else {
             const int ins = table_insert(a.table, f);
+            PH_MARK(3);  // visited-table probe / insert
             if (ins == INS_NEW) {
               c_new++;
               int pi = -1;
-              const NodeView view{w, P::kNodeWords, d.node, d.nw};
+              // the changed node's words go through LDS: a view pointing at the register array
+              // would take its address and push the whole delta into scratch
+              uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
+#pragma unroll
+              for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+              const NodeView view{w, P::kNodeWords, d.node, my_nw};
               const int v = judge_view<P>(view, prm, set, a.depth, &pi);
               if (v == V_VALID) {
                 if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = true;
@@ -274,7 +336,9 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
           atomicAdd(&a.ctr->err_overflow, 1ull);
         }
       }
+      PH_MARK(4);  // judge (+ divergence wait)
       const unsigned long long idx = block_reserve(s_resv, &a.ctr->next_size, is_valid, 0, 1);
+      PH_MARK(5);  // reservation
       const bool fits = is_valid && idx < a.next_cap;
       if (fits) {
         const uint32_t* w = rows + j * NW;
@@ -284,6 +348,7 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
         c_next_work += (unsigned long long)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
       }
       wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+      PH_MARK(6);  // history + row emission
       // beyond the estimated capacity: spill (parent, event); materialized after the level (rare)
       const bool spill = is_valid && !fits;
       if (__ballot(spill)) {
@@ -298,8 +363,11 @@ __global__ void __launch_bounds__(kBlock) k_level(LevelArgs<P> a, typename P::Pa
         if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
       }
     }
+    __syncthreads();  // the window's LDS arrays are reused by the next window
+    }
     __syncthreads();  // LDS is reused by the next chunk
   }
+  PH_FLUSH(s_red, a.ctr);
   block_flush(s_red, &a.ctr->successors, c_succ);
   block_flush(s_red, &a.ctr->new_states, c_new);
   block_flush(s_red, &a.ctr->next_work, c_next_work);
@@ -426,6 +494,7 @@ template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   __shared__ BlockResv s_resv;
+  __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -443,7 +512,10 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       f = delta_fingerprint<P>(w, a.cur_fp[parent], d);
       dest = owner_of(f, a.W);
       int pi = -1;
-      const NodeView view{w, P::kNodeWords, d.node, d.nw};
+      uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
+#pragma unroll
+      for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+      const NodeView view{w, P::kNodeWords, d.node, my_nw};
       const int v = judge_view<P>(view, prm, set, a.depth, &pi);
       if (v == V_VALID) {
         ship = true;

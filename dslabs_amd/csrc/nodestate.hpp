@@ -80,20 +80,30 @@ struct Net {
 };
 
 // Sends emitted by one handler invocation (duplicates collapse, as in the network set).
+// Every access to r[] uses a compile-time index (fully unrolled loops predicated on i < n), so
+// the list lives in VGPRs; a dynamically indexed per-lane array would be placed in scratch and
+// every send would pay a memory round trip.
 template <class P>
 struct Sender {
   using Rec = typename P::Rec;
+  static constexpr int K = P::kMaxSends;
   int n = 0;
   bool overflow = false;
-  Rec r[P::kMaxSends];
+  Rec r[K];
   DSL_HD void send(Rec x) {
-    for (int i = 0; i < n; i++)
-      if (r[i] == x) return;
-    if (n >= P::kMaxSends) {
+    bool dup = false;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+      if (i < n && r[i] == x) dup = true;
+    if (dup) return;
+    if (n >= K) {
       overflow = true;
       return;
     }
-    r[n++] = x;
+#pragma unroll
+    for (int i = 0; i < K; i++)
+      if (i == n) r[i] = x;
+    n++;
   }
 };
 
@@ -204,6 +214,13 @@ DSL_HD int locate_event(const uint32_t* w, const typename P::Params& prm, const 
   return INT32_MIN;
 }
 
+// Handler class of event k (messages: P::msg_class, timers: 15).
+template <class P>
+DSL_HD int event_class(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
+  const int e = locate_event<P>(w, prm, set, k);
+  return e >= 0 ? P::msg_class(Net<P>::at(w, e)) : 15;
+}
+
 // A successor as a delta of its parent.
 template <class P>
 struct Delta {
@@ -216,16 +233,30 @@ struct Delta {
 // the rest ascending, i.e. exactly the records the successor adds to the set, in merge order.
 template <class P>
 DSL_HD void canon_sends(const uint32_t* w, Delta<P>& d) {
-  int m = 0;
-  for (int j = 0; j < d.out.n; j++) {
-    const auto r = d.out.r[j];
-    if (Net<P>::contains(w, r)) continue;
-    int k = m++;
-    while (k > 0 && r < d.out.r[k - 1]) {
-      d.out.r[k] = d.out.r[k - 1];
-      k--;
+  constexpr int K = P::kMaxSends;
+  const int n = d.out.n;
+  int m = 0;  // sorted prefix r[0..m) of kept sends; m <= i, so r[i] is read before it is overwritten
+#pragma unroll
+  for (int i = 0; i < K; i++) {
+    if (i < n) {
+      const auto x = d.out.r[i];
+      if (!Net<P>::contains(w, x)) {
+        bool done = false;
+#pragma unroll
+        for (int j = i; j >= 1; j--) {
+          if (j <= m && !done) {
+            if (x < d.out.r[j - 1]) {
+              d.out.r[j] = d.out.r[j - 1];
+            } else {
+              d.out.r[j] = x;
+              done = true;
+            }
+          }
+        }
+        if (!done) d.out.r[0] = x;
+        m++;
+      }
     }
-    d.out.r[k] = r;
   }
   d.out.n = m;
 }
@@ -260,7 +291,9 @@ template <class P>
 DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
   Fp f = fp_xor(parent, node_hash<P>(d.node, w + d.node * P::kNodeWords));
   f = fp_xor(f, node_hash<P>(d.node, d.nw));
-  for (int j = 0; j < d.out.n; j++) f = fp_xor(f, msg_hash<P>(d.out.r[j]));  // canonical: all new
+#pragma unroll
+  for (int j = 0; j < P::kMaxSends; j++)
+    if (j < d.out.n) f = fp_xor(f, msg_hash<P>(d.out.r[j]));  // canonical: all new
   return f;
 }
 
@@ -272,9 +305,12 @@ DSL_HD int delta_event_count(const uint32_t* w, int parent_events, const Delta<P
   int n = parent_events;
   if (deliver_timers(set, d.node))
     n += P::num_timer_events(d.node, d.nw, prm) - P::num_timer_events(d.node, w + d.node * P::kNodeWords, prm);
-  for (int j = 0; j < d.out.n; j++) {  // canonical: every send is new to the set
-    const auto r = d.out.r[j];
-    if (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))) n++;
+#pragma unroll
+  for (int j = 0; j < P::kMaxSends; j++) {  // canonical: every send is new to the set
+    if (j < d.out.n) {
+      const auto r = d.out.r[j];
+      if (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))) n++;
+    }
   }
   return n;
 }

@@ -49,11 +49,11 @@ struct MultiPaxos {
   enum { M_REQUEST = 0, M_REPLY, M_P1A, M_P1B, M_P2A, M_P2B, M_DECISION, M_HEARTBEAT, T_TICK = 8, T_CLIENT = 9 };
   enum { EMPTY = 0, ACCEPTED = 1, CHOSEN = 2 };
 
-  static DSL_HD int get(const uint32_t* w, int bit, int width) { return (w[bit >> 5] >> (bit & 31)) & ((1 << width) - 1); }
-  static DSL_HD void put(uint32_t* w, int bit, int width, int v) {
-    uint32_t m = ((1u << width) - 1) << (bit & 31);
-    w[bit >> 5] = (w[bit >> 5] & ~m) | (((uint32_t)v << (bit & 31)) & m);
-  }
+  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // by class so that the lanes of a wavefront run the same handler.
+  static DSL_HD int msg_class(Rec r) { return m_type(r); }
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
   // ---- server fields ------------------------------------------------------------------------------
   static DSL_HD uint32_t entry(const uint32_t* w, int slot) { return get(w, 32 + 16 * (slot - 1), 16); }
   static DSL_HD void set_entry(uint32_t* w, int slot, uint32_t e) { put(w, 32 + 16 * (slot - 1), 16, (int)e); }

@@ -41,11 +41,11 @@ struct PingPong {
   static DSL_HD int rec_from(Rec r) { return rec_type(r) ? 0 : rec_client(r); }
   static DSL_HD int rec_to(Rec r) { return rec_type(r) ? rec_client(r) : 0; }
 
-  static DSL_HD int get(const uint32_t* w, int bit, int width) { return (w[bit >> 5] >> (bit & 31)) & ((1 << width) - 1); }
-  static DSL_HD void put(uint32_t* w, int bit, int width, int v) {
-    uint32_t m = ((1u << width) - 1) << (bit & 31);
-    w[bit >> 5] = (w[bit >> 5] & ~m) | (((uint32_t)v << (bit & 31)) & m);
-  }
+  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // by class so that the lanes of a wavefront run the same handler.
+  static DSL_HD int msg_class(Rec r) { return rec_type(r); }
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
   static DSL_HD int ping(const uint32_t* w) { return get(w, 0, 4); }
   static DSL_HD int pong(const uint32_t* w) { return get(w, 4, 4); }
   static DSL_HD int nres(const uint32_t* w) { return get(w, 8, 4); }

@@ -44,11 +44,11 @@ struct SIPaxos {
   static DSL_HD int r_an(Rec r) { return (r >> 8) & 0xff; }
   static DSL_HD int r_av(Rec r) { return r & 3; }
 
-  static DSL_HD int get(const uint32_t* w, int bit, int width) { return (w[bit >> 5] >> (bit & 31)) & ((1 << width) - 1); }
-  static DSL_HD void put(uint32_t* w, int bit, int width, int v) {
-    uint32_t m = ((1u << width) - 1) << (bit & 31);
-    w[bit >> 5] = (w[bit >> 5] & ~m) | (((uint32_t)v << (bit & 31)) & m);
-  }
+  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // by class so that the lanes of a wavefront run the same handler.
+  static DSL_HD int msg_class(Rec r) { return r_type(r); }
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
   // proposer fields
   static DSL_HD int has_proposed(const uint32_t* w) { return get(w, 0, 1); }
   static DSL_HD int prep_fin(const uint32_t* w) { return get(w, 1, 1); }
