@@ -265,12 +265,15 @@ struct BfsEngine : EngineBase {
   }
 
   // Parents per workgroup chunk: about three passes of 256 lanes at the observed branching,
-  // within 64 KiB of LDS.
-  int chunk_parents() const {
+  // within the LDS budget of 4 resident workgroups per CU; a small level is spread over at least
+  // ~1024 workgroups instead (one short pass each), since its time is the serial latency chain
+  // of one chunk, not throughput.
+  int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
-    int lds_max = (int)((64 * 1024 - 64) / per);
+    int lds_max = (int)((24 * 1024) / per);
     int want = (int)((3 * kBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
-    int pb = std::max(1, std::min({want, lds_max, kBlock}));
+    const int spread = (int)std::max<uint64_t>(1, (F + 1023) / 1024);
+    int pb = std::max(1, std::min({want, lds_max, kBlock, spread}));
     return pb;
   }
 
@@ -374,7 +377,9 @@ struct BfsEngine : EngineBase {
         // The next frontier gets min(work, 4F) rows (typical growth is ~3 new states per
         // parent); VALID states beyond that are spilled as 8-byte items and materialized after
         // the kernel, so the estimate never fails and never reserves the worst case.
-        const int PB = chunk_parents();
+        uint64_t Fmax = 0;
+        for (auto& S : sh) Fmax = std::max(Fmax, S.F);
+        const int PB = chunk_parents(Fmax);
         for (auto& S : sh) {
           const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 1 << 16)) + 1;
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
@@ -429,9 +434,11 @@ struct BfsEngine : EngineBase {
         // spilled VALID states: grow the next frontier and materialize them after the local rows
         for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
         DSL_HIP(hipStreamSynchronize(stream));
+        bool unspilled = false;
         for (auto& S : sh) {
           const uint64_t ns = std::min<uint64_t>(S.lc.spilled, S.spill_cap);
           if (!ns || S.lc.err_frontier || S.lc.err_overflow) continue;
+          unspilled = true;
           const uint64_t keep = S.launch_cap, need = keep + ns + 1;
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
           DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
@@ -517,8 +524,10 @@ struct BfsEngine : EngineBase {
             }
           }
         }
-        for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
-        DSL_HIP(hipStreamSynchronize(stream));
+        if (W > 1 || unspilled) {  // counters changed after the first read
+          for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+          DSL_HIP(hipStreamSynchronize(stream));
+        }
         {
           float kms = 0;
           (void)hipEventElapsedTime(&kms, ev0, ev1);
