@@ -104,7 +104,10 @@ struct BfsEngine : EngineBase {
     uint64_t spill_cap = 0;
     uint64_t F = 0;
     uint64_t work = 0;        // enabled events of the current frontier (exact)
-    uint64_t launch_cap = 0;  // next-frontier rows available to k_level
+    std::vector<uint64_t> seg_base, seg_cnt;  // row ranges of the current frontier
+    unsigned long long* seg_ctr = nullptr;    // kSegs reservation counters
+    uint64_t segcap = 0;
+    int nseg = 1;
     std::vector<uint64_t> level_base, level_size;
     uint64_t cap_fp = 0, cap_v = 0, cap_s = 0;
     uint64_t n_in_fp = 0, n_in_items = 0, n_in_st = 0;
@@ -140,6 +143,7 @@ struct BfsEngine : EngineBase {
     std::memset(s.timers_active, -1, sizeof(s.timers_active));
     hset = s;
     resolve_settings(hset, P::num_nodes(prm), &P::known_predicate, &dset);
+    set_pred_reads<P>(dset, prm);
     const int nlocal = comm ? 1 : W;
     sh.resize(nlocal);
     for (int i = 0; i < nlocal; i++) sh[i].gid = comm ? comm->rank() : i;
@@ -149,7 +153,7 @@ struct BfsEngine : EngineBase {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,    s.cur,   s.next,   s.cur_fp,    s.next_fp, s.hist_parent,
                       s.hist_event, s.ctr, s.terms,  s.rc,        s.seed,    s.out_fp,
-                      s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill};
+                      s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.seg_ctr};
       for (void* q : ptrs) (void)hipFree(q);
     }
     if (ev0) (void)hipEventDestroy(ev0);
@@ -161,7 +165,10 @@ struct BfsEngine : EngineBase {
   int state_bytes() const override { return (int)sizeof(typename P::State); }
   int set_settings(const dsl_settings& s) override {
     int rc = resolve_settings(s, P::num_nodes(prm), &P::known_predicate, &dset);
-    if (rc == DSL_OK) hset = s;
+    if (rc == DSL_OK) {
+      hset = s;
+      set_pred_reads<P>(dset, prm);
+    }
     return rc;
   }
   int set_initial(const uint8_t* p, size_t len, int depth) override {
@@ -268,12 +275,13 @@ struct BfsEngine : EngineBase {
   // within the LDS budget of 4 resident workgroups per CU; a small level is spread over at least
   // ~1024 workgroups instead (one short pass each), since its time is the serial latency chain
   // of one chunk, not throughput.
+  static constexpr uint64_t kLevelGrid = 256ull * 16;
   int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     int lds_max = (int)((24 * 1024) / per);
-    int want = (int)((3 * kBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
+    int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
     const int spread = (int)std::max<uint64_t>(1, (F + 1023) / 1024);
-    int pb = std::max(1, std::min({want, lds_max, kBlock, spread}));
+    int pb = std::max(1, std::min({want, lds_max, kLevelBlock, spread}));
     return pb;
   }
 
@@ -307,6 +315,9 @@ struct BfsEngine : EngineBase {
       if (!S.terms) DSL_HIP(hipMalloc(&S.terms, sizeof(TerminalRec) * kTermCap));
       if (!S.rc) DSL_HIP(hipMalloc(&S.rc, sizeof(RouteCounters)));
       if (!S.seed) DSL_HIP(hipMalloc(&S.seed, 4 * sizeof(int32_t)));
+      if (!S.seg_ctr) DSL_HIP(hipMalloc(&S.seg_ctr, sizeof(unsigned long long) * kSegs * kSegStride));
+      S.seg_base.clear();
+      S.seg_cnt.clear();
       DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
       DSL_TRY(grow_rows(&S.cur, &S.cur_cap, 1024, false, 0));
       DSL_TRY(grow_rows(&S.next, &S.next_cap, 1024, false, 0));
@@ -339,6 +350,8 @@ struct BfsEngine : EngineBase {
       DSL_HIP(hipStreamSynchronize(stream));
       init_enc = ((uint64_t)seed[0] << 32) | (uint32_t)(seed[1] + 1);
       S.F = 1;
+      S.seg_base.assign(1, 0);
+      S.seg_cnt.assign(1, 1);
       S.work = (uint64_t)count_events<P>(init.w, prm, dset);
       S.level_size[0] = 1;
     }
@@ -375,21 +388,28 @@ struct BfsEngine : EngineBase {
 
         // Capacity: the level has exactly S.work work items, an upper bound on its new states.
         // The next frontier gets min(work, 4F) rows (typical growth is ~3 new states per
-        // parent); VALID states beyond that are spilled as 8-byte items and materialized after
-        // the kernel, so the estimate never fails and never reserves the worst case.
+        // parent) split into nseg equal segments; VALID states beyond a segment's rows are
+        // spilled as 8-byte items (room for all `work` of them) and materialized after the
+        // kernel, so the estimate never fails and never reserves the worst case.
         uint64_t Fmax = 0;
         for (auto& S : sh) Fmax = std::max(Fmax, S.F);
         const int PB = chunk_parents(Fmax);
         for (auto& S : sh) {
-          const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 1 << 16)) + 1;
+          uint64_t nchunks = 0;
+          for (size_t q = 0; q < S.seg_cnt.size(); q++) nchunks += (S.seg_cnt[q] + PB - 1) / PB;
+          const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(nchunks, kLevelGrid));
+          S.nseg = (int)std::min<uint64_t>(kSegs, blocks);
+          const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 8192)) + 1;
+          S.segcap = (want + S.nseg - 1) / S.nseg + 1;
+          const uint64_t rows = S.segcap * S.nseg;
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
-          DSL_TRY(grow_rows(&S.next, &S.next_cap, want, false, 0));
-          DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, want, false, 0));
-          DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + want, true, hbase));
-          DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + want, true, hbase));
-          S.launch_cap = std::min(S.next_cap, S.nextfp_cap);
-          DSL_TRY(grow(&S.spill, &S.spill_cap, S.work > S.launch_cap ? S.work - S.launch_cap : 1, false, 0));
+          DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
+          DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
+          DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + rows, true, hbase));
+          DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + rows, true, hbase));
+          DSL_TRY(grow(&S.spill, &S.spill_cap, std::max<uint64_t>(S.work, 1), false, 0));
           DSL_HIP(hipMemsetAsync(S.ctr, 0, sizeof(LevelCounters), stream));
+          DSL_HIP(hipMemsetAsync(S.seg_ctr, 0, sizeof(unsigned long long) * S.nseg * kSegStride, stream));
           if (W > 1) {
             S.cap_fp = std::max<uint64_t>(S.work, 1);
             DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
@@ -402,15 +422,24 @@ struct BfsEngine : EngineBase {
           LevelArgs<P> a;
           a.cur = S.cur;
           a.cur_fp = S.cur_fp;
-          a.F = S.F;
+          a.segs.n = (int32_t)S.seg_cnt.size();
+          a.segs.chunk0[0] = 0;
+          for (int q = 0; q < a.segs.n; q++) {
+            a.segs.base[q] = S.seg_base[q];
+            a.segs.cnt[q] = S.seg_cnt[q];
+            a.segs.chunk0[q + 1] = a.segs.chunk0[q] + (S.seg_cnt[q] + PB - 1) / PB;
+          }
           a.PB = PB;
           a.depth = depth + 1;
+          a.incremental = depth > init_depth ? 1 : 0;
           a.next = S.next;
           a.next_fp = S.next_fp;
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
           a.next_parent = S.hist_parent + hbase;
           a.next_event = S.hist_event + hbase;
-          a.next_cap = S.launch_cap;
+          a.seg_ctr = S.seg_ctr;
+          a.nseg = S.nseg;
+          a.segcap = S.segcap;
           a.spill = S.spill;
           a.spill_cap = S.spill_cap;
           a.ctr = S.ctr;
@@ -422,24 +451,42 @@ struct BfsEngine : EngineBase {
           a.out_fp = S.out_fp;
           a.cap_fp = S.cap_fp;
           a.rc = S.rc;
-          const uint64_t nchunks = (S.F + PB - 1) / PB;
-          const int blocks = (int)std::min<uint64_t>(nchunks, 256ull * 16);
+          const uint64_t nchunks = a.segs.chunk0[a.segs.n];
+          const int blocks = (int)std::min<uint64_t>(nchunks, kLevelGrid);
           if (W > 1)
-            hipLaunchKernelGGL((k_level<P, true>), dim3(blocks), dim3(kBlock), lds, stream, a, prm, dset);
+            hipLaunchKernelGGL((k_level<P, true>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
           else
-            hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kBlock), lds, stream, a, prm, dset);
+            hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
           DSL_HIP(hipGetLastError());
         }
         DSL_HIP(hipEventRecord(ev1, stream));
         // spilled VALID states: grow the next frontier and materialize them after the local rows
-        for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+        std::vector<std::vector<unsigned long long>> segc(L, std::vector<unsigned long long>(kSegs * kSegStride));
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+          DSL_HIP(hipMemcpyAsync(segc[l].data(), S.seg_ctr, sizeof(unsigned long long) * S.nseg * kSegStride,
+                                 hipMemcpyDeviceToHost, stream));
+        }
         DSL_HIP(hipStreamSynchronize(stream));
+        // next frontier: the filled part of each segment, then the spill range (then received)
+        std::vector<std::vector<uint64_t>> nbase(L), ncnt(L);
+        std::vector<uint64_t> span(L);
         bool unspilled = false;
-        for (auto& S : sh) {
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          for (int q = 0; q < S.nseg; q++) {
+            const uint64_t c = std::min<uint64_t>(segc[l][(size_t)q * kSegStride], S.segcap);
+            if (c) {
+              nbase[l].push_back((uint64_t)q * S.segcap);
+              ncnt[l].push_back(c);
+            }
+          }
+          span[l] = S.segcap * S.nseg;
           const uint64_t ns = std::min<uint64_t>(S.lc.spilled, S.spill_cap);
           if (!ns || S.lc.err_frontier || S.lc.err_overflow) continue;
           unspilled = true;
-          const uint64_t keep = S.launch_cap, need = keep + ns + 1;
+          const uint64_t keep = span[l], need = keep + ns;
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
           DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
           DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
@@ -448,7 +495,9 @@ struct BfsEngine : EngineBase {
           const int blocks = (int)std::min<uint64_t>((ns + kBlock - 1) / kBlock, 256ull * 32);
           hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, ns, S.cur, S.cur_fp, S.next,
                              S.next_fp, S.hist_parent + hbase, S.hist_event + hbase, keep, S.gid, S.ctr, prm, dset);
-          stats.exchanged += 0;
+          nbase[l].push_back(keep);
+          ncnt[l].push_back(ns);
+          span[l] = need;
         }
 
         if (W > 1) {
@@ -494,6 +543,7 @@ struct BfsEngine : EngineBase {
             ma.W = W;
             ma.me = S.gid;
             ma.depth = depth + 1;
+            ma.incremental = depth > init_depth ? 1 : 0;
             ma.out = S.out_st;
             ma.cap_s = S.cap_s;
             ma.rc = S.rc;
@@ -505,23 +555,22 @@ struct BfsEngine : EngineBase {
           DSL_TRY(read_route_counts(cnt));
           DSL_TRY(exchange(&Shard::out_st, &Shard::cap_s, &Shard::in_st, &Shard::in_st_cap, &Shard::n_in_st, cnt,
                            src_off));
-          for (auto& S : sh) {
-            LevelCounters c;
-            DSL_HIP(hipMemcpyAsync(&c, S.ctr, sizeof(c), hipMemcpyDeviceToHost, stream));
-            DSL_HIP(hipStreamSynchronize(stream));
-            const uint64_t local_next = std::min<uint64_t>(c.next_size, S.next_cap);
-            const uint64_t need = local_next + S.n_in_st + 1;
-            DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, local_next));
-            DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, local_next));
+          for (int l = 0; l < L; l++) {
+            Shard& S = sh[l];
+            if (!S.n_in_st) continue;
+            const uint64_t keep = span[l], need = keep + S.n_in_st;
+            DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
+            DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
             const uint64_t hbase = S.level_base.back() + S.level_size.back();
-            DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + need, true, hbase + local_next));
-            DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + need, true, hbase + local_next));
-            if (S.n_in_st) {
-              const int blocks = (int)std::min<uint64_t>((S.n_in_st + kBlock - 1) / kBlock, 256ull * 32);
-              hipLaunchKernelGGL(k_append_received<P>, dim3(blocks), dim3(kBlock), 0, stream, S.in_st, S.n_in_st,
-                                 S.next, S.next_fp, S.hist_parent + hbase, S.hist_event + hbase,
-                                 std::min(S.next_cap, S.nextfp_cap), S.ctr);
-            }
+            DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + need, true, hbase + keep));
+            DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + need, true, hbase + keep));
+            const int blocks = (int)std::min<uint64_t>((S.n_in_st + kBlock - 1) / kBlock, 256ull * 32);
+            hipLaunchKernelGGL(k_append_received<P>, dim3(blocks), dim3(kBlock), 0, stream, S.in_st, S.n_in_st,
+                               S.next + keep * NW, S.next_fp + keep, S.hist_parent + hbase + keep,
+                               S.hist_event + hbase + keep, S.n_in_st, S.ctr);
+            nbase[l].push_back(keep);
+            ncnt[l].push_back(S.n_in_st);
+            span[l] = need;
           }
         }
         if (W > 1 || unspilled) {  // counters changed after the first read
@@ -550,7 +599,9 @@ struct BfsEngine : EngineBase {
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
           gsum[0] += S.lc.new_states;
-          gsum[1] += S.lc.next_size;
+          uint64_t fn = 0;
+          for (uint64_t c : ncnt[l]) fn += c;
+          gsum[1] += fn;
           gsum[2] += S.lc.successors;
           gsum[3] += S.lc.err_overflow;
           gsum[4] += S.lc.err_table;
@@ -560,7 +611,7 @@ struct BfsEngine : EngineBase {
           stats.parents += S.F;
           stats.work_items += S.lc.work_items;
           stats.new_states += S.lc.new_states;
-          stats.appended += S.lc.next_size;
+          stats.appended += fn;
           if (S.lc.n_terminals) {
             const uint32_t nt = (uint32_t)std::min<unsigned long long>(S.lc.n_terminals, kTermCap);
             std::vector<TerminalRec> terms(nt);
@@ -593,10 +644,11 @@ struct BfsEngine : EngineBase {
         if (gsum[0]) per_depth.push_back(gsum[0]);
         progress_states = total_states;
         progress_depth = depth;
-        for (auto& S : sh) {
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
           const uint64_t hbase = S.level_base.back() + S.level_size.back();
           S.level_base.push_back(hbase);
-          S.level_size.push_back(S.lc.next_size);
+          S.level_size.push_back(span[l]);
         }
         level_ms_max = std::max(
             level_ms_max, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count());
@@ -643,12 +695,16 @@ struct BfsEngine : EngineBase {
           break;
         }
         if (gsum[1] == 0) break;
-        for (auto& S : sh) {
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
           std::swap(S.cur, S.next);
           std::swap(S.cur_cap, S.next_cap);
           std::swap(S.cur_fp, S.next_fp);
           std::swap(S.curfp_cap, S.nextfp_cap);
-          S.F = S.lc.next_size;
+          S.seg_base = nbase[l];
+          S.seg_cnt = ncnt[l];
+          S.F = 0;
+          for (uint64_t c : ncnt[l]) S.F += c;
           S.work = S.lc.next_work;
         }
       }

@@ -27,7 +27,10 @@ struct DevPred {
   int32_t id;
   int32_t negate;
   int64_t arg0, arg1;
+  uint32_t reads;  // nodes whose words the predicate reads (bit i = node i; bit 31 = the network)
+  uint32_t pad;
 };
+constexpr uint32_t kReadsAll = 0xffffffffu;
 
 // Device form of SearchSettings/TestSettings. The tri-state precedence of
 // TestSettings.shouldDeliver (TestSettings.java:224-245) is resolved on the host into a

@@ -20,9 +20,28 @@
 namespace dsl {
 
 constexpr int kBlock = 256;
+// k_level workgroup: 4 wavefronts share a chunk of parents staged in LDS (measured: one
+// wavefront per workgroup is slower -- its smaller chunks sort into more handler classes per
+// wavefront -- despite having no cross-wavefront barrier waits).
+constexpr int kLevelBlock = 256;
 constexpr uint32_t kTermCap = 1024;
 constexpr int kMaxShards = 16;
 constexpr int kWin = 1024;  // work items per class-sorted window of k_level
+// The next frontier is written into up to kSegs segments, one reservation counter each (a
+// workgroup appends to segment blockIdx % nseg), so every wavefront reserves its rows with one
+// returning atomic and no workgroup barrier, and no counter word carries more than 1/kSegs of
+// the level's reservations. A frontier is then a short list of row ranges: the segments, the
+// spill range and (multi-shard) the received range.
+constexpr int kSegs = 32;
+constexpr int kMaxSegs = kSegs + 2;
+constexpr int kSegStride = 16;  // u64 words between segment counters (one 128-byte line each)
+
+struct SegTable {
+  int32_t n;
+  uint64_t base[kMaxSegs];
+  uint64_t cnt[kMaxSegs];
+  uint64_t chunk0[kMaxSegs + 1];  // first chunk of each segment; chunk0[n] = chunks of the level
+};
 
 struct LevelCounters {
   unsigned long long new_states;    // newly discovered successors (all verdicts)
@@ -43,7 +62,7 @@ struct LevelCounters {
 #ifdef DSL_PHASES
 #define PH_DECL unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long ph_t = clock64();
 #define PH_MARK(i) do { const unsigned long long ph_n = clock64(); ph_acc[i] += ph_n - ph_t; ph_t = ph_n; } while (0)
-#define PH_FLUSH(red, ctr) do { for (int ph_i = 0; ph_i < 8; ph_i++) block_flush(red, &(ctr)->phase[ph_i], __lane_id() == 0 ? ph_acc[ph_i] : 0ull); } while (0)
+#define PH_FLUSH(red, ctr) do { for (int ph_i = 0; ph_i < 8; ph_i++) block_flush<kLevelBlock>(red, &(ctr)->phase[ph_i], __lane_id() == 0 ? ph_acc[ph_i] : 0ull); } while (0)
 #else
 #define PH_DECL
 #define PH_MARK(i) do { } while (0)
@@ -85,12 +104,14 @@ __device__ __forceinline__ unsigned long long wave_reserve(unsigned long long* c
 // destination per call per workgroup, not per wave -- a single device-scope counter word
 // saturates near 90 returning atomics/us on MI355X, so per-wave reservations from every CU
 // serialize the whole level on that word. Has barriers: every thread of the block calls it.
+template <int BS = kBlock>
 struct BlockResv {
-  int cnt[kBlock / 64][kMaxShards];
-  unsigned long long off[kBlock / 64][kMaxShards];
+  int cnt[BS / 64][kMaxShards];
+  unsigned long long off[BS / 64][kMaxShards];
 };
 
-__device__ __forceinline__ unsigned long long block_reserve(BlockResv& s, unsigned long long* ctrs, bool pred,
+template <int BS = kBlock>
+__device__ __forceinline__ unsigned long long block_reserve(BlockResv<BS>& s, unsigned long long* ctrs, bool pred,
                                                             int dest, int W) {
   const int wid = threadIdx.x >> 6, lane = __lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
@@ -105,9 +126,9 @@ __device__ __forceinline__ unsigned long long block_reserve(BlockResv& s, unsign
   if ((int)threadIdx.x < W) {
     const int d = threadIdx.x;
     unsigned long long tot = 0;
-    for (int w = 0; w < kBlock / 64; w++) tot += (unsigned long long)s.cnt[w][d];
+    for (int w = 0; w < BS / 64; w++) tot += (unsigned long long)s.cnt[w][d];
     unsigned long long base = tot ? atomicAdd(&ctrs[d], tot) : 0ull;
-    for (int w = 0; w < kBlock / 64; w++) {
+    for (int w = 0; w < BS / 64; w++) {
       s.off[w][d] = base;
       base += (unsigned long long)s.cnt[w][d];
     }
@@ -117,6 +138,7 @@ __device__ __forceinline__ unsigned long long block_reserve(BlockResv& s, unsign
 }
 
 // Sums a per-thread value over the workgroup and adds it to *ctr with one atomic (kernel exit).
+template <int BS = kBlock>
 __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned long long* ctr, unsigned long long v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   __syncthreads();
@@ -124,7 +146,7 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
-    for (int w = 0; w < kBlock / 64; w++) t += red[w];
+    for (int w = 0; w < BS / 64; w++) t += red[w];
     if (t) atomicAdd(ctr, t);
   }
 }
@@ -181,16 +203,19 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
 
 template <class P>
 struct LevelArgs {
-  const uint32_t* cur;       // F rows of kWords
+  const uint32_t* cur;       // frontier rows of kWords (row ranges in `segs`)
   const Fp* cur_fp;
-  uint64_t F;
+  SegTable segs;
   int32_t PB;                // parents per chunk
   int32_t depth;             // depth of the successors
+  int32_t incremental;       // parents are expanded non-initial states (judge_view)
   uint32_t* next;            // next frontier rows
   Fp* next_fp;
   uint64_t* next_parent;     // history arena slice of the next level
   uint32_t* next_event;
-  uint64_t next_cap;
+  unsigned long long* seg_ctr;  // nseg counters, kSegStride apart
+  int32_t nseg;
+  uint64_t segcap;              // rows per next-frontier segment
   LevelCounters* ctr;
   TerminalRec* terms;
   Table table;
@@ -208,16 +233,16 @@ template <class P, bool ROUTE>
 #ifndef DSL_KLEVEL_ATTR
 #define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
-__global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
+__global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // PB * NW
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // PB
   int* off = reinterpret_cast<int*>(fps + a.PB);           // PB + 1
   __shared__ int s_total;
-  __shared__ BlockResv s_resv;
-  __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
-  __shared__ unsigned long long s_red[kBlock / 64];
+  __shared__ BlockResv<kLevelBlock> s_resv;
+  __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
+  __shared__ unsigned long long s_red[kLevelBlock / 64];
   __shared__ int s_hist[16];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
@@ -225,10 +250,13 @@ __global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a
   unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
   PH_DECL
 
-  const uint64_t nchunks = (a.F + a.PB - 1) / a.PB;
+  const uint64_t nchunks = a.segs.chunk0[a.segs.n];
+  const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
+  int g = 0;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    const uint64_t p0 = chunk * a.PB;
-    const int pb = (int)min<uint64_t>((uint64_t)a.PB, a.F - p0);
+    while (chunk >= a.segs.chunk0[g + 1]) g++;  // chunks ascend: the segment index only grows
+    const uint64_t p0 = a.segs.base[g] + (chunk - a.segs.chunk0[g]) * (uint64_t)a.PB;
+    const int pb = (int)min<uint64_t>((uint64_t)a.PB, a.segs.base[g] + a.segs.cnt[g] - p0);
     // 1. stage the parents (contiguous rows) and their fingerprints in LDS
     {
       const uint4* src = reinterpret_cast<const uint4*>(a.cur + p0 * NW);
@@ -314,7 +342,7 @@ __global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a
 #pragma unroll
               for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
               const NodeView view{w, P::kNodeWords, d.node, my_nw};
-              const int v = judge_view<P>(view, prm, set, a.depth, &pi);
+              const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
               if (v == V_VALID) {
                 if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = true;
                 else atomicAdd(&a.ctr->err_overflow, 1ull);
@@ -337,9 +365,10 @@ __global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a
         }
       }
       PH_MARK(4);  // judge (+ divergence wait)
-      const unsigned long long idx = block_reserve(s_resv, &a.ctr->next_size, is_valid, 0, 1);
+      const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
       PH_MARK(5);  // reservation
-      const bool fits = is_valid && idx < a.next_cap;
+      const bool fits = is_valid && li < a.segcap;
+      const uint64_t idx = (uint64_t)seg * a.segcap + li;
       if (fits) {
         const uint32_t* w = rows + j * NW;
         a.next_fp[idx] = f;
@@ -359,7 +388,7 @@ __global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a
         }
       }
       if (ROUTE) {
-        const unsigned long long ridx = block_reserve(s_resv, a.rc->out, route, dest, a.W);
+        const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out, route, dest, a.W);
         if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
       }
     }
@@ -368,10 +397,10 @@ __global__ void __launch_bounds__(kBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a
     __syncthreads();  // LDS is reused by the next chunk
   }
   PH_FLUSH(s_red, a.ctr);
-  block_flush(s_red, &a.ctr->successors, c_succ);
-  block_flush(s_red, &a.ctr->new_states, c_new);
-  block_flush(s_red, &a.ctr->next_work, c_next_work);
-  block_flush(s_red, &a.ctr->work_items, c_work);
+  block_flush<kLevelBlock>(s_red, &a.ctr->successors, c_succ);
+  block_flush<kLevelBlock>(s_red, &a.ctr->new_states, c_new);
+  block_flush<kLevelBlock>(s_red, &a.ctr->next_work, c_next_work);
+  block_flush<kLevelBlock>(s_red, &a.ctr->work_items, c_work);
 }
 
 // Materializes spilled VALID states (already inserted, counted and judged) at next_size.
@@ -439,7 +468,7 @@ struct ProbeArgs {
 };
 
 __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
-  __shared__ BlockResv s_resv;
+  __shared__ BlockResv<> s_resv;
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_new = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -482,7 +511,7 @@ struct MaterializeArgs {
   uint64_t n;
   const uint32_t* cur;
   const Fp* cur_fp;
-  int32_t W, me, depth;
+  int32_t W, me, depth, incremental;
   StateRec<P>* out;  // W regions of cap_s records
   uint64_t cap_s;
   RouteCounters* rc;
@@ -493,7 +522,7 @@ struct MaterializeArgs {
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
-  __shared__ BlockResv s_resv;
+  __shared__ BlockResv<> s_resv;
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
@@ -516,7 +545,7 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
 #pragma unroll
       for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
       const NodeView view{w, P::kNodeWords, d.node, my_nw};
-      const int v = judge_view<P>(view, prm, set, a.depth, &pi);
+      const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
       if (v == V_VALID) {
         ship = true;
       } else if (v >= V_TERM_EXCEPTION) {
@@ -545,8 +574,9 @@ template <class P>
 __global__ void __launch_bounds__(kBlock) k_append_received(const StateRec<P>* in, uint64_t n, uint32_t* next, Fp* next_fp,
                                                             uint64_t* next_parent, uint32_t* next_event,
                                                             uint64_t next_cap, LevelCounters* ctr) {
+  // rows [0, next_cap) of the received range; ctr->next_size counts them (k_level does not)
   constexpr int NW = Layout<P>::kWords;
-  __shared__ BlockResv s_resv;
+  __shared__ BlockResv<> s_resv;
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_next_work = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;

@@ -432,10 +432,22 @@ void describe_event(const uint32_t* w, int k, const typename P::Params& prm, con
 }
 
 // checkState order over a node view (Search.java:162-231).
+// incremental: the view is a successor of an EXPANDED, non-initial parent, which therefore had
+// every invariant true, every goal false or throwing (ignored) and every prune false (a state
+// that violated, matched or was pruned is never expanded; only the initial state is expanded
+// when pruned, Search.java:475). A predicate that reads neither the changed node nor the
+// network has the parent's value, so it is skipped with that outcome. tests/hostcheck checks
+// the incremental verdict against the full one on every generated successor.
+template <class P>
+DSL_HD bool pred_unchanged(const DevPred& pr, const NodeView& v, bool incremental) {
+  return incremental && v.changed >= 0 && !((pr.reads >> v.changed) & 1u) && !(pr.reads >> 31);
+}
+
 template <class P>
 DSL_HD Verdict judge_view(const NodeView& v, const typename P::Params& prm, const DevSettings& set, int depth,
-                          int* pred_index) {
+                          int* pred_index, bool incremental = false) {
   for (int i = 0; i < set.n_inv; i++) {
+    if (pred_unchanged<P>(set.inv[i], v, incremental)) continue;
     int x = P::eval(set.inv[i], v, prm);
     if (x != PV_THREW && set.inv[i].negate) x = !x;
     if (x != PV_TRUE) {
@@ -444,6 +456,7 @@ DSL_HD Verdict judge_view(const NodeView& v, const typename P::Params& prm, cons
     }
   }
   for (int i = 0; i < set.n_goal; i++) {
+    if (pred_unchanged<P>(set.goal[i], v, incremental)) continue;
     int x = P::eval(set.goal[i], v, prm);
     if (x == PV_THREW) continue;
     if (set.goal[i].negate) x = !x;
@@ -453,12 +466,21 @@ DSL_HD Verdict judge_view(const NodeView& v, const typename P::Params& prm, cons
     }
   }
   for (int i = 0; i < set.n_prune; i++) {
+    if (pred_unchanged<P>(set.prune[i], v, incremental)) continue;
     int x = P::eval(set.prune[i], v, prm);
     if (x != PV_THREW && set.prune[i].negate) x = !x;
     if (x != PV_FALSE) return V_PRUNED;
   }
   if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
   return V_VALID;
+}
+
+// Fills DevPred::reads from the protocol's read sets (host, after resolve_settings).
+template <class P>
+void set_pred_reads(DevSettings& d, const typename P::Params& prm) {
+  for (int i = 0; i < d.n_inv; i++) d.inv[i].reads = P::pred_reads(d.inv[i], prm);
+  for (int i = 0; i < d.n_goal; i++) d.goal[i].reads = P::pred_reads(d.goal[i], prm);
+  for (int i = 0; i < d.n_prune; i++) d.prune[i].reads = P::pred_reads(d.prune[i], prm);
 }
 
 }  // namespace dsl

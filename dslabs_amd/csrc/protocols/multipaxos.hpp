@@ -479,6 +479,17 @@ struct MultiPaxos {
     }
   }
 
+  // Read sets (judge_view's incremental check): client predicates read client nodes only,
+  // LOGS_CONSISTENT the servers only.
+  static uint32_t pred_reads(const DevPred& pr, const Params& p) {
+    const uint32_t servers = (1u << p.servers) - 1u, clients = ((1u << p.clients) - 1u) << p.servers;
+    switch (pr.id) {
+      case DSL_PRED_LOGS_CONSISTENT: return servers;
+      case DSL_PRED_RESULTS_OK: case DSL_PRED_CLIENTS_DONE: case DSL_PRED_CLIENT_DONE: case DSL_PRED_NONE_DECIDED:
+      case DSL_PRED_CLIENT_HAS_RESULTS: case DSL_PRED_APPENDS_LINEARIZABLE: return clients;
+      default: return kReadsAll;
+    }
+  }
   static bool known_predicate(int id) {
     return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == DSL_PRED_LOGS_CONSISTENT ||
            id == DSL_PRED_APPENDS_LINEARIZABLE;

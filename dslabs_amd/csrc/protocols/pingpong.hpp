@@ -142,6 +142,11 @@ struct PingPong {
     }
   }
 
+  // Read sets (judge_view's incremental check): every predicate reads client nodes only.
+  static uint32_t pred_reads(const DevPred& pr, const Params& p) {
+    return (pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) ? (((1u << p.clients) - 1u) << 1)
+                                                                                   : kReadsAll;
+  }
   static bool known_predicate(int id) { return id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS; }
   static bool valid(const Params& p) {
     return p.clients >= 1 && p.clients <= kMaxClients && p.pings >= 1 && p.pings <= kMaxPings;

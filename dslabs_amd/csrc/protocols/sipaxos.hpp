@@ -171,6 +171,11 @@ struct SIPaxos {
     }
   }
 
+  // Read sets (judge_view's incremental check): the predicates read proposer nodes only.
+  static uint32_t pred_reads(const DevPred& pr, const Params& p) {
+    return (pr.id >= DSL_PRED_SIP_AGREEMENT && pr.id <= DSL_PRED_SIP_TERMINATION) ? ((1u << p.proposers) - 1u)
+                                                                                   : kReadsAll;
+  }
   static bool known_predicate(int id) { return id >= DSL_PRED_SIP_AGREEMENT && id <= DSL_PRED_SIP_TERMINATION; }
   static bool valid(const Params& p) {
     return p.proposers >= 1 && p.proposers <= kMaxP && p.acceptors >= 1 && p.acceptors <= kMaxA;

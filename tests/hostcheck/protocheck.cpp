@@ -24,6 +24,7 @@ using namespace dsl;
 template <class P>
 static int run(const dsl_protocol_desc& d, DevSettings set) {
   typename P::Params prm = P::from_desc(d);
+  set_pred_reads<P>(set, prm);
   if (!P::valid(prm)) {
     printf("{\"error\":\"invalid params\"}\n");
     return 1;
@@ -55,7 +56,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
-  long long fp_mismatch = 0, emit_mismatch = 0;
+  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
@@ -101,6 +102,11 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       per[d]++;
       NodeView view{n.s.w, P::kNodeWords, dl.node, dl.nw};
       v = judge_view<P>(view, prm, set, d, &pi);
+      if (n.depth > 0) {  // the kernels' incremental check must give the same verdict
+        int pi2 = -1;
+        const int v2 = judge_view<P>(view, prm, set, d, &pi2, true);
+        if (v2 != v || (v >= V_TERM_EXCEPTION && pi2 != pi)) judge_mismatch++;
+      }
       if (v >= V_TERM_EXCEPTION) {
         if (tdepth < 0) tdepth = d;
         if (first_term_parent == -2) first_term_parent = n.id, first_term_event = k;
@@ -116,7 +122,8 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
   unsigned long long total = 0;
   printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"emit_mismatch\":%lld,"
-         "\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch, emit_mismatch);
+         "\"judge_mismatch\":%lld,\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch, emit_mismatch,
+         judge_mismatch);
   for (size_t i = 0; i < per.size(); i++) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];

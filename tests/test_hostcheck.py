@@ -77,4 +77,4 @@ def test_encoding_matches_oracle(protocheck, name):
     want = oracle_util.run("bfs", oargs, timeout=600)
     assert got["end"] == want["end"]
     assert got["per_depth"] == want["per_depth"]
-    assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0
+    assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
