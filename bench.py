@@ -77,19 +77,40 @@ def cpu_baseline(oracle_args, depth: int) -> dict:
                       f"oracle/dslabs_oracle single-threaded)"}
 
 
-def roofline(stats: dict) -> dict:
-    """Algorithmic bytes of k_expand per launch (SURVEY.md §8d byte model):
+def pmc_traffic(workload: str, depth: int):
+    """HBM bytes per k_level launch from the committed rocprofv3 PMC summary of the same
+    workload (tools/gpu_prof.sh + tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950 16-B/lane
+    correction) + WRITE_SIZE, separate --pmc passes), or None if this workload has none."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_d{depth}.json"))):
+        best = f
+    if best is None:
+        return None, None
+    d = json.load(open(best))
+    v = d.get("hbm_bytes_per_launch")
+    return (int(v) if v else None), os.path.relpath(best, ROOT)
+
+
+def roofline(stats: dict, workload: str, depth: int) -> dict:
+    """Algorithmic bytes of k_level per launch (SURVEY.md §8d byte model):
     parents read once (S B), one 64-B bucket line probed per successor, one bucket line written
-    back + 12 B parent/event per new state, S B per successor appended to the next frontier."""
+    back + 12 B parent/event per new state, S B per successor appended to the next frontier;
+    divided by the summed k_level durations (HIP events on the engine's stream)."""
     S = stats["state_bytes"]
     alg = stats["parents"] * S + stats["work_items"] * 64 + stats["new_states"] * (64 + 12) + stats["appended"] * S
     t = stats["expand_ms"] / 1e3
     achieved = alg / t / 1e9 if t > 0 else 0.0
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-            "kernel": "k_expand", "launches": stats["expand_launches"],
-            "avg_launch_ms": round(stats["expand_ms"] / max(1, stats["expand_launches"]), 4),
-            "alg_bytes_per_launch": int(alg / max(1, stats["expand_launches"]))}
+    launches = max(1, stats["expand_launches"])
+    traffic, src = pmc_traffic(workload, depth)
+    out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+           "kernel": "k_level", "launches": stats["expand_launches"],
+           "avg_launch_ms": round(stats["expand_ms"] / launches, 4),
+           "alg_bytes_per_launch": int(alg / launches)}
+    if src:
+        out["traffic_source"] = src
+    return out
 
 
 def main():
@@ -170,7 +191,7 @@ def main():
                        "unique_states_per_step": res.states, "per_depth": res.per_depth,
                        "end_condition": res.endCondition().name, "state_bytes": stats["state_bytes"],
                        "successors_per_step": res.successors, "parallelism": f"hash-sharded x{world}"},
-            "roofline": roofline(stats),
+            "roofline": roofline(stats, args.workload, depth),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(oracle_args, wl["cpu_depth"])

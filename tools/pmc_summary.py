@@ -1,0 +1,64 @@
+"""Summarizes a tools/gpu_prof.sh run (rocprofv3 kernel trace + separate PMC passes) for the
+dominant kernel k_level: per-launch duration, FETCH_SIZE / WRITE_SIZE (KB in rocprofv3), HBM
+traffic per launch with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the
+bytes of 16-byte-per-lane reads: x2), and the SQ counters. Writes one JSON object.
+
+    python tools/pmc_summary.py gpurun_out/prof_TAG > profiles/rNN_pmc_WORKLOAD_dDEPTH.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNEL = "k_level"
+
+
+def per_dispatch(path):
+    by = defaultdict(dict)
+    names = {}
+    for r in csv.DictReader(open(path)):
+        if KERNEL not in r["Kernel_Name"]:
+            continue
+        d = int(r["Dispatch_Id"])
+        by[d][r["Counter_Name"]] = float(r["Counter_Value"])
+        names[d] = r["Kernel_Name"]
+    return by
+
+
+def main(d):
+    out = {"kernel": KERNEL, "source": os.path.basename(d.rstrip("/"))}
+    kt = os.path.join(d, "kt", "run_kernel_trace.csv")
+    if os.path.exists(kt):
+        rows = [r for r in csv.DictReader(open(kt)) if KERNEL in r["Kernel_Name"]]
+        durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
+        out["launches_traced"] = len(durs)
+        out["avg_launch_ms"] = sum(durs) / max(1, len(durs))
+        out["vgpr"] = rows[0].get("VGPR_Count") if rows else None
+        out["scratch_bytes_per_lane"] = rows[0].get("Scratch_Size") if rows else None
+    tot = defaultdict(float)
+    n = 0
+    for f in glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv")):
+        disp = per_dispatch(f)
+        n = max(n, len(disp))
+        for v in disp.values():
+            for k, x in v.items():
+                tot[k] += x
+    if n:
+        out["pmc_launches"] = n
+        out["counters_total"] = {k: v for k, v in sorted(tot.items())}
+        fetch = tot.get("FETCH_SIZE", 0.0) * 1024
+        write = tot.get("WRITE_SIZE", 0.0) * 1024
+        out["fetch_bytes_raw_per_launch"] = fetch / n
+        out["write_bytes_per_launch"] = write / n
+        # gfx950: FETCH_SIZE counts half the bytes of 16-B/lane reads (the staging and bucket loads)
+        out["hbm_bytes_per_launch"] = (2 * fetch + write) / n
+        if "SQ_WAVE_CYCLES" in tot and tot.get("SQ_WAVE_CYCLES"):
+            out["wait_frac"] = tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in tot else None
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
