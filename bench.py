@@ -36,6 +36,11 @@ WORKLOADS = {
                             "RESULTS_OK, LOGS_CONSISTENT_ALL_SLOTS, APPENDS_LINEARIZABLE, timers on, BFS to maxDepth"),
     # The reference's own Paxos ("Paxos Made Simple", SingleInstancePaxos.java:50-127): 2
     # proposers, 3 acceptors, invariants Integrity + Agreement, exhaustive to maxDepth.
+    # BASELINE config C3: the table-driven synthetic protocol, 5 nodes, 64-byte
+    # packed state, ~20-25 successors per state, maxDepth 10 (~8e8 unique states).
+    "synthetic": dict(depth=10, cpu_depth=6, table_log2=31,
+                      desc="table-driven synthetic protocol (5 nodes, K=64, pokes at v%7==0, seed 0x5EEDD51AB5), "
+                           "invariant NOT_ALL_MAX, BFS to maxDepth"),
     "sipaxos": dict(depth=15, cpu_depth=10,
                     desc="reference SingleInstancePaxos (2 proposers, 3 acceptors), invariants "
                          "Integrity+Agreement, BFS to maxDepth"),
@@ -45,7 +50,7 @@ WORKLOADS = {
 def build_search(name: str, depth: int):
     from dslabs_amd import SearchSettings
     from dslabs_amd import RESULTS_OK
-    from dslabs_amd.protocols import MultiPaxos, SIPaxos
+    from dslabs_amd.protocols import MultiPaxos, SIPaxos, Synthetic
     if name == "multipaxos":
         proto = MultiPaxos(3, 2, "append-xy")
         s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
@@ -54,6 +59,12 @@ def build_search(name: str, depth: int):
         s.table_log2_slots = 28
         return proto, s, ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
                           "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
+    if name == "synthetic":
+        proto = Synthetic(5, 64, 7)
+        s = SearchSettings().addInvariant(proto.predicate("NOT_ALL_MAX"))
+        s.maxDepth(depth)
+        s.table_log2_slots = WORKLOADS[name].get("table_log2", 28) if depth >= 10 else 28
+        return proto, s, ["--proto", "synthetic", "--inv", "NOT_ALL_MAX"]
     if name == "sipaxos":
         proto = SIPaxos(2, 3, ("a", "b"))
         s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))

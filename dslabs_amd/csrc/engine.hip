@@ -241,6 +241,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_PINGPONG: return make_engine<PingPong>(d, cfg, out);
     case DSL_PROTO_SIPAXOS: return make_engine<SIPaxos>(d, cfg, out);
     case DSL_PROTO_MULTIPAXOS: return make_engine<MultiPaxos>(d, cfg, out);
+    case DSL_PROTO_SYNTHETIC: return make_engine<Synthetic>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -271,6 +272,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_PINGPONG: return (int)sizeof(dsl::PingPong::State);
     case DSL_PROTO_SIPAXOS: return (int)sizeof(dsl::SIPaxos::State);
     case DSL_PROTO_MULTIPAXOS: return (int)sizeof(dsl::MultiPaxos::State);
+    case DSL_PROTO_SYNTHETIC: return (int)sizeof(dsl::Synthetic::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }

@@ -3,4 +3,5 @@
 #include "multipaxos.hpp"
 #include "pingpong.hpp"
 #include "sipaxos.hpp"
+#include "synthetic.hpp"
 #define DSL_HAVE_MULTIPAXOS 1

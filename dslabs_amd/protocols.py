@@ -218,3 +218,37 @@ class MultiPaxos(Protocol):
         else:
             body = f"Heartbeat({self._ballot(self._mballot(m))})"
         return f"Message({a[e.from_]} -> {a[e.to]}, {body})"
+
+
+class Synthetic(Protocol):
+    """The table-driven synthetic protocol of BASELINE config C3 (builder-defined):
+    nodes "node1..N", each with a value v in [0, K), a poke counter and four always-deliverable
+    timers SynthTimer(0..3); transitions come from a seeded splitmix64 table. 64-byte packed
+    state, ~20-25 enabled events per state: a dedup / all-to-all stress test."""
+
+    proto_id = DSL_PROTO_SYNTHETIC
+    SEED = 0x5EEDD51AB5
+
+    def __init__(self, nodes: int = 5, values: int = 64, poke_mod: int = 7, seed: int = SEED):
+        self.nodes = nodes
+        self.values = values
+        self.poke_mod = poke_mod
+        self.seed = seed
+        self.addresses = [f"node{i}" for i in range(1, nodes + 1)]
+
+    def params(self):
+        return [self.nodes, self.values, self.poke_mod, self.seed]
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        if name == "NOT_ALL_MAX":
+            return StatePredicate("NOT_ALL_MAX", 200)
+        if name.startswith("COUNTER_LT:"):
+            _, node, bound = name.split(":")
+            return StatePredicate(name, 201, int(node), int(bound))
+        raise KeyError(name)
+
+    def render_event(self, e) -> str:
+        if e.is_timer:
+            return f"Timer(-> {self.addresses[e.to]}, SynthTimer({e.fields[0]}))"
+        return f"Message({self.addresses[e.from_]} -> {self.addresses[e.to]}, Poke())"

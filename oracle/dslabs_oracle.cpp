@@ -19,6 +19,7 @@
 #include "proto_multipaxos.hpp"
 #include "proto_pingpong.hpp"
 #include "proto_sipaxos.hpp"
+#include "proto_synthetic.hpp"
 
 using namespace oracle;
 
@@ -115,6 +116,21 @@ static Scenario build(const Args& a) {
       if (p) return *p;
       if (n == "LOGS_CONSISTENT_ALL_SLOTS") return multipaxos::logsConsistent(cfg);
       if (n == "APPENDS_LINEARIZABLE") return multipaxos::appendsLinearizable(cfg);
+      throw std::runtime_error("unknown predicate " + n);
+    };
+  } else if (a.proto == "synthetic") {
+    synthetic::Table tab;
+    tab.nodes = a.geti("nodes", 5);
+    tab.K = a.geti("values", 64);
+    tab.P = a.geti("poke-mod", 7);
+    if (a.has("seed")) tab.seed = std::stoull(a.get("seed"), nullptr, 0);
+    sc.init = synthetic::initial(tab, sc.names);
+    sc.pred = [tab](const std::string& n) -> Predicate {
+      if (n == "NOT_ALL_MAX") return synthetic::notAllMax(tab);
+      if (n.rfind("COUNTER_LT:", 0) == 0) {
+        auto parts = split(n, ':');
+        return synthetic::counterLt(std::stoi(parts[1]), std::stoi(parts[2]));
+      }
       throw std::runtime_error("unknown predicate " + n);
     };
   } else {

@@ -91,7 +91,7 @@ def gen(cases, fname):
         json.dump(out, f, indent=1)
 
 
-if __name__ == "__main__":
+def gen_lab0_sip():
     gen(LAB0, "lab0.json")
     SIP = {
         "sipaxos_2p3a_d9": dict(
@@ -148,5 +148,28 @@ MULTIPAXOS = {
     "mp_xz_d8": dict(args=MP + ["--workload", "append-xz"] + INV3 + ["--max-depth", "8"], pinned={}),
 }
 
+SY = ["--proto", "synthetic"]
+SYNTHETIC = {
+    # BASELINE C3 (builder-defined): 5 nodes, K = 64, pokes at v % 7 == 0, seed
+    # 0x5EEDD51AB5; the bench runs the same configuration to maxDepth 10 (~8e8 states).
+    "synth_c3_d5": dict(args=SY + ["--inv", "NOT_ALL_MAX", "--max-depth", "5"], pinned={}),
+    "synth_3n_k8_d9": dict(args=SY + ["--nodes", "3", "--values", "8", "--poke-mod", "3", "--inv", "NOT_ALL_MAX",
+                                      "--max-depth", "9", "--finish-level"], pinned={}),
+    # a reachable value bound: the first violation depth and its trace
+    "synth_counter_violation": dict(args=SY + ["--nodes", "4", "--values", "32", "--inv", "COUNTER_LT:2:30",
+                                               "--finish-level"], pinned={}),
+    # goal + prune combination
+    "synth_goal_prune": dict(args=SY + ["--nodes", "3", "--values", "64", "--goal", "!COUNTER_LT:0:63", "--prune",
+                                        "!COUNTER_LT:1:40", "--finish-level"], pinned={}),
+    # the whole reachable space of a small configuration (no depth bound)
+    "synth_2n_k4_exhaustive": dict(args=SY + ["--nodes", "2", "--values", "4", "--poke-mod", "2"], pinned={}),
+}
+
 if __name__ == "__main__":
-    gen(MULTIPAXOS, "multipaxos.json")
+    which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic"}
+    if "lab0" in which or "sipaxos" in which:
+        gen_lab0_sip()
+    if "multipaxos" in which:
+        gen(MULTIPAXOS, "multipaxos.json")
+    if "synthetic" in which:
+        gen(SYNTHETIC, "synthetic.json")

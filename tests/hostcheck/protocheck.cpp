@@ -178,6 +178,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_PINGPONG: return run<PingPong>(d, set);
     case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, set);
     case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, set);
+    case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
   }
   return 2;
 }

@@ -67,6 +67,11 @@ CASES = {
                     ["--proto", "multipaxos", "--servers", "2", "--clients", "1", "--workload", "append-x", "--inv",
                      "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--prune",
                      "CLIENTS_DONE", "--max-depth", "11"]),
+    # synthetic C3: nodes K P seed -- invariant NOT_ALL_MAX (200)
+    "synth_c3_d6": ([3, 5, 64, 7, 0x5EEDD51AB5, "--", 200, "/", "/", 6],
+                    ["--proto", "synthetic", "--inv", "NOT_ALL_MAX", "--max-depth", "6"]),
+    "synth_2n_k4": ([3, 2, 4, 2, 0x5EEDD51AB5, "--", "/", "/", -1],
+                    ["--proto", "synthetic", "--nodes", "2", "--values", "4", "--poke-mod", "2"]),
 }
 
 

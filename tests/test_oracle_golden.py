@@ -66,3 +66,14 @@ def test_oracle_replay_readme_trace():
     r = oracle_util.replay(args, case["pinned"]["trace"])
     assert r["ok"] and r["depth"] == 3
     assert r["invariants"][0]["value"] is False
+
+
+SYN = _load("synthetic.json")
+
+
+@pytest.mark.parametrize("name", sorted(SYN))
+def test_synthetic_oracle_matches_fixture(name):
+    case = SYN[name]
+    r = oracle_util.run("bfs", case["args"], timeout=300)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
