@@ -64,7 +64,8 @@ class dsl_settings(ctypes.Structure):
 
 class dsl_engine_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32),
-                ("virtual_shards", ctypes.c_int32), ("comm_id", ctypes.c_uint8 * 128)]
+                ("virtual_shards", ctypes.c_int32), ("comm_id", ctypes.c_uint8 * 128),
+                ("replicate_below", ctypes.c_int64)]
 
 
 class dsl_event(ctypes.Structure):

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -276,6 +277,9 @@ struct BfsEngine : EngineBase {
   // ~1024 workgroups instead (one short pass each), since its time is the serial latency chain
   // of one chunk, not throughput.
   static constexpr uint64_t kLevelGrid = 256ull * 16;
+  // Frontier size below which a multi-shard search runs the level replicated (see run()):
+  // dsl_engine_config.replicate_below, -1 = default, 0 = never.
+  uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 19) : (uint64_t)cfg.replicate_below; }
   int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     int lds_max = (int)((24 * 1024) / per);
@@ -338,8 +342,16 @@ struct BfsEngine : EngineBase {
     const Fp init_fp = full_fingerprint<P>(init.w);
     const int init_owner = owner_of(init_fp, W);
     uint64_t init_enc = ~0ull;
+    // Replicated small levels: while the frontier is below rep_threshold, every shard runs the
+    // whole level itself (identical work, no exchange; each table then holds every state of
+    // those levels, a superset of what it owns, so later owner probes stay exact). The first
+    // level above the threshold expands only owned parents, and from there on the search is
+    // hash-sharded. Per-level latency of a sharded level is ~3 exchange rounds, so sharding a
+    // level pays only once it has enough work.
+    bool rep_active = W > 1 && rep_threshold() > 0;
+    bool first_sharded = W > 1 && !rep_active;
     for (auto& S : sh) {
-      if (S.gid != init_owner) continue;
+      if (S.gid != init_owner && !rep_active) continue;
       DSL_HIP(hipMemcpyAsync(S.cur, init.w, NW * 4, hipMemcpyHostToDevice, stream));
       DSL_HIP(hipMemcpyAsync(S.cur_fp, &init_fp, sizeof(Fp), hipMemcpyHostToDevice, stream));
       Table t = tbl_proto;
@@ -372,14 +384,25 @@ struct BfsEngine : EngineBase {
     } else {
       while (true) {
         const auto lt0 = std::chrono::steady_clock::now();
+        // every shard holds the same frontier in a replicated level: the decision is identical
+        const bool rep = rep_active && sh[0].F < rep_threshold();
+        if (rep_active && !rep) {
+          rep_active = false;
+          first_sharded = true;
+        }
+        const bool route = W > 1 && !rep;
         std::vector<uint64_t> g(2, 0);  // [frontier states, time-up flag]
-        for (auto& S : sh) g[0] += S.F;
+        if (rep) {
+          g[0] = sh[0].F;
+        } else {
+          for (auto& S : sh) g[0] += S.F;
+        }
         if (hset.max_time_ms > 0) {
           const double el =
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
           if (el > hset.max_time_ms) g[1] = 1;
         }
-        DSL_TRY(global_sum(g));
+        if (!rep || hset.max_time_ms > 0) DSL_TRY(global_sum(g));
         if (g[1]) {
           end = DSL_TIME_EXHAUSTED;
           break;
@@ -410,7 +433,7 @@ struct BfsEngine : EngineBase {
           DSL_TRY(grow(&S.spill, &S.spill_cap, std::max<uint64_t>(S.work, 1), false, 0));
           DSL_HIP(hipMemsetAsync(S.ctr, 0, sizeof(LevelCounters), stream));
           DSL_HIP(hipMemsetAsync(S.seg_ctr, 0, sizeof(unsigned long long) * S.nseg * kSegStride, stream));
-          if (W > 1) {
+          if (route) {
             S.cap_fp = std::max<uint64_t>(S.work, 1);
             DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
           }
@@ -448,12 +471,13 @@ struct BfsEngine : EngineBase {
           a.table.slots = S.table;
           a.W = W;
           a.me = S.gid;
+          a.owner_filter = route && first_sharded ? 1 : 0;
           a.out_fp = S.out_fp;
           a.cap_fp = S.cap_fp;
           a.rc = S.rc;
           const uint64_t nchunks = a.segs.chunk0[a.segs.n];
           const int blocks = (int)std::min<uint64_t>(nchunks, kLevelGrid);
-          if (W > 1)
+          if (route)
             hipLaunchKernelGGL((k_level<P, true>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
           else
             hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
@@ -500,7 +524,7 @@ struct BfsEngine : EngineBase {
           span[l] = need;
         }
 
-        if (W > 1) {
+        if (route) {
           std::vector<std::vector<uint64_t>> cnt, src_off;
           DSL_TRY(read_route_counts(cnt));
           for (int l = 0; l < L; l++)
@@ -573,7 +597,7 @@ struct BfsEngine : EngineBase {
             span[l] = need;
           }
         }
-        if (W > 1 || unspilled) {  // counters changed after the first read
+        if (route || unspilled) {  // counters changed after the first read
           for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
           DSL_HIP(hipStreamSynchronize(stream));
         }
@@ -596,7 +620,7 @@ struct BfsEngine : EngineBase {
         std::vector<uint64_t> gsum(8, 0);
         uint64_t enc = ~0ull;
         std::vector<TerminalRec> local_best(L);
-        for (int l = 0; l < L; l++) {
+        for (int l = 0; l < (rep ? 1 : L); l++) {  // replicated: every shard has the same counts
           Shard& S = sh[l];
           gsum[0] += S.lc.new_states;
           uint64_t fn = 0;
@@ -623,8 +647,11 @@ struct BfsEngine : EngineBase {
             enc = std::min(enc, ((uint64_t)b.verdict << 60) | ((b.key >> 12) << 8) | (uint64_t)S.gid);
           }
         }
-        DSL_TRY(global_sum(gsum));
-        if (comm) DSL_TRY(comm->allreduce_u64(&enc, 1, true, stream));
+        if (!rep) {
+          DSL_TRY(global_sum(gsum));
+          if (comm) DSL_TRY(comm->allreduce_u64(&enc, 1, true, stream));
+        }
+        if (route) first_sharded = false;
         if (gsum[3]) {
           set_error("a successor exceeded the packed state's bounds (" + std::to_string(gsum[3]) + " times)");
           return DSL_ERR_STATE_OVERFLOW;
@@ -663,7 +690,7 @@ struct BfsEngine : EngineBase {
               rec[2] = (uint64_t)b.verdict;
               rec[3] = (uint64_t)(b.pred_index + 1);
             }
-          if (comm) DSL_TRY(comm->bcast_u64(rec, 4, wrank, stream));
+          if (comm && !rep) DSL_TRY(comm->bcast_u64(rec, 4, wrank, stream));
           const int v = (int)rec[2];
           end = v == V_TERM_EXCEPTION ? DSL_EXCEPTION_THROWN : v == V_TERM_INVARIANT ? DSL_INVARIANT_VIOLATED
                                                                                      : DSL_GOAL_FOUND;
@@ -686,7 +713,8 @@ struct BfsEngine : EngineBase {
                 hop[0] = p;
                 hop[1] = e;
               }
-            if (comm) DSL_TRY(comm->bcast_u64(hop, 2, r, stream));
+            // a terminal of a replicated level has a local chain on every rank: no exchange
+            if (comm && !rep) DSL_TRY(comm->bcast_u64(hop, 2, r, stream));
             evs.push_back((uint32_t)hop[1]);
             ref = hop[0];
           }

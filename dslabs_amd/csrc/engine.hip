@@ -303,6 +303,7 @@ int dsl_create(const dsl_protocol_desc* proto, const dsl_engine_config* cfg, dsl
   dsl_engine_config c{};
   c.device = -1;
   c.world_size = 1;
+  c.replicate_below = -1;
   if (cfg) c = *cfg;
   if (c.world_size < 1) c.world_size = 1;
   dsl::EngineBase* impl = nullptr;

@@ -222,6 +222,7 @@ struct LevelArgs {
   uint64_t* spill;           // (parent << 20 | event) of VALID states past next_cap
   uint64_t spill_cap;
   int32_t W, me;             // shards (ROUTE only)
+  int32_t owner_filter;      // expand only parents this shard owns (first hash-sharded level)
   FpRec* out_fp;             // W regions of cap_fp records (ROUTE only)
   uint64_t cap_fp;
   RouteCounters* rc;
@@ -267,7 +268,10 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     }
     __syncthreads();
     // 2. enabled events per parent, workgroup-local exclusive scan
-    if (threadIdx.x < pb) off[threadIdx.x + 1] = count_events<P>(rows + threadIdx.x * NW, prm, set);
+    if (threadIdx.x < pb)
+      off[threadIdx.x + 1] = (ROUTE && a.owner_filter && owner_of(fps[threadIdx.x], a.W) != a.me)
+                                 ? 0
+                                 : count_events<P>(rows + threadIdx.x * NW, prm, set);
     __syncthreads();
     if (threadIdx.x == 0) {
       off[0] = 0;

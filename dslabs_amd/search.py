@@ -328,7 +328,8 @@ class Engine:
     """One engine (one GPU, or one shard of a multi-GPU search)."""
 
     def __init__(self, protocol, device: int = -1, rank: int = 0, world_size: int = 1,
-                 virtual_shards: int = 0, comm_id: Optional[bytes] = None, host_comm=None):
+                 virtual_shards: int = 0, comm_id: Optional[bytes] = None, host_comm=None,
+                 replicate_below: int = -1):
         lib = _lib.load()
         self.lib = lib
         self.protocol = protocol
@@ -338,6 +339,7 @@ class Engine:
         cfg.rank = rank
         cfg.world_size = world_size
         cfg.virtual_shards = virtual_shards
+        cfg.replicate_below = replicate_below
         if comm_id is not None:
             ctypes.memmove(cfg.comm_id, comm_id, 128)
         handle = ctypes.c_void_p()

@@ -129,6 +129,8 @@ typedef struct {
   int32_t rank, world_size; /* shard index / number of shards (one process or thread per GPU) */
   int32_t virtual_shards;   /* >1: emulate that many hash shards on this one device (tests) */
   uint8_t comm_id[128];     /* RCCL ncclUniqueId when world_size > 1 */
+  int64_t replicate_below;  /* multi-shard: a level whose frontier is smaller runs replicated on every
+                               shard (no exchange); -1 = default (524288), 0 = always hash-sharded */
 } dsl_engine_config;
 
 /* A decoded event (MessageEnvelope / TimerEnvelope, T/MessageEnvelope.java, T/TimerEnvelope.java). */

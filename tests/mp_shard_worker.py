@@ -64,7 +64,8 @@ def main():
             s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
             s.maxDepth(9)
         s.table_log2_slots = 22
-        eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc)
+        rb = int(os.environ.get("DSL_TEST_REPLICATE_BELOW", "0"))
+        eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=rb)
         r = eng.bfs(proto.initial_state(), s)
         res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states,
                    exchanged=eng.kernel_stats()["exchanged"])

@@ -33,10 +33,10 @@ def test_multipaxos_parity(name):
         assert r.max_depth == case["terminal_depth"]
 
 
-@pytest.mark.parametrize("shards", [2, 8])
-def test_multipaxos_c5_sharded(shards):
+@pytest.mark.parametrize("shards,rep", [(2, 0), (8, 0), (8, 2000)])
+def test_multipaxos_c5_sharded(shards, rep):
     case = GOLD["mp_c5_d12"]
-    r = _run(case, virtual_shards=shards)
+    r = _run(case, virtual_shards=shards, replicate_below=rep)
     assert r.per_depth == case["per_depth"]
 
 

@@ -14,21 +14,23 @@ LAB0 = json.load(open(os.path.join(GOLD, "lab0.json")))
 SIP = json.load(open(os.path.join(GOLD, "sipaxos.json")))
 
 
-@pytest.mark.parametrize("shards", [2, 3, 8])
-def test_virtual_shards_lab0(shards):
-    eng = Engine(PingPong(2, 10), virtual_shards=shards)
+@pytest.mark.parametrize("shards,rep", [(2, 0), (3, 0), (8, 0), (3, 40), (8, -1)])
+def test_virtual_shards_lab0(shards, rep):
+    """rep = replicate_below: 0 = hash-sharded from the first level, 40 = replicated small
+    levels then sharded (crossover mid-search), -1 = default (this space stays replicated)."""
+    eng = Engine(PingPong(2, 10), virtual_shards=shards, replicate_below=rep)
     s = SearchSettings().addInvariant(RESULTS_OK).addPrune(CLIENTS_DONE)
     s.table_log2_slots = 20
     r = eng.bfs(eng.protocol.initial_state(), s)
     assert r.endCondition() == EndCondition.SPACE_EXHAUSTED
     assert r.per_depth == LAB0["lab0_2c10p_exhaustive"]["per_depth"]
-    assert eng.kernel_stats()["exchanged"] > 0
+    assert (eng.kernel_stats()["exchanged"] > 0) == (rep >= 0)
 
 
-@pytest.mark.parametrize("shards", [2, 5])
-def test_virtual_shards_sipaxos(shards):
+@pytest.mark.parametrize("shards,rep", [(2, 0), (5, 0), (5, 100)])
+def test_virtual_shards_sipaxos(shards, rep):
     proto = SIPaxos(2, 3, ("a", "b"))
-    eng = Engine(proto, virtual_shards=shards)
+    eng = Engine(proto, virtual_shards=shards, replicate_below=rep)
     s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
     s.maxDepth(9)
     s.table_log2_slots = 22
@@ -36,9 +38,9 @@ def test_virtual_shards_sipaxos(shards):
     assert r.per_depth == SIP["sipaxos_2p3a_d9"]["per_depth"]
 
 
-@pytest.mark.parametrize("shards", [2, 4])
-def test_virtual_shards_terminal_trace(shards):
-    eng = Engine(PingPong(1, 10, check_value=False), virtual_shards=shards)
+@pytest.mark.parametrize("shards,rep", [(2, 0), (4, 0), (4, -1)])
+def test_virtual_shards_terminal_trace(shards, rep):
+    eng = Engine(PingPong(1, 10, check_value=False), virtual_shards=shards, replicate_below=rep)
     s = SearchSettings().addInvariant(RESULTS_OK).addGoal(CLIENTS_DONE)
     s.table_log2_slots = 20
     r = eng.bfs(eng.protocol.initial_state(), s)
@@ -48,10 +50,12 @@ def test_virtual_shards_terminal_trace(shards):
     assert st.trace() == LAB0["lab0_mutant_nocheck"]["pinned"]["trace"]
 
 
-@pytest.mark.parametrize("mode,world", [("lab0", 2), ("sipaxos", 3), ("mutant", 2)])
-def test_multiprocess_shards_one_gpu(mode, world):
-    """world processes on cuda:0, one shard each, exchanging through the gloo host transport."""
-    res = run_workers(mode, world)
+@pytest.mark.parametrize("mode,world,rep", [("lab0", 2, 0), ("sipaxos", 3, 0), ("mutant", 2, 0), ("lab0", 3, 40),
+                                            ("sipaxos", 2, 100), ("mutant", 2, 40)])
+def test_multiprocess_shards_one_gpu(mode, world, rep):
+    """world processes on cuda:0, one shard each, exchanging through the gloo host transport;
+    rep > 0: replicated small levels first (a terminal inside them walks a local chain)."""
+    res = run_workers(mode, world, replicate_below=rep)
     for r in res:
         assert r["errors"] == []
     if mode == "lab0":
@@ -66,4 +70,5 @@ def test_multiprocess_shards_one_gpu(mode, world):
         else:
             assert r["end"] == "INVARIANT_VIOLATED" and r["depth"] == 3
             assert r["trace"] == LAB0["lab0_mutant_nocheck"]["pinned"]["trace"]
-    assert sum(r["exchanged"] for r in res) > 0
+    if not (mode == "mutant" and rep > 0):
+        assert sum(r["exchanged"] for r in res) > 0

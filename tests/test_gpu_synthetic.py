@@ -39,9 +39,9 @@ def test_synthetic_parity(name):
         assert rep["depth"] == st.depth() == case["terminal_depth"]
 
 
-@pytest.mark.parametrize("shards", [2, 5, 8])
-def test_synthetic_sharded(shards):
+@pytest.mark.parametrize("shards,rep", [(2, 0), (5, 0), (8, 0), (8, 1000)])
+def test_synthetic_sharded(shards, rep):
     for name in ("synth_c3_d5", "synth_2n_k4_exhaustive"):
         case = GOLD[name]
-        r = _run(case, virtual_shards=shards)
+        r = _run(case, virtual_shards=shards, replicate_below=rep)
         assert r.per_depth == case["per_depth"], (name, shards)
