@@ -41,6 +41,13 @@ WORKLOADS = {
     "synthetic": dict(depth=10, cpu_depth=6, table_log2=31,
                       desc="table-driven synthetic protocol (5 nodes, K=64, pokes at v%7==0, seed 0x5EEDD51AB5), "
                            "invariant NOT_ALL_MAX, BFS to maxDepth"),
+    # BASELINE config C2: lab1 AMO KV, ClientServerPart2Test.test10 workload
+    # (APPEND:foo:%i x 3, APPENDS_LINEARIZABLE, prune CLIENTS_DONE), exhaustive; "amokv3" = the
+    # same with 3 clients (1,225,876 states).
+    "amokv": dict(depth=-1, cpu_depth=-1, clients=2,
+                  desc="lab1 AMO KV, 2 clients APPEND:foo:%i x3, APPENDS_LINEARIZABLE, prune CLIENTS_DONE, exhaustive"),
+    "amokv3": dict(depth=-1, cpu_depth=14, clients=3,
+                   desc="lab1 AMO KV, 3 clients APPEND:foo:%i x3, APPENDS_LINEARIZABLE, prune CLIENTS_DONE, exhaustive"),
     "sipaxos": dict(depth=15, cpu_depth=10,
                     desc="reference SingleInstancePaxos (2 proposers, 3 acceptors), invariants "
                          "Integrity+Agreement, BFS to maxDepth"),
@@ -50,7 +57,8 @@ WORKLOADS = {
 def build_search(name: str, depth: int):
     from dslabs_amd import SearchSettings
     from dslabs_amd import RESULTS_OK
-    from dslabs_amd.protocols import MultiPaxos, SIPaxos, Synthetic
+    from dslabs_amd import CLIENTS_DONE
+    from dslabs_amd.protocols import AmoKV, MultiPaxos, SIPaxos, Synthetic
     if name == "multipaxos":
         proto = MultiPaxos(3, 2, "append-xy")
         s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
@@ -59,6 +67,14 @@ def build_search(name: str, depth: int):
         s.table_log2_slots = 28
         return proto, s, ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
                           "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
+    if name in ("amokv", "amokv3"):
+        c = WORKLOADS[name]["clients"]
+        proto = AmoKV(c, "samekey3")
+        s = SearchSettings().addInvariant(proto.predicate("APPENDS_LINEARIZABLE")).addPrune(CLIENTS_DONE)
+        s.maxDepth(depth)
+        s.table_log2_slots = 24
+        return proto, s, ["--proto", "amokv", "--clients", str(c), "--workload", "samekey3", "--inv",
+                          "APPENDS_LINEARIZABLE", "--prune", "CLIENTS_DONE"]
     if name == "synthetic":
         proto = Synthetic(5, 64, 7)
         s = SearchSettings().addInvariant(proto.predicate("NOT_ALL_MAX"))

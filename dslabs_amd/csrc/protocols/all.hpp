@@ -1,5 +1,6 @@
 // all.hpp -- every protocol with device transition functions.
 #pragma once
+#include "amokv.hpp"
 #include "multipaxos.hpp"
 #include "pingpong.hpp"
 #include "sipaxos.hpp"

@@ -252,3 +252,113 @@ class Synthetic(Protocol):
         if e.is_timer:
             return f"Timer(-> {self.addresses[e.to]}, SynthTimer({e.fields[0]}))"
         return f"Message({self.addresses[e.from_]} -> {self.addresses[e.to]}, Poke())"
+
+
+class AmoKV(Protocol):
+    """lab1 at-most-once client/server KV store (builder-authored): "server"
+    (SimpleServer over AMOApplication(KVStore)) and ClientWorkers "client1..c" (SimpleClient).
+    Workloads are the KVStoreWorkload ones the lab1 search tests use
+    (labs/lab1-clientserver/tst/dslabs/kvstore/KVStoreWorkload.java, ClientServerPart2Test.java)."""
+
+    proto_id = DSL_PROTO_AMOKV
+    PREDICATES = {"APPENDS_LINEARIZABLE": (300, "Sequence of appends to the same key is linearizable")}
+    # same names and templates as oracle/proto_amokv.hpp (commands, results, numTimes)
+    WORKLOADS = {
+        "diffkey3": (["APPEND:KEY-%a:0", "APPEND:KEY-%a:1", "APPEND:KEY-%a:2"], ["0", "01", "012"], 1),
+        "diffkey2": (["APPEND:KEY-%a:0", "APPEND:KEY-%a:1"], ["0", "01"], 1),
+        "samekey3": (["APPEND:foo:%i"], [], 3),
+        "samekey2": (["APPEND:foo:%i"], [], 2),
+        "appendappendget": (["APPEND:foo:bar", "APPEND:foo:bar", "GET:foo"], ["bar", "barbar", "barbar"], 1),
+        "putappendget": (["PUT:foo:bar", "APPEND:foo:baz", "GET:foo"], ["Ok", "barbaz", "barbaz"], 1),
+        "getput": (["GET:foo", "PUT:foo:bar", "GET:foo"], ["KeyNotFound", "Ok", "bar"], 1),
+    }
+    OPS = {"GET": 0, "PUT": 1, "APPEND": 2}
+    RTYPES = ["AppendResult", "GetResult", "KeyNotFound", "PutOk"]
+
+    def __init__(self, clients: int = 2, workload: str = "diffkey3"):
+        cmds, results, times = self.WORKLOADS[workload]
+        self.clients = clients
+        self.workload = workload
+        self.addresses = ["server"] + [f"client{i}" for i in range(1, clients + 1)]
+        self.keys, self.syms = [], []
+        self.cmds = []  # per client: [(op, key, value)]
+        self.expected = []  # per client: [result string or None]
+        n = len(cmds) * times
+        self.ncmds = n
+        for c in range(1, clients + 1):
+            cl, ex = [], []
+            for i in range(n):
+                t = cmds[i % len(cmds)].replace("%a", f"client{c}").replace("%i", str(i + 1))
+                sp = t.split(":", 2)
+                op = sp[0]
+                key = sp[1] if op != "GET" or len(sp) == 2 else sp[1] + sp[2]
+                val = sp[2] if op != "GET" else None
+                if key not in self.keys:
+                    self.keys.append(key)
+                if val is not None and val not in self.syms:
+                    self.syms.append(val)
+                cl.append((op, key, val))
+                ex.append(results[i % len(cmds)].replace("%a", f"client{c}").replace("%i", str(i + 1))
+                          if results else None)
+            self.cmds.append(cl)
+            self.expected.append(ex)
+        assert len(self.keys) <= 3 and len(self.syms) <= 4 and n <= 3 and clients <= 3
+        assert len({len(s) for s in self.syms}) <= 1, "value tokens must have equal length"
+
+    def _value_bits(self, s: str) -> int:
+        toks, w = [], len(self.syms[0]) if self.syms else 1
+        for k in range(0, len(s), w):
+            toks.append(self.syms.index(s[k:k + w]))
+        v = len(toks)
+        for j, t in enumerate(toks):
+            v |= t << (4 + 2 * j)
+        return v
+
+    def _result_bits(self, op: str, r: str) -> int:
+        if op == "APPEND":
+            return 0 | (self._value_bits(r) << 2)
+        if op == "GET":
+            return 2 if r == "KeyNotFound" else 1 | (self._value_bits(r) << 2)
+        return 3  # PutOk
+
+    def params(self):
+        ps = [self.clients, self.ncmds]
+        for c in range(3):
+            for k in range(3):
+                if c < self.clients and k < self.ncmds:
+                    op, key, val = self.cmds[c][k]
+                    exp = self.expected[c][k]
+                    ps += [self.OPS[op], self.keys.index(key), self.syms.index(val) if val is not None else 0,
+                           self._result_bits(op, exp) if exp is not None else -1]
+                else:
+                    ps += [0, 0, 0, -1]
+        return ps
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        pid, full = self.PREDICATES[name]
+        return StatePredicate(full, pid)
+
+    def _value_str(self, v: int) -> str:
+        return "".join(self.syms[(v >> (4 + 2 * j)) & 3] for j in range(v & 15))
+
+    def _result_str(self, r: int) -> str:
+        t, v = r & 3, r >> 2
+        if t == 0:
+            return f"AppendResult({self._value_str(v)})"
+        if t == 1:
+            return f"GetResult({self._value_str(v)})"
+        return "KeyNotFound()" if t == 2 else "PutOk()"
+
+    def _cmd_str(self, c: int, seq: int) -> str:
+        op, key, val = self.cmds[c - 1][seq - 1]
+        return {"GET": f"Get({key})", "PUT": f"Put({key}, {val})", "APPEND": f"Append({key}, {val})"}[op]
+
+    def render_event(self, e) -> str:
+        a = self.addresses
+        if e.is_timer:
+            return f"Timer(-> {a[e.to]}, ClientTimer({e.fields[0]}))"
+        seq = e.fields[0]
+        if e.type == 0:
+            return f"Message({a[e.from_]} -> {a[e.to]}, Request({self._cmd_str(e.from_, seq)}, {seq}))"
+        return f"Message({a[e.from_]} -> {a[e.to]}, Reply({self._result_str(e.fields[1])}, {seq}))"

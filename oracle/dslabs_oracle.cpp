@@ -16,6 +16,7 @@
 #include <iostream>
 
 #include "oracle_core.hpp"
+#include "proto_amokv.hpp"
 #include "proto_multipaxos.hpp"
 #include "proto_pingpong.hpp"
 #include "proto_sipaxos.hpp"
@@ -116,6 +117,16 @@ static Scenario build(const Args& a) {
       if (p) return *p;
       if (n == "LOGS_CONSISTENT_ALL_SLOTS") return multipaxos::logsConsistent(cfg);
       if (n == "APPENDS_LINEARIZABLE") return multipaxos::appendsLinearizable(cfg);
+      throw std::runtime_error("unknown predicate " + n);
+    };
+  } else if (a.proto == "amokv") {
+    amokv::Config cfg = amokv::Config::fromArgs(a.geti("clients", 2), a.get("workload", "diffkey3"));
+    sc.init = amokv::initial(cfg, sc.names);
+    Names* nm = &sc.names;
+    sc.pred = [common, cfg, nm](const std::string& n) -> Predicate {
+      auto p = common(n);
+      if (p) return *p;
+      if (n == "APPENDS_LINEARIZABLE") return amokv::appendsLinearizable(cfg, *nm);
       throw std::runtime_error("unknown predicate " + n);
     };
   } else if (a.proto == "synthetic") {

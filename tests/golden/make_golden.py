@@ -165,11 +165,44 @@ SYNTHETIC = {
     "synth_2n_k4_exhaustive": dict(args=SY + ["--nodes", "2", "--values", "4", "--poke-mod", "2"], pinned={}),
 }
 
+KV = ["--proto", "amokv"]
+AMOKV = {
+    # ClientServerPart2Test.test09 (:221-238): 2 clients, appendDifferentKeyWorkload(3), RESULTS_OK
+    "kv_test09_exhaustive": dict(args=KV + ["--clients", "2", "--workload", "diffkey3", "--inv", "RESULTS_OK",
+                                            "--prune", "CLIENTS_DONE"], pinned={}),
+    "kv_test09_goal": dict(args=KV + ["--clients", "2", "--workload", "diffkey3", "--inv", "RESULTS_OK", "--goal",
+                                      "CLIENTS_DONE", "--finish-level"], pinned={}),
+    # ClientServerPart2Test.test10 (:243-263): 2 clients, APPEND:foo:%i x 3, APPENDS_LINEARIZABLE
+    "kv_test10_exhaustive": dict(args=KV + ["--clients", "2", "--workload", "samekey3", "--inv",
+                                            "APPENDS_LINEARIZABLE", "--prune", "CLIENTS_DONE"], pinned={}),
+    "kv_3c_diffkey3": dict(args=KV + ["--clients", "3", "--workload", "diffkey3", "--inv", "RESULTS_OK", "--prune",
+                                      "CLIENTS_DONE"], pinned={}),
+    # BASELINE C2 at 3 clients: 1,225,876 states (the oracle takes ~6 min; checked on the GPU only)
+    "kv_3c_samekey3": dict(args=KV + ["--clients", "3", "--workload", "samekey3", "--inv", "APPENDS_LINEARIZABLE",
+                                      "--prune", "CLIENTS_DONE"], pinned={}),
+    # test08-style workloads with two clients on one key: RESULTS_OK is violated
+    "kv_appendappendget_2c": dict(args=KV + ["--clients", "2", "--workload", "appendappendget", "--inv",
+                                             "RESULTS_OK", "--prune", "CLIENTS_DONE", "--finish-level"], pinned={}),
+    "kv_putappendget_1c": dict(args=KV + ["--clients", "1", "--workload", "putappendget", "--inv", "RESULTS_OK",
+                                          "--prune", "CLIENTS_DONE"], pinned={}),
+    "kv_getput_2c": dict(args=KV + ["--clients", "2", "--workload", "getput", "--inv", "RESULTS_OK", "--prune",
+                                    "CLIENTS_DONE", "--finish-level"], pinned={}),
+    # APPENDS_LINEARIZABLE over a workload with a GET: the predicate throws (invariant violated)
+    "kv_linearizable_throws": dict(args=KV + ["--clients", "1", "--workload", "appendappendget", "--inv",
+                                              "APPENDS_LINEARIZABLE", "--prune", "CLIENTS_DONE", "--finish-level"],
+                                   pinned={}),
+    "kv_test10_partition": dict(args=KV + ["--clients", "2", "--workload", "samekey2", "--inv",
+                                           "APPENDS_LINEARIZABLE", "--prune", "CLIENTS_DONE", "--partition",
+                                           "server,client1|client2"], pinned={}),
+}
+
 if __name__ == "__main__":
-    which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic"}
+    which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic", "amokv"}
     if "lab0" in which or "sipaxos" in which:
         gen_lab0_sip()
     if "multipaxos" in which:
         gen(MULTIPAXOS, "multipaxos.json")
     if "synthetic" in which:
         gen(SYNTHETIC, "synthetic.json")
+    if "amokv" in which:
+        gen(AMOKV, "amokv.json")

@@ -179,6 +179,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, set);
     case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, set);
     case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
+    case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
   }
   return 2;
 }

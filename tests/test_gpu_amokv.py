@@ -1,0 +1,50 @@
+"""lab1 at-most-once KV store (BASELINE C2) on the MI355X engine vs the oracle's
+golden vectors: per-depth counts, end conditions, replayable traces, sharding."""
+import json
+import os
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import Engine
+
+pytestmark = pytest.mark.gpu
+GOLD = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "amokv.json")))
+
+
+def _run(case, **eng):
+    proto = argmap.protocol(case["args"])
+    s = argmap.settings(case["args"], proto)
+    e = Engine(proto, **eng)
+    try:
+        return e.bfs(proto.initial_state(), s)
+    finally:
+        e.close()
+
+
+@pytest.mark.parametrize("name", sorted(GOLD))
+def test_amokv_parity(name):
+    case = GOLD[name]
+    r = _run(case)
+    assert r.endCondition().name == case["end"]
+    assert r.per_depth == case["per_depth"], name
+    assert r.states == case["states"]
+    if case["terminal_depth"] >= 0:
+        assert r.max_depth == case["terminal_depth"]
+        st = r.invariantViolatingState() or r.goalMatchingState()
+        args = [a for a in case["args"] if a != "--finish-level"]
+        rep = oracle_util.replay(args, st.trace())
+        assert rep["ok"], rep["error"]
+        assert rep["depth"] == st.depth() == case["terminal_depth"]
+        if r.endCondition().name == "INVARIANT_VIOLATED":
+            # a violated invariant is false or threw (TestSettings.invariantViolated)
+            assert not all(i["value"] and not i["threw"] for i in rep["invariants"])
+
+
+@pytest.mark.parametrize("shards,rep", [(2, 0), (4, 0), (4, 500)])
+def test_amokv_sharded(shards, rep):
+    for name in ("kv_test10_exhaustive", "kv_3c_diffkey3"):
+        case = GOLD[name]
+        r = _run(case, virtual_shards=shards, replicate_below=rep)
+        assert r.per_depth == case["per_depth"], (name, shards)

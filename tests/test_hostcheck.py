@@ -72,6 +72,16 @@ CASES = {
                     ["--proto", "synthetic", "--inv", "NOT_ALL_MAX", "--max-depth", "6"]),
     "synth_2n_k4": ([3, 2, 4, 2, 0x5EEDD51AB5, "--", "/", "/", -1],
                     ["--proto", "synthetic", "--nodes", "2", "--values", "4", "--poke-mod", "2"]),
+    # lab1 AMO KV (C2): params from dslabs_amd.protocols.AmoKV(clients, workload).params()
+    "kv_test09": ([4, 2, 3, 2, 0, 0, 4, 2, 0, 1, 264, 2, 0, 2, 2316, 2, 1, 0, 4, 2, 1, 1, 264, 2, 1, 2, 2316, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, -1],
+                  ["--proto", "amokv", "--clients", "2", "--workload", "diffkey3", "--inv", "RESULTS_OK", "--prune",
+                   "CLIENTS_DONE"]),
+    "kv_test10": ([4, 2, 3, 2, 0, 0, -1, 2, 0, 1, -1, 2, 0, 2, -1, 2, 0, 0, -1, 2, 0, 1, -1, 2, 0, 2, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 300, "/", "/", 2, -1],
+                  ["--proto", "amokv", "--clients", "2", "--workload", "samekey3", "--inv", "APPENDS_LINEARIZABLE",
+                   "--prune", "CLIENTS_DONE"]),
+    "kv_putappendget": ([4, 1, 3, 1, 0, 0, 3, 2, 0, 1, 264, 0, 0, 0, 265, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, -1],
+                        ["--proto", "amokv", "--clients", "1", "--workload", "putappendget", "--inv", "RESULTS_OK",
+                         "--prune", "CLIENTS_DONE"]),
 }
 
 

@@ -77,3 +77,14 @@ def test_synthetic_oracle_matches_fixture(name):
     r = oracle_util.run("bfs", case["args"], timeout=300)
     assert r["end"] == case["end"]
     assert r["per_depth"] == case["per_depth"]
+
+
+KVG = _load("amokv.json") if os.path.exists(os.path.join(GOLD, "amokv.json")) else {}
+
+
+@pytest.mark.parametrize("name", sorted(n for n in KVG if n != "kv_3c_samekey3"))  # that one takes minutes
+def test_amokv_oracle_matches_fixture(name):
+    case = KVG[name]
+    r = oracle_util.run("bfs", case["args"], timeout=300)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
