@@ -48,6 +48,11 @@ WORKLOADS = {
                   desc="lab1 AMO KV, 2 clients APPEND:foo:%i x3, APPENDS_LINEARIZABLE, prune CLIENTS_DONE, exhaustive"),
     "amokv3": dict(depth=-1, cpu_depth=14, clients=3,
                    desc="lab1 AMO KV, 3 clients APPEND:foo:%i x3, APPENDS_LINEARIZABLE, prune CLIENTS_DONE, exhaustive"),
+    # BASELINE config C4: lab2 primary-backup + ViewServer, 2 servers, 1 client
+    # putGetWorkload, RESULTS_OK, prunes CLIENTS_DONE and hasViewReply(INITIAL_VIEWNUM + 3).
+    "pb": dict(depth=22, cpu_depth=14,
+               desc="lab2 primary-backup + ViewServer, 2 servers, 1 client putGet, RESULTS_OK, prunes CLIENTS_DONE "
+                    "and hasViewReply(4), BFS to maxDepth from the start state"),
     "sipaxos": dict(depth=15, cpu_depth=10,
                     desc="reference SingleInstancePaxos (2 proposers, 3 acceptors), invariants "
                          "Integrity+Agreement, BFS to maxDepth"),
@@ -58,7 +63,7 @@ def build_search(name: str, depth: int):
     from dslabs_amd import SearchSettings
     from dslabs_amd import RESULTS_OK
     from dslabs_amd import CLIENTS_DONE
-    from dslabs_amd.protocols import AmoKV, MultiPaxos, SIPaxos, Synthetic
+    from dslabs_amd.protocols import PB, AmoKV, MultiPaxos, SIPaxos, Synthetic
     if name == "multipaxos":
         proto = MultiPaxos(3, 2, "append-xy")
         s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
@@ -67,6 +72,13 @@ def build_search(name: str, depth: int):
         s.table_log2_slots = 28
         return proto, s, ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
                           "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
+    if name == "pb":
+        proto = PB(2, 1, "putget")
+        s = SearchSettings().addInvariant(RESULTS_OK).addPrune(CLIENTS_DONE).addPrune(proto.predicate("hasViewReply:4"))
+        s.maxDepth(depth)
+        s.table_log2_slots = 28
+        return proto, s, ["--proto", "pb", "--servers", "2", "--clients", "1", "--workload", "putget", "--inv",
+                          "RESULTS_OK", "--prune", "CLIENTS_DONE", "--prune", "hasViewReply:4"]
     if name in ("amokv", "amokv3"):
         c = WORKLOADS[name]["clients"]
         proto = AmoKV(c, "samekey3")

@@ -243,6 +243,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_MULTIPAXOS: return make_engine<MultiPaxos>(d, cfg, out);
     case DSL_PROTO_SYNTHETIC: return make_engine<Synthetic>(d, cfg, out);
     case DSL_PROTO_AMOKV: return make_engine<AmoKV>(d, cfg, out);
+    case DSL_PROTO_PB: return make_engine<PB>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -275,6 +276,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_MULTIPAXOS: return (int)sizeof(dsl::MultiPaxos::State);
     case DSL_PROTO_SYNTHETIC: return (int)sizeof(dsl::Synthetic::State);
     case DSL_PROTO_AMOKV: return (int)sizeof(dsl::AmoKV::State);
+    case DSL_PROTO_PB: return (int)sizeof(dsl::PB::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }

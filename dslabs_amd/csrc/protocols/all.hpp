@@ -2,6 +2,7 @@
 #pragma once
 #include "amokv.hpp"
 #include "multipaxos.hpp"
+#include "pb.hpp"
 #include "pingpong.hpp"
 #include "sipaxos.hpp"
 #include "synthetic.hpp"

@@ -1,0 +1,424 @@
+// pb.hpp -- lab2 primary-backup with a ViewServer (BASELINE config C4) as node-local device
+// handlers. The reference's lab2 classes are stubs (labs/lab2-primarybackup/src/dslabs/
+// primarybackup/*.java); this is the builder-authored solution of DESIGN.md §12, restated
+// object-style in oracle/proto_pb.hpp (whose ViewServer passes the reference's ViewServerTest).
+//
+// Nodes: 0 = "viewserver", 1..S = "server1.." (PBServer), S+1.. = "client1.." (ClientWorker around
+// a PBClient). Server ids in views: 1..3, 0 = null. View = num:4 | primary:2 @4 | backup:2 @6.
+// KV values: len:2 | 3 symbols x 2 bits @2 (8 bits); results: type:2 | value @2 (10 bits).
+//
+// Node words (3):
+//   viewserver: w0 = view:8 | acked @8 | recent:3 @9 | aliveLast:3 @12 | maxSent:4 @15
+//     (maxSent = the highest view number of any ViewReply it has sent: the network is a set that
+//      never loses a message and only the ViewServer sends ViewReplies, so "the network holds a
+//      ViewReply with viewNum >= n" (PrimaryBackupTest.hasViewReply) is exactly maxSent >= n; it is
+//      a function of the network, so state equality is unchanged)
+//   server: w0 = view:8 | started @8 | lastStarted:4 @9;  w1 = key0:8 | key1:8 @8 | amo0:12 @16;
+//           w2 = amo1:12   (amo = seq:2 | result:10 @2)
+//   client: w0 = viewNum:4 | primary:2 @4 | seq:2 @6 | hasResult @8 | nres:2 @9 | ntim:3 @11 |
+//           timer seqs 4 x 2 @14;  w1 = result:10 | results[0]:10 @10 | results[1]:10 @20;
+//           w2 = results[2]:10
+// Records (64 bit): type:4 @60 | from:3 @57 | to:3 @54 | payload
+//   0 Ping num:4      1 GetView      2 ViewReply view:8      3 Request seq:2
+//   4 Reply seq:2 | result:10 @2     5 StateTransfer view:8 | app:40 @8 (w1, w2 of the primary)
+//   6 StateTransferAck num:4         7 Forward num:4 | client:3 @4 | seq:2 @7      8 ForwardAck (same)
+// PingCheckTimer (viewserver, 100 ms) and PingTimer (servers, 25 ms) are re-set on every fire:
+// constant one-entry queues, not stored. Client queues hold ClientTimer(seq) (100 ms): head only.
+#pragma once
+#include "../nodestate.hpp"
+
+namespace dsl {
+
+struct PB {
+  static constexpr int kMaxServers = 3, kMaxClients = 2, kMaxCmds = 3, kMaxKeys = 2, kTimerCap = 4;
+  static constexpr int kNodes = 1 + kMaxServers + kMaxClients, kNodeWords = 3, kNetCap = 64, kMaxSends = 3;
+  static constexpr int kMaxView = 15;
+  using Rec = uint64_t;
+  using State = StateOf<PB>;
+  enum { M_PING = 0, M_GETVIEW, M_VIEWREPLY, M_REQUEST, M_REPLY, M_ST, M_STACK, M_FORWARD, M_FORWARDACK,
+         T_PINGCHECK = 9, T_PING = 10, T_CLIENT = 11 };
+  enum { OP_GET = 0, OP_PUT = 1, OP_APPEND = 2 };
+  enum { R_APPEND = 0, R_GET = 1, R_NOTFOUND = 2, R_PUTOK = 3 };
+
+  struct Params {
+    int32_t servers, clients, ncmds, pad;
+    int32_t op[kMaxClients][kMaxCmds], key[kMaxClients][kMaxCmds], sym[kMaxClients][kMaxCmds];
+    int32_t expected[kMaxClients][kMaxCmds];  // result encoding (10 bits), -1 = none
+  };
+
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
+
+  static DSL_HD Rec msg(int type, int from, int to, uint64_t payload) {
+    return ((Rec)type << 60) | ((Rec)from << 57) | ((Rec)to << 54) | payload;
+  }
+  static DSL_HD int m_type(Rec m) { return (int)(m >> 60); }
+  static DSL_HD int rec_from(Rec m) { return (int)((m >> 57) & 7); }
+  static DSL_HD int rec_to(Rec m) { return (int)((m >> 54) & 7); }
+  static DSL_HD int msg_class(Rec r) { return m_type(r); }
+
+  // views
+  static DSL_HD int v_num(int v) { return v & 15; }
+  static DSL_HD int v_p(int v) { return (v >> 4) & 3; }
+  static DSL_HD int v_b(int v) { return (v >> 6) & 3; }
+  static DSL_HD int mk_view(int n, int p, int b) { return n | (p << 4) | (b << 6); }
+
+  // ---- application: KV + AMO over (w1, w2) of a server ----------------------------------------------
+  static DSL_HD int val_len(int v) { return v & 3; }
+  // returns the 10-bit result, or -1 for a superseded command, -2 on overflow
+  static DSL_HD int execute(uint32_t* w, int c, int seq, const Params& p) {
+    const int amo = c == 0 ? get(w, 48, 12) : get(w, 64, 12);
+    const int last = amo & 3;
+    if (seq < last) return -1;
+    if (seq == last) return amo >> 2;
+    const int k = seq - 1, op = p.op[c][k], key = p.key[c][k], sym = p.sym[c][k];
+    const int vb = 32 + 8 * key;
+    int v = get(w, vb, 8), r;
+    if (op == OP_GET) {
+      r = val_len(v) ? (R_GET | (v << 2)) : R_NOTFOUND;
+    } else if (op == OP_PUT) {
+      put(w, vb, 8, 1 | (sym << 2));
+      r = R_PUTOK;
+    } else {
+      const int n = val_len(v);
+      if (n >= 3) return -2;
+      v = (v & ~3) | (n + 1) | (sym << (2 + 2 * n));
+      put(w, vb, 8, v);
+      r = R_APPEND | (v << 2);
+    }
+    const int na = seq | (r << 2);
+    if (c == 0) put(w, 48, 12, na); else put(w, 64, 12, na);
+    return r;
+  }
+
+  // ---- view server (README.md:161-216; pinned by ViewServerTest) --------------------------------------
+  static DSL_HD int vs_idle(int alive, int p, int b, const Params& prm) {  // lowest live server not P/B
+    for (int s = 1; s <= prm.servers; s++)
+      if (((alive >> (s - 1)) & 1) && s != p && s != b) return s;
+    return 0;
+  }
+  static DSL_HD bool vs_new_view(uint32_t* w, int p, int b) {
+    const int n = v_num(get(w, 0, 8)) + 1;
+    if (n > kMaxView) return false;
+    put(w, 0, 8, mk_view(n, p, b));
+    put(w, 8, 1, 0);
+    return true;
+  }
+  static DSL_HD int vs_reply(uint32_t* w, int to, Sender<PB>& out) {
+    const int view = get(w, 0, 8);
+    if (v_num(view) > get(w, 15, 4)) put(w, 15, 4, v_num(view));
+    out.send(msg(M_VIEWREPLY, 0, to, (uint64_t)view));
+    return STEP_OK;
+  }
+  static DSL_HD int vs_ping(uint32_t* w, int from, int n, Sender<PB>& out, const Params& prm) {
+    put(w, 9, 3, get(w, 9, 3) | (1 << (from - 1)));
+    int view = get(w, 0, 8);
+    if (v_num(view) == 0) {  // any server may be the first primary
+      put(w, 0, 8, mk_view(1, from, 0));
+      put(w, 8, 1, 0);
+      view = get(w, 0, 8);
+    }
+    if (from == v_p(view) && n == v_num(view)) put(w, 8, 1, 1);
+    if (get(w, 8, 1) && v_b(view) == 0) {
+      const int s = vs_idle(get(w, 9, 3) | get(w, 12, 3), v_p(view), 0, prm);
+      if (s && !vs_new_view(w, v_p(view), s)) return STEP_OVERFLOW;
+    }
+    return vs_reply(w, from, out);
+  }
+  static DSL_HD int vs_check(uint32_t* w, const Params& prm) {
+    const int alive = get(w, 9, 3);
+    put(w, 12, 3, alive);
+    put(w, 9, 3, 0);
+    const int view = get(w, 0, 8);
+    if (!get(w, 8, 1) || v_num(view) == 0) return STEP_OK;
+    const int P = v_p(view), B = v_b(view);
+    const bool pAlive = (alive >> (P - 1)) & 1, bAlive = B && ((alive >> (B - 1)) & 1);
+    bool ok = true;
+    if (!pAlive) {
+      if (bAlive) ok = vs_new_view(w, B, vs_idle(alive, B, 0, prm));
+    } else if (B && !bAlive) {
+      ok = vs_new_view(w, P, vs_idle(alive, P, 0, prm));
+    } else if (!B) {
+      const int s = vs_idle(alive, P, 0, prm);
+      if (s) ok = vs_new_view(w, P, s);
+    }
+    return ok ? STEP_OK : STEP_OVERFLOW;
+  }
+
+  // ---- PBServer ---------------------------------------------------------------------------------------
+  static DSL_HD int server_msg(int me, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+    const int type = m_type(m), from = rec_from(m);
+    const int view = get(w, 0, 8), P = v_p(view), B = v_b(view);
+    const bool primary = P == me, started = get(w, 8, 1);
+    switch (type) {
+      case M_VIEWREPLY: {
+        const int v = (int)(m & 0xff);
+        if (v_num(v) <= v_num(view)) return STEP_OK;
+        put(w, 0, 8, v);
+        put(w, 8, 1, 0);
+        if (v_p(v) == me) {
+          if (v_b(v) == 0) {
+            put(w, 8, 1, 1);
+            put(w, 9, 4, v_num(v));
+          } else {
+            const uint64_t app = (uint64_t)(w[1] & 0xfffffffu) | ((uint64_t)(w[2] & 0xfffu) << 28);
+            out.send(msg(M_ST, me, v_b(v), (uint64_t)v | (app << 8)));
+          }
+        }
+        return STEP_OK;
+      }
+      case M_ST: {
+        const int v = (int)(m & 0xff);
+        if (v_num(v) < v_num(view) || v_b(v) != me || v_p(v) != from) return STEP_OK;
+        put(w, 0, 8, v);
+        put(w, 8, 1, 0);
+        const uint64_t app = (m >> 8) & ((1ull << 40) - 1);
+        w[1] = (uint32_t)(app & 0xfffffffu);
+        w[2] = (uint32_t)(app >> 28);
+        out.send(msg(M_STACK, me, from, (uint64_t)v_num(v)));
+        return STEP_OK;
+      }
+      case M_STACK:
+        if (primary && !started && (int)(m & 15) == v_num(view)) {
+          put(w, 8, 1, 1);
+          put(w, 9, 4, v_num(view));
+        }
+        return STEP_OK;
+      case M_REQUEST: {
+        const int seq = (int)(m & 3), c = from - 1 - p.servers;
+        if (c < 0 || c >= p.clients || seq < 1 || seq > p.ncmds) return STEP_EXCEPTION;
+        if (!primary || !started) return STEP_OK;
+        if (B == 0) {
+          const int r = execute(w, c, seq, p);
+          if (r == -2) return STEP_OVERFLOW;
+          if (r >= 0) out.send(msg(M_REPLY, me, from, (uint64_t)seq | ((uint64_t)r << 2)));
+        } else {
+          out.send(msg(M_FORWARD, me, B, (uint64_t)v_num(view) | ((uint64_t)from << 4) | ((uint64_t)seq << 7)));
+        }
+        return STEP_OK;
+      }
+      case M_FORWARD:
+      case M_FORWARDACK: {
+        const int n = (int)(m & 15), ca = (int)((m >> 4) & 7), seq = (int)((m >> 7) & 3), c = ca - 1 - p.servers;
+        if (c < 0 || c >= p.clients || seq < 1 || seq > p.ncmds) return STEP_EXCEPTION;
+        if (type == M_FORWARD) {
+          if (v_num(view) != n || B != me || P != from) return STEP_OK;
+          if (execute(w, c, seq, p) == -2) return STEP_OVERFLOW;
+          out.send(msg(M_FORWARDACK, me, from, m & 0x1ff));
+        } else {
+          if (!primary || !started || v_num(view) != n) return STEP_OK;
+          const int r = execute(w, c, seq, p);
+          if (r == -2) return STEP_OVERFLOW;
+          if (r >= 0) out.send(msg(M_REPLY, me, ca, (uint64_t)seq | ((uint64_t)r << 2)));
+        }
+        return STEP_OK;
+      }
+      default:
+        return STEP_EXCEPTION;
+    }
+  }
+
+  // ---- PBClient inside a ClientWorker ---------------------------------------------------------------
+  static DSL_HD int seq_of(const uint32_t* w) { return get(w, 6, 2); }
+  static DSL_HD int has_result(const uint32_t* w) { return get(w, 8, 1); }
+  static DSL_HD int nres(const uint32_t* w) { return get(w, 9, 2); }
+  static DSL_HD int ntim(const uint32_t* w) { return get(w, 11, 3); }
+  static DSL_HD int timer(const uint32_t* w, int j) { return get(w, 14 + 2 * j, 2); }
+  static DSL_HD int result_at(const uint32_t* w, int k) { return k < 2 ? get(w, 42 + 10 * k, 10) : get(w, 64, 10); }
+  static DSL_HD void set_result_at(uint32_t* w, int k, int r) {
+    if (k < 2) put(w, 42 + 10 * k, 10, r); else put(w, 64, 10, r);
+  }
+  static DSL_HD bool push_timer(uint32_t* w, int seq) {
+    const int n = ntim(w);
+    if (n >= kTimerCap) return false;
+    put(w, 14 + 2 * n, 2, seq);
+    put(w, 11, 3, n + 1);
+    return true;
+  }
+  static DSL_HD void send_request(int me, const uint32_t* w, Sender<PB>& out) {
+    const int primary = get(w, 4, 2);
+    if (primary) out.send(msg(M_REQUEST, me, primary, (uint64_t)seq_of(w)));
+    else out.send(msg(M_GETVIEW, me, 0, 0));
+  }
+  static DSL_HD bool worker_continue(int me, uint32_t* w, Sender<PB>& out, const Params& p) {
+    int n = nres(w);
+    if (n < seq_of(w) && has_result(w)) {
+      set_result_at(w, n, get(w, 32, 10));
+      n++;
+      put(w, 9, 2, n);
+    }
+    if (n == seq_of(w) && seq_of(w) < p.ncmds) {  // PBClient.sendCommand
+      put(w, 6, 2, seq_of(w) + 1);
+      put(w, 8, 1, 0);
+      put(w, 32, 10, 0);
+      send_request(me, w, out);
+      return push_timer(w, seq_of(w));
+    }
+    return true;
+  }
+  static DSL_HD int client_msg(int me, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+    const bool waiting = seq_of(w) > 0 && !has_result(w);
+    if (m_type(m) == M_VIEWREPLY) {
+      const int v = (int)(m & 0xff);
+      if (v_num(v) > get(w, 0, 4)) {
+        put(w, 0, 4, v_num(v));
+        put(w, 4, 2, v_p(v));
+        if (waiting) send_request(me, w, out);
+      }
+    } else if (m_type(m) == M_REPLY) {
+      if (waiting && (int)(m & 3) == seq_of(w)) {
+        put(w, 32, 10, (int)((m >> 2) & 0x3ff));
+        put(w, 8, 1, 1);
+      }
+    } else {
+      return STEP_EXCEPTION;
+    }
+    return worker_continue(me, w, out, p) ? STEP_OK : STEP_OVERFLOW;
+  }
+
+  // ---- protocol interface -------------------------------------------------------------------------
+  static DSL_HD int num_nodes(const Params& p) { return 1 + p.servers + p.clients; }
+  static DSL_HD bool is_client(int i, const Params& p) { return i > p.servers; }
+  static DSL_HD void init_node(int i, uint32_t* w, Sender<PB>& out, const Params& p) {
+    if (i == 0) return;                                           // set(PingCheckTimer): constant queue
+    if (!is_client(i, p)) {
+      out.send(msg(M_PING, i, 0, 0));                             // Ping(STARTUP_VIEWNUM); set(PingTimer)
+      return;
+    }
+    if (!worker_continue(i, w, out, p)) out.overflow = true;
+  }
+  static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {
+    return is_client(i, p) ? (ntim(w) > 0) : 1;
+  }
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+    if (i == 0) {
+      if (m_type(m) == M_GETVIEW) return vs_reply(w, rec_from(m), out);
+      if (m_type(m) != M_PING) return STEP_EXCEPTION;
+      const int from = rec_from(m);
+      if (from < 1 || from > p.servers) return STEP_EXCEPTION;
+      return vs_ping(w, from, (int)(m & 15), out, p);
+    }
+    if (!is_client(i, p)) return server_msg(i, w, m, out, p);
+    return client_msg(i, w, m, out, p);
+  }
+  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<PB>& out, const Params& p) {
+    if (i == 0) return vs_check(w, p);
+    if (!is_client(i, p)) {  // PingTimer: the latest view, unless primary of a view not yet started
+      const int view = get(w, 0, 8);
+      const int n = (v_p(view) == i && !get(w, 8, 1)) ? get(w, 9, 4) : v_num(view);
+      out.send(msg(M_PING, i, 0, (uint64_t)n));
+      return STEP_OK;
+    }
+    const int t = timer(w, 0);  // ClientTimer at the head
+    if (seq_of(w) > 0 && !has_result(w) && t == seq_of(w)) {
+      out.send(msg(M_GETVIEW, i, 0, 0));
+      const int primary = get(w, 4, 2);
+      if (primary) out.send(msg(M_REQUEST, i, primary, (uint64_t)t));
+      if (!push_timer(w, t)) return STEP_OVERFLOW;
+    }
+    if (!worker_continue(i, w, out, p)) return STEP_OVERFLOW;
+    const int n = ntim(w);
+    for (int j = 0; j + 1 < kTimerCap; j++) put(w, 14 + 2 * j, 2, j + 1 < n ? timer(w, j + 1) : 0);
+    put(w, 14 + 2 * (kTimerCap - 1), 2, 0);
+    put(w, 11, 3, n - 1);
+    return STEP_OK;
+  }
+
+  // ---- predicates -------------------------------------------------------------------------------------
+  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const Params& p) {
+    const int c0 = 1 + p.servers;
+    switch (pr.id) {
+      case DSL_PRED_RESULTS_OK:
+        for (int c = 0; c < p.clients; c++) {
+          const uint32_t* w = v.node(c0 + c);
+          for (int k = 0; k < nres(w); k++)
+            if (p.expected[c][k] >= 0 && result_at(w, k) != p.expected[c][k]) return PV_FALSE;
+        }
+        return PV_TRUE;
+      case DSL_PRED_CLIENTS_DONE:
+        for (int c = 0; c < p.clients; c++)
+          if (nres(v.node(c0 + c)) < p.ncmds) return PV_FALSE;
+        return PV_TRUE;
+      case DSL_PRED_CLIENT_DONE:
+        if (pr.arg0 < c0 || pr.arg0 >= c0 + p.clients) return PV_THREW;
+        return nres(v.node((int)pr.arg0)) >= p.ncmds ? PV_TRUE : PV_FALSE;
+      case DSL_PRED_NONE_DECIDED:
+        for (int c = 0; c < p.clients; c++)
+          if (nres(v.node(c0 + c)) > 0) return PV_FALSE;
+        return PV_TRUE;
+      case DSL_PRED_CLIENT_HAS_RESULTS:
+        if (pr.arg0 < c0 || pr.arg0 >= c0 + p.clients) return PV_THREW;
+        return nres(v.node((int)pr.arg0)) == pr.arg1 ? PV_TRUE : PV_FALSE;
+      case DSL_PRED_PB_HAS_VIEW_REPLY:
+        return get(v.node(0), 15, 4) >= pr.arg0 ? PV_TRUE : PV_FALSE;
+      default:
+        return PV_THREW;
+    }
+  }
+  static uint32_t pred_reads(const DevPred& pr, const Params& p) {
+    const uint32_t clients = ((1u << p.clients) - 1u) << (1 + p.servers);
+    switch (pr.id) {
+      case DSL_PRED_PB_HAS_VIEW_REPLY: return 1u;  // the viewserver's maxSent (see the header)
+      case DSL_PRED_RESULTS_OK: case DSL_PRED_CLIENTS_DONE: case DSL_PRED_CLIENT_DONE: case DSL_PRED_NONE_DECIDED:
+      case DSL_PRED_CLIENT_HAS_RESULTS: return clients;
+      default: return kReadsAll;
+    }
+  }
+  static bool known_predicate(int id) {
+    return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == DSL_PRED_PB_HAS_VIEW_REPLY;
+  }
+  static bool valid(const Params& p) {
+    if (p.servers < 1 || p.servers > kMaxServers || p.clients < 1 || p.clients > kMaxClients || p.ncmds < 1 ||
+        p.ncmds > kMaxCmds)
+      return false;
+    for (int c = 0; c < p.clients; c++)
+      for (int k = 0; k < p.ncmds; k++)
+        if (p.op[c][k] < 0 || p.op[c][k] > 2 || p.key[c][k] < 0 || p.key[c][k] >= kMaxKeys || p.sym[c][k] < 0 ||
+            p.sym[c][k] > 3)
+          return false;
+    return true;
+  }
+  // params: servers, clients, ncmds, then per client c < 2, command k < 3: op, key, sym, expected
+  static Params from_desc(const dsl_protocol_desc& d) {
+    Params p{};
+    p.servers = (int32_t)d.params[0];
+    p.clients = (int32_t)d.params[1];
+    p.ncmds = (int32_t)d.params[2];
+    for (int c = 0; c < kMaxClients; c++)
+      for (int k = 0; k < kMaxCmds; k++) {
+        const int b = 3 + 4 * (c * kMaxCmds + k);
+        p.op[c][k] = (int32_t)d.params[b];
+        p.key[c][k] = (int32_t)d.params[b + 1];
+        p.sym[c][k] = (int32_t)d.params[b + 2];
+        p.expected[c][k] = (int32_t)d.params[b + 3];
+      }
+    return p;
+  }
+  static void describe_message(Rec m, dsl_event* e) {
+    e->from = rec_from(m);
+    e->to = rec_to(m);
+    e->type = m_type(m);
+    e->n_fields = 1;
+    e->fields[0] = (int64_t)(m & ((1ull << 54) - 1));
+  }
+  static void describe_timer(int i, const uint32_t* w, int, const Params& p, dsl_event* e) {
+    e->is_timer = 1;
+    e->from = e->to = i;
+    e->n_fields = 1;
+    if (i == 0) {
+      e->type = T_PINGCHECK;
+      e->timer_min = e->timer_max = 100;
+      e->fields[0] = 0;
+    } else if (!is_client(i, p)) {
+      e->type = T_PING;
+      e->timer_min = e->timer_max = 25;
+      e->fields[0] = 0;
+    } else {
+      e->type = T_CLIENT;
+      e->timer_min = e->timer_max = 100;
+      e->fields[0] = timer(w, 0);
+    }
+  }
+};
+
+}  // namespace dsl

@@ -18,6 +18,7 @@ DSL_PROTO_SIPAXOS = 2
 DSL_PROTO_SYNTHETIC = 3
 DSL_PROTO_AMOKV = 4
 DSL_PROTO_MULTIPAXOS = 5
+DSL_PROTO_PB = 6
 
 
 class Protocol:
@@ -362,3 +363,125 @@ class AmoKV(Protocol):
         if e.type == 0:
             return f"Message({a[e.from_]} -> {a[e.to]}, Request({self._cmd_str(e.from_, seq)}, {seq}))"
         return f"Message({a[e.from_]} -> {a[e.to]}, Reply({self._result_str(e.fields[1])}, {seq}))"
+
+
+class PB(Protocol):
+    """lab2 primary-backup with a ViewServer (builder-authored): "viewserver",
+    PBServers "server1..S", ClientWorkers "client1..c" around PBClients; KVStore workloads as in
+    lab1 (PrimaryBackupTest uses putGetWorkload, PrimaryBackupTest.java:680-711)."""
+
+    proto_id = DSL_PROTO_PB
+    WORKLOADS = dict(AmoKV.WORKLOADS, putget=(["PUT:foo:bar", "GET:foo"], ["Ok", "bar"], 1))
+    RTYPES = AmoKV.RTYPES
+
+    def __init__(self, servers: int = 2, clients: int = 1, workload: str = "putget"):
+        self.servers = servers
+        self.clients = clients
+        self.workload = workload
+        self.addresses = ["viewserver"] + [f"server{i}" for i in range(1, servers + 1)] + \
+                         [f"client{i}" for i in range(1, clients + 1)]
+        # reuse the KV workload expansion of AmoKV (commands per client, keys, value tokens)
+        kv = AmoKV.__new__(AmoKV)
+        saved = AmoKV.WORKLOADS
+        AmoKV.WORKLOADS = self.WORKLOADS
+        try:
+            AmoKV.__init__(kv, clients, workload)
+        finally:
+            AmoKV.WORKLOADS = saved
+        self.kv = kv
+        assert len(kv.keys) <= 2 and servers <= 3 and clients <= 2 and kv.ncmds <= 3
+
+    def _value_bits(self, s: str) -> int:
+        w = len(self.kv.syms[0]) if self.kv.syms else 1
+        toks = [self.kv.syms.index(s[k:k + w]) for k in range(0, len(s), w)]
+        assert len(toks) <= 3
+        v = len(toks)
+        for j, t in enumerate(toks):
+            v |= t << (2 + 2 * j)
+        return v
+
+    def _result_bits(self, op: str, r: str) -> int:
+        if op == "APPEND":
+            return 0 | (self._value_bits(r) << 2)
+        if op == "GET":
+            return 2 if r == "KeyNotFound" else 1 | (self._value_bits(r) << 2)
+        return 3
+
+    def params(self):
+        kv = self.kv
+        ps = [self.servers, self.clients, kv.ncmds]
+        for c in range(2):
+            for k in range(3):
+                if c < self.clients and k < kv.ncmds:
+                    op, key, val = kv.cmds[c][k]
+                    exp = kv.expected[c][k]
+                    ps += [AmoKV.OPS[op], kv.keys.index(key), kv.syms.index(val) if val is not None else 0,
+                           self._result_bits(op, exp) if exp is not None else -1]
+                else:
+                    ps += [0, 0, 0, -1]
+        return ps
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        if name.startswith("hasViewReply:"):
+            n = int(name.split(":")[1])
+            return StatePredicate(f"ViewReply with viewNum: {n}", 500, n)
+        raise KeyError(name)
+
+    # ---- rendering in the oracle's toString form ------------------------------------------------
+    def _value_str(self, v: int) -> str:
+        return "".join(self.kv.syms[(v >> (2 + 2 * j)) & 3] for j in range(v & 3))
+
+    def _result_str(self, r: int) -> str:
+        t, v = r & 3, r >> 2
+        if t == 0:
+            return f"AppendResult({self._value_str(v)})"
+        if t == 1:
+            return f"GetResult({self._value_str(v)})"
+        return "KeyNotFound()" if t == 2 else "PutOk()"
+
+    @staticmethod
+    def _view_str(v: int) -> str:
+        p, b = (v >> 4) & 3, (v >> 6) & 3
+        return f"View({v & 15}, {p if p else -1}, {b if b else -1})"
+
+    def _app_str(self, app: int) -> str:
+        w1, w2 = app & 0xFFFFFFF, app >> 28
+        s = ""
+        for k, key in enumerate(self.kv.keys):
+            v = (w1 >> (8 * k)) & 0xFF
+            if v & 3:
+                s += f"{key}={self._value_str(v)};"
+        s += "|"
+        for c, amo in enumerate([(w1 >> 16) & 0xFFF, w2 & 0xFFF]):
+            if amo & 3:
+                s += f"{1 + self.servers + c}:{amo & 3}:{self._result_str(amo >> 2)};"
+        return s
+
+    def render_event(self, e) -> str:
+        a = self.addresses
+        if e.is_timer:
+            if e.type == 9:
+                return f"Timer(-> {a[e.to]}, PingCheckTimer())"
+            if e.type == 10:
+                return f"Timer(-> {a[e.to]}, PingTimer())"
+            return f"Timer(-> {a[e.to]}, ClientTimer({e.fields[0]}))"
+        m, t = e.fields[0], e.type
+        if t == 0:
+            body = f"Ping({m & 15})"
+        elif t == 1:
+            body = "GetView()"
+        elif t == 2:
+            body = f"ViewReply({self._view_str(m & 0xFF)})"
+        elif t == 3:
+            body = f"Request({m & 3})"
+        elif t == 4:
+            body = f"Reply({self._result_str((m >> 2) & 0x3FF)}, {m & 3})"
+        elif t == 5:
+            body = f"StateTransfer({self._view_str(m & 0xFF)}, {self._app_str((m >> 8) & ((1 << 40) - 1))})"
+        elif t == 6:
+            body = f"StateTransferAck({m & 15})"
+        else:
+            name = "Forward" if t == 7 else "ForwardAck"
+            body = f"{name}({m & 15}, {(m >> 4) & 7}, {(m >> 7) & 3})"
+        return f"Message({a[e.from_]} -> {a[e.to]}, {body})"

@@ -70,7 +70,8 @@ typedef enum {
   DSL_PROTO_SIPAXOS = 2,    /* single-instance Paxos (T/visualization/examples/paxosmadesimple) */
   DSL_PROTO_SYNTHETIC = 3,  /* table-driven synthetic protocol (BASELINE config C3) */
   DSL_PROTO_AMOKV = 4,      /* lab1 at-most-once KV client/server (BASELINE config C2) */
-  DSL_PROTO_MULTIPAXOS = 5  /* lab3 Multi-Paxos (BASELINE config C5) */
+  DSL_PROTO_MULTIPAXOS = 5, /* lab3 Multi-Paxos (BASELINE config C5) */
+  DSL_PROTO_PB = 6          /* lab2 primary-backup + ViewServer (BASELINE config C4) */
 } dsl_protocol_id;
 
 typedef struct {
@@ -93,7 +94,8 @@ typedef enum {
   DSL_PRED_SYNTH_NOT_ALL_MAX = 200, /* synthetic: not every node word at its maximum */
   DSL_PRED_SYNTH_COUNTER_LT = 201,  /* synthetic: node word arg0 < arg1 */
   DSL_PRED_APPENDS_LINEARIZABLE = 300, /* KVStoreWorkload.APPENDS_LINEARIZABLE */
-  DSL_PRED_LOGS_CONSISTENT = 400    /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS */
+  DSL_PRED_LOGS_CONSISTENT = 400,   /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS */
+  DSL_PRED_PB_HAS_VIEW_REPLY = 500  /* PrimaryBackupTest.hasViewReply(n): arg0 = n */
 } dsl_predicate_id;
 
 typedef struct {

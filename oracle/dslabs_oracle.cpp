@@ -18,6 +18,7 @@
 #include "oracle_core.hpp"
 #include "proto_amokv.hpp"
 #include "proto_multipaxos.hpp"
+#include "proto_pb.hpp"
 #include "proto_pingpong.hpp"
 #include "proto_sipaxos.hpp"
 #include "proto_synthetic.hpp"
@@ -129,6 +130,22 @@ static Scenario build(const Args& a) {
       if (n == "APPENDS_LINEARIZABLE") return amokv::appendsLinearizable(cfg, *nm);
       throw std::runtime_error("unknown predicate " + n);
     };
+  } else if (a.proto == "pb") {
+    pb::Config cfg;
+    cfg.servers = a.geti("servers", 2);
+    cfg.clients = a.geti("clients", 1);
+    cfg.kv = amokv::Config::fromArgs(cfg.clients, a.get("workload", "putget"));
+    sc.init = pb::initial(cfg, sc.names);
+    sc.pred = [common](const std::string& n) -> Predicate {
+      auto p = common(n);
+      if (p) return *p;
+      if (n.rfind("hasViewReply:", 0) == 0) {  // hasViewReply:N or hasViewReply:N:P:B
+        auto parts = split(n, ':');
+        if (parts.size() == 2) return pb::hasViewReply(std::stoi(parts[1]));
+        return pb::hasViewReplyExact(std::stoi(parts[1]), std::stoi(parts[2]), std::stoi(parts[3]));
+      }
+      throw std::runtime_error("unknown predicate " + n);
+    };
   } else if (a.proto == "synthetic") {
     synthetic::Table tab;
     tab.nodes = a.geti("nodes", 5);
@@ -161,6 +178,10 @@ static Settings settingsFrom(const Args& a, Scenario& sc) {
   for (auto& n : a.all("prune")) st.prunes.push_back(mk(n));
   st.maxDepth = a.geti("max-depth", -1);
   for (auto& n : a.all("no-timers")) st.timersActive[addrOf(sc.names, n)] = false;
+  for (auto& n : a.all("inactive")) {  // TestSettings.nodeActive(n, false)
+    st.senderActive[addrOf(sc.names, n)] = false;
+    st.receiverActive[addrOf(sc.names, n)] = false;
+  }
   if (a.has("partition")) {  // TestSettings.partition: network off, links inside each group on
     st.networkActive = false;
     for (auto& group : split(a.get("partition"), '|')) {
@@ -235,6 +256,113 @@ static int runBfs(const Args& a) {
 
 // Replays a list of event strings from the initial state (TraceReplaySearch.java:76-101 /
 // stepEvent(skipChecks=false): every event must be enabled in the state it is applied to).
+// ViewServerTest (labs/lab2-primarybackup/tst/dslabs/primarybackup/ViewServerTest.java:156-303)
+// replayed against the oracle's ViewServer: the reference's own known-answer tests for the view
+// service. Addresses: 0 = viewserver, 1..3 = server1..3, 9 = the test client.
+static int runVsTest(const Args&) {
+  using namespace pb;
+  struct Harness {
+    std::shared_ptr<ViewServer> vs = std::make_shared<ViewServer>();
+    std::vector<TimerEnv> timers;
+    bool ok = true;
+    std::string why;
+    Harness() {
+      Ctx c{0, {}, {}};
+      vs->init(c);
+      timers = c.timers;
+    }
+    void ping(int n, int from) {
+      Ctx c{0, {}, {}};
+      vs->handleMessage(Rec{"Ping", {std::to_string(n)}}, from, 0, c);
+    }
+    void timeout() {
+      if (timers.empty()) { ok = false; why = "no timer"; return; }
+      TimerEnv t = timers.front();
+      timers.erase(timers.begin());
+      Ctx c{0, {}, {}};
+      vs->onTimer(t.t, c);
+      for (auto& x : c.timers) timers.push_back(x);
+    }
+    View get() {
+      Ctx c{0, {}, {}};
+      vs->handleMessage(Rec{"GetView", {}}, 9, 0, c);
+      return View::parse(c.sent.back().m.f[0]);
+    }
+    void check(int p, int b, int n) {
+      View v = get();
+      if (v.primary != p || v.backup != b || (n >= 0 && v.num != n)) {
+        if (ok) why = "expected (" + std::to_string(n) + "," + std::to_string(p) + "," + std::to_string(b) + ") got " + v.str();
+        ok = false;
+      }
+    }
+    void setup(int p, int b, bool ack) {
+      ping(STARTUP_VIEWNUM, p);
+      check(p, -1, INITIAL_VIEWNUM);
+      if (b >= 0) {
+        ping(INITIAL_VIEWNUM, p);
+        ping(STARTUP_VIEWNUM, b);
+        check(p, b, INITIAL_VIEWNUM + 1);
+      }
+      if (ack) ping(b < 0 ? INITIAL_VIEWNUM : INITIAL_VIEWNUM + 1, p);
+    }
+    void timeoutFully(std::vector<int> pingers) {
+      View cur = get();
+      for (int i = 0; i < 2; i++) {
+        for (int x : pingers) ping(cur.num, x);
+        timeout();
+      }
+    }
+  };
+  std::vector<std::pair<std::string, std::function<void(Harness&)>>> tests = {
+      {"test01StartupViewCorrect", [](Harness& h) { h.check(-1, -1, STARTUP_VIEWNUM); }},
+      {"test02firstPrimary", [](Harness& h) { h.setup(1, -1, false); }},
+      {"test03FirstBackup", [](Harness& h) { h.setup(1, 2, false); }},
+      {"test04BackupPingsFirst", [](Harness& h) {
+         h.setup(1, -1, false); h.ping(STARTUP_VIEWNUM, 2); h.ping(INITIAL_VIEWNUM, 1);
+         h.check(1, 2, INITIAL_VIEWNUM + 1); }},
+      {"test05BackupTakesOver", [](Harness& h) {
+         h.setup(1, 2, true);
+         h.ping(INITIAL_VIEWNUM + 1, 2); h.check(1, 2, INITIAL_VIEWNUM + 1); h.timeout();
+         h.ping(INITIAL_VIEWNUM + 1, 2); h.check(1, 2, INITIAL_VIEWNUM + 1); h.timeout();
+         h.check(2, -1, INITIAL_VIEWNUM + 2); }},
+      {"test06OldServerBecomesBackup", [](Harness& h) {
+         h.setup(1, 2, true); h.timeoutFully({2}); h.check(2, -1, INITIAL_VIEWNUM + 2);
+         h.ping(INITIAL_VIEWNUM + 2, 2); h.ping(INITIAL_VIEWNUM + 1, 1); h.check(2, 1, INITIAL_VIEWNUM + 3); }},
+      {"test07IdleThirdServerBecomesBackup", [](Harness& h) {
+         h.setup(1, 2, true); h.timeoutFully({2, 3}); h.check(2, 3, INITIAL_VIEWNUM + 2); }},
+      {"test08WaitForPrimaryAck", [](Harness& h) {
+         h.ping(STARTUP_VIEWNUM, 1); h.ping(STARTUP_VIEWNUM, 2); h.check(1, -1, INITIAL_VIEWNUM);
+         h.ping(INITIAL_VIEWNUM, 1); h.check(1, 2, INITIAL_VIEWNUM + 1); h.ping(INITIAL_VIEWNUM, 2);
+         h.timeoutFully({2}); h.check(1, 2, INITIAL_VIEWNUM + 1); }},
+      {"test09DeadBackupRemoved", [](Harness& h) {
+         h.setup(1, 2, true); h.timeoutFully({1}); h.check(1, -1, INITIAL_VIEWNUM + 2); }},
+      {"test10UninitializedNotPromoted", [](Harness& h) {
+         h.setup(1, 2, true); h.timeoutFully({2, 3}); h.check(2, 3, INITIAL_VIEWNUM + 2);
+         h.timeoutFully({3}); h.check(2, 3, INITIAL_VIEWNUM + 2); }},
+      {"test11DeadServerNotMadeBackup", [](Harness& h) {
+         h.setup(1, -1, false); h.ping(STARTUP_VIEWNUM, 2); h.timeoutFully({}); h.ping(INITIAL_VIEWNUM, 1);
+         h.check(1, -1, INITIAL_VIEWNUM); }},
+      {"test12NewViewNotStarted", [](Harness& h) {
+         h.setup(1, -1, false); h.timeoutFully({1}); h.check(1, -1, INITIAL_VIEWNUM);
+         h.timeoutFully({}); h.check(1, -1, INITIAL_VIEWNUM); h.ping(INITIAL_VIEWNUM, 1);
+         h.timeoutFully({1}); h.check(1, -1, INITIAL_VIEWNUM); h.timeoutFully({}); h.check(1, -1, INITIAL_VIEWNUM);
+         h.ping(STARTUP_VIEWNUM, 2); h.check(1, 2, INITIAL_VIEWNUM + 1); h.ping(INITIAL_VIEWNUM + 1, 1);
+         h.check(1, 2, INITIAL_VIEWNUM + 1); h.timeoutFully({1, 2}); h.check(1, 2, INITIAL_VIEWNUM + 1);
+         h.timeoutFully({});
+         View v = h.get();
+         if (v.primary == 1 && v.backup == 2 && v.num != INITIAL_VIEWNUM + 1) h.ok = false; }},
+  };
+  std::cout << "{\"results\":[";
+  for (size_t i = 0; i < tests.size(); i++) {
+    Harness h;
+    tests[i].second(h);
+    std::cout << (i ? "," : "") << "{\"name\":\"" << tests[i].first << "\",\"ok\":" << (h.ok ? "true" : "false")
+              << ",\"why\":\"" << jsonEsc(h.why) << "\"}";
+  }
+  std::cout << "]}" << std::endl;
+  return 0;
+}
+
 static int runReplay(const Args& a) {
   Scenario sc = build(a);
   Settings st = settingsFrom(a, sc);
@@ -329,6 +457,7 @@ int main(int argc, char** argv) {
   try {
     if (a.mode == "bfs") return runBfs(a);
     if (a.mode == "replay") return runReplay(a);
+    if (a.mode == "vstest") return runVsTest(a);
     if (a.mode == "timerqueue") return runTimerQueue();
   } catch (const std::exception& e) {
     std::cout << "{\"error\":\"" << jsonEsc(e.what()) << "\"}" << std::endl;

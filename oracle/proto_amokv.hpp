@@ -47,6 +47,9 @@ struct Config {
     } else if (workload == "putappendget") {  // KVStoreWorkload.putAppendGetWorkload
       c.cmds = {"PUT:foo:bar", "APPEND:foo:baz", "GET:foo"};
       c.results = {"Ok", "barbaz", "barbaz"};
+    } else if (workload == "putget") {  // KVStoreWorkload.putGetWorkload (PrimaryBackupTest test17)
+      c.cmds = {"PUT:foo:bar", "GET:foo"};
+      c.results = {"Ok", "bar"};
     } else if (workload == "getput") {  // a GET before any PUT: KeyNotFound
       c.cmds = {"GET:foo", "PUT:foo:bar", "GET:foo"};
       c.results = {"KeyNotFound", "Ok", "bar"};

@@ -1,0 +1,367 @@
+// oracle/proto_pb.hpp -- TEST INFRASTRUCTURE ONLY (see oracle_core.hpp).
+//
+// lab2 primary-backup with a ViewServer (BASELINE config C4). The reference ships stubs
+// (labs/lab2-primarybackup/src/dslabs/primarybackup/ViewServer.java, PBServer.java, PBClient.java,
+// Messages.java: Ping(viewNum), GetView, ViewReply(view); Timers.java: PingCheckTimer 100 ms,
+// PingTimer 25 ms, ClientTimer 100 ms; View.java: (viewNum, primary, backup)). This is the
+// builder-authored solution specified in DESIGN.md §12, following labs/lab2-primarybackup/README.md
+// :154-330. The ViewServer restatement is pinned by the reference's own unit tests
+// (tst/dslabs/primarybackup/ViewServerTest.java test01-test12), replayed by `dslabs_oracle vstest`.
+#pragma once
+#include "oracle_core.hpp"
+#include "proto_amokv.hpp"
+
+namespace oracle {
+namespace pb {
+
+constexpr int STARTUP_VIEWNUM = 0, INITIAL_VIEWNUM = 1;
+constexpr int PING_CHECK_MILLIS = 100, PING_MILLIS = 25, CLIENT_RETRY_MILLIS = 100;
+
+struct View {
+  int num = STARTUP_VIEWNUM, primary = -1, backup = -1;  // -1 = null
+  bool operator==(const View& o) const { return num == o.num && primary == o.primary && backup == o.backup; }
+  std::string str() const {
+    return "View(" + std::to_string(num) + ", " + std::to_string(primary) + ", " + std::to_string(backup) + ")";
+  }
+  static View parse(const std::string& s) {
+    View v;
+    sscanf(s.c_str(), "View(%d, %d, %d)", &v.num, &v.primary, &v.backup);
+    return v;
+  }
+};
+
+// ---- ViewServer (README.md:161-216) --------------------------------------------------------------
+struct ViewServer : Node {
+  int nservers = 3;  // server addresses are 1..nservers
+  View view;
+  bool acked = false;
+  std::set<int> recent;     // servers that pinged since the last PingCheckTimer
+  std::set<int> aliveLast;  // servers that pinged in the interval ending at the last PingCheckTimer
+
+  std::shared_ptr<Node> clone() const override { return std::make_shared<ViewServer>(*this); }
+  void key(std::string& out) const override {
+    out += "VS{" + view.str() + (acked ? "A" : "") + "|";
+    for (int s : recent) out += std::to_string(s);
+    out += "|";
+    for (int s : aliveLast) out += std::to_string(s);
+    out += "}";
+  }
+  std::string str() const override { return "ViewServer(" + view.str() + ")"; }
+  void init(Ctx& ctx) override { ctx.set(Rec{"PingCheckTimer", {}}, PING_CHECK_MILLIS); }
+  bool live(int s) const { return recent.count(s) || aliveLast.count(s); }
+  int idle(const std::set<int>& alive) const {  // lowest-numbered live server that is neither P nor B
+    for (int s : alive)
+      if (s != view.primary && s != view.backup) return s;
+    return -1;
+  }
+  std::set<int> liveSet() const {
+    std::set<int> a = recent;
+    a.insert(aliveLast.begin(), aliveLast.end());
+    return a;
+  }
+  void newView(int primary, int backup) {
+    view = View{view.num + 1, primary, backup};
+    acked = false;
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    if (m.type == "GetView") {
+      ctx.send(Rec{"ViewReply", {view.str()}}, from);
+      return;
+    }
+    if (m.type != "Ping") throw HandlerException("no handler");
+    const int n = std::stoi(m.f[0]);
+    recent.insert(from);
+    if (view.num == STARTUP_VIEWNUM) {
+      view = View{INITIAL_VIEWNUM, from, -1};  // any server may be the first primary
+      acked = false;
+    }
+    if (from == view.primary && n == view.num) acked = true;
+    if (acked && view.backup < 0) {  // no backup and an idle live server: it becomes the backup
+      const int s = idle(liveSet());
+      if (s >= 0) newView(view.primary, s);
+    }
+    ctx.send(Rec{"ViewReply", {view.str()}}, from);
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    if (t.type != "PingCheckTimer") throw HandlerException("no timer handler");
+    aliveLast = recent;  // dead = no ping between the last two PingCheckTimers
+    recent.clear();
+    if (acked && view.num != STARTUP_VIEWNUM) {
+      const bool pAlive = aliveLast.count(view.primary) > 0;
+      const bool bAlive = view.backup >= 0 && aliveLast.count(view.backup) > 0;
+      if (!pAlive) {
+        if (bAlive) {  // the backup of view i becomes the primary of view i+1
+          const int b = view.backup;
+          view.backup = -1;  // idle() excludes the new primary; the dead old primary is not alive
+          view.primary = b;
+          newView(b, idle(aliveLast));
+        }
+      } else if (view.backup >= 0 && !bAlive) {
+        view.backup = -1;
+        newView(view.primary, idle(aliveLast));
+      } else if (view.backup < 0) {
+        const int s = idle(aliveLast);
+        if (s >= 0) newView(view.primary, s);
+      }
+    }
+    ctx.set(t, PING_CHECK_MILLIS);
+  }
+};
+
+// ---- KV application with at-most-once semantics (lab1's, reused) -------------------------------------
+struct App {
+  std::map<std::string, std::string> kv;
+  std::map<int, std::pair<int, std::string>> amo;  // client -> (last seq, result)
+  std::string str() const {
+    std::string s;
+    for (auto& e : kv) s += e.first + "=" + e.second + ";";
+    s += "|";
+    for (auto& e : amo) s += std::to_string(e.first) + ":" + std::to_string(e.second.first) + ":" + e.second.second + ";";
+    return s;
+  }
+  // executes (client, seq, cmd); returns the result, or "" for a superseded command
+  std::string execute(int client, int seq, const Rec& c) {
+    auto it = amo.find(client);
+    const int last = it == amo.end() ? 0 : it->second.first;
+    if (seq < last) return "";
+    if (seq == last) return it->second.second;
+    amokv::SimpleServer tmp;
+    tmp.kv = kv;
+    const std::string r = tmp.executeKV(c).str();
+    kv = tmp.kv;
+    amo[client] = {seq, r};
+    return r;
+  }
+};
+
+struct Commands {  // the workload's command of (client, seq), shared by servers (requests carry seq only)
+  std::map<std::pair<int, int>, Rec> cmd;
+};
+
+// ---- PBServer ------------------------------------------------------------------------------------
+struct PBServer : Node {
+  int me = 1, vs = 0;
+  std::shared_ptr<const Commands> cmds;
+  View view;
+  bool started = false;  // primary: the backup holds the state of this view (or there is none)
+  int lastStarted = STARTUP_VIEWNUM;
+  App app;
+
+  std::shared_ptr<Node> clone() const override { return std::make_shared<PBServer>(*this); }
+  void key(std::string& out) const override {
+    out += "PB{" + view.str() + (started ? "S" : "") + std::to_string(lastStarted) + "|" + app.str() + "}";
+  }
+  std::string str() const override { return "PBServer(" + view.str() + ")"; }
+  void init(Ctx& ctx) override {
+    ctx.send(Rec{"Ping", {std::to_string(STARTUP_VIEWNUM)}}, vs);
+    ctx.set(Rec{"PingTimer", {}}, PING_MILLIS);
+  }
+  bool primary() const { return view.primary == me; }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    if (t.type != "PingTimer") throw HandlerException("no timer handler");
+    // ping with the latest view, unless primary of a view that has not started
+    const int n = primary() && !started ? lastStarted : view.num;
+    ctx.send(Rec{"Ping", {std::to_string(n)}}, vs);
+    ctx.set(t, PING_MILLIS);
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    if (m.type == "ViewReply") {
+      const View v = View::parse(m.f[0]);
+      if (v.num <= view.num) return;
+      view = v;
+      started = false;
+      if (primary()) {
+        if (view.backup < 0) {
+          started = true;
+          lastStarted = view.num;
+        } else {
+          ctx.send(Rec{"StateTransfer", {view.str(), app.str()}}, view.backup);
+        }
+      }
+      return;
+    }
+    if (m.type == "StateTransfer") {
+      const View v = View::parse(m.f[0]);
+      if (v.num < view.num || v.backup != me || v.primary != from) return;
+      view = v;
+      started = false;
+      app = parseApp(m.f[1]);
+      ctx.send(Rec{"StateTransferAck", {std::to_string(v.num)}}, from);
+      return;
+    }
+    if (m.type == "StateTransferAck") {
+      if (primary() && !started && std::stoi(m.f[0]) == view.num) {
+        started = true;
+        lastStarted = view.num;
+      }
+      return;
+    }
+    if (m.type == "Request") {  // client -> primary
+      const int seq = std::stoi(m.f[0]);
+      if (!primary() || !started) return;
+      if (view.backup < 0) {
+        const std::string r = app.execute(from, seq, cmds->cmd.at({from, seq}));
+        if (!r.empty()) ctx.send(Rec{"Reply", {r, std::to_string(seq)}}, from);
+      } else {
+        ctx.send(Rec{"Forward", {std::to_string(view.num), std::to_string(from), std::to_string(seq)}}, view.backup);
+      }
+      return;
+    }
+    if (m.type == "Forward") {  // primary -> backup
+      const int n = std::stoi(m.f[0]), c = std::stoi(m.f[1]), seq = std::stoi(m.f[2]);
+      if (view.num != n || view.backup != me || view.primary != from) return;
+      app.execute(c, seq, cmds->cmd.at({c, seq}));
+      ctx.send(Rec{"ForwardAck", {m.f[0], m.f[1], m.f[2]}}, from);
+      return;
+    }
+    if (m.type == "ForwardAck") {  // backup -> primary: the backup executed it; execute and reply
+      const int n = std::stoi(m.f[0]), c = std::stoi(m.f[1]), seq = std::stoi(m.f[2]);
+      if (!primary() || !started || view.num != n) return;
+      const std::string r = app.execute(c, seq, cmds->cmd.at({c, seq}));
+      if (!r.empty()) ctx.send(Rec{"Reply", {r, std::to_string(seq)}}, c);
+      return;
+    }
+    throw HandlerException("no handler");
+  }
+  static App parseApp(const std::string& s) {
+    App a;
+    const size_t bar = s.find('|');
+    std::string kvs = s.substr(0, bar), amos = s.substr(bar + 1);
+    size_t p = 0;
+    while (p < kvs.size()) {
+      const size_t q = kvs.find(';', p), e = kvs.find('=', p);
+      a.kv[kvs.substr(p, e - p)] = kvs.substr(e + 1, q - e - 1);
+      p = q + 1;
+    }
+    p = 0;
+    while (p < amos.size()) {
+      const size_t q = amos.find(';', p), c1 = amos.find(':', p), c2 = amos.find(':', c1 + 1);
+      a.amo[std::stoi(amos.substr(p, c1 - p))] = {std::stoi(amos.substr(c1 + 1, c2 - c1 - 1)),
+                                                  amos.substr(c2 + 1, q - c2 - 1)};
+      p = q + 1;
+    }
+    return a;
+  }
+};
+
+// ---- PBClient (lab1's SimpleClient plus a cached view) ---------------------------------------------
+struct PBClient : Client {
+  int vs = 0;
+  View view;
+  int seq = 0;
+  std::optional<Rec> pending, result;
+
+  std::shared_ptr<Node> clone() const override { return std::make_shared<PBClient>(*this); }
+  void key(std::string& out) const override {
+    out += "PBC{" + std::to_string(view.num) + "," + std::to_string(view.primary) + "," + std::to_string(seq) + "," +
+           (result ? result->str() : "null") + "}";
+  }
+  std::string str() const override { return "PBClient(seq=" + std::to_string(seq) + ")"; }
+  void sendRequest(Ctx& ctx) {
+    if (view.primary >= 0) ctx.send(Rec{"Request", {std::to_string(seq)}}, view.primary);
+    else ctx.send(Rec{"GetView", {}}, vs);
+  }
+  void sendCommand(const Rec& cmd, Ctx& ctx) override {
+    seq++;
+    pending = cmd;
+    result.reset();
+    sendRequest(ctx);
+    ctx.set(Rec{"ClientTimer", {std::to_string(seq)}}, CLIENT_RETRY_MILLIS);
+  }
+  bool hasResult() const override { return result.has_value(); }
+  Rec getResult() const override { return *result; }
+  void handleMessage(const Rec& m, int, int, Ctx& ctx) override {
+    if (m.type == "ViewReply") {
+      const View v = View::parse(m.f[0]);
+      if (v.num > view.num) {
+        view = v;
+        if (pending && !result) sendRequest(ctx);
+      }
+      return;
+    }
+    if (m.type != "Reply") throw HandlerException("no handler");
+    if (pending && !result && std::stoi(m.f[1]) == seq) result = amokv::parseRec(m.f[0]);
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    if (t.type != "ClientTimer") throw HandlerException("no timer handler");
+    if (pending && !result && std::stoi(t.f[0]) == seq) {
+      ctx.send(Rec{"GetView", {}}, vs);  // the primary may be dead: ask for the current view
+      if (view.primary >= 0) ctx.send(Rec{"Request", {std::to_string(seq)}}, view.primary);
+      ctx.set(t, CLIENT_RETRY_MILLIS);
+    }
+  }
+};
+
+struct Config {
+  int servers = 2, clients = 1;
+  amokv::Config kv;
+};
+
+// Address 0 = "viewserver", 1..S = "server1..", S+1.. = "client1..".
+inline std::shared_ptr<State> initial(const Config& cfg, Names& names) {
+  std::vector<std::shared_ptr<Node>> nodes;
+  std::vector<Kind> kinds;
+  names.addr = {"viewserver"};
+  auto vs = std::make_shared<ViewServer>();
+  vs->nservers = cfg.servers;
+  nodes.push_back(vs);
+  kinds.push_back(Kind::Server);
+  auto cmds = std::make_shared<Commands>();
+  for (int c = 1; c <= cfg.clients; c++) {
+    Workload w;
+    w.cmds = cfg.kv.cmds;
+    w.results = cfg.kv.results;
+    w.numTimes = cfg.kv.numTimes;
+    w.parser = amokv::parse;
+    const int addr = cfg.servers + c;
+    for (int k = 1; w.hasNext(); k++) cmds->cmd[{addr, k}] = w.next("client" + std::to_string(c)).first;
+  }
+  for (int s = 1; s <= cfg.servers; s++) {
+    names.addr.push_back("server" + std::to_string(s));
+    auto n = std::make_shared<PBServer>();
+    n->me = s;
+    n->cmds = cmds;
+    nodes.push_back(n);
+    kinds.push_back(Kind::Server);
+  }
+  for (int c = 1; c <= cfg.clients; c++) {
+    names.addr.push_back("client" + std::to_string(c));
+    auto cw = std::make_shared<ClientWorker>();
+    cw->client = std::make_shared<PBClient>();
+    cw->addrName = names.addr.back();
+    cw->workload.cmds = cfg.kv.cmds;
+    cw->workload.results = cfg.kv.results;
+    cw->workload.numTimes = cfg.kv.numTimes;
+    cw->workload.parser = amokv::parse;
+    nodes.push_back(cw);
+    kinds.push_back(Kind::ClientWorker);
+  }
+  return makeInitial(nodes, kinds);
+}
+
+// PrimaryBackupTest.hasViewReply (PrimaryBackupTest.java:104-117): the network holds a ViewReply
+// with view number >= n (or exactly the view (n, p, b)).
+inline Predicate hasViewReply(int n) {
+  return {"ViewReply with viewNum: " + std::to_string(n), [n](const State& s) {
+            PredResult r;
+            r.value = false;
+            for (const auto* net : {&s.network, &s.dropped})
+              for (auto& e : *net)
+                if (e.m.type == "ViewReply" && View::parse(e.m.f[0]).num >= n) r.value = true;
+            return r;
+          }};
+}
+inline Predicate hasViewReplyExact(int n, int p, int b) {
+  const View v{n, p, b};
+  return {"ViewReply with " + v.str(), [v](const State& s) {
+            PredResult r;
+            r.value = false;
+            for (const auto* net : {&s.network, &s.dropped})
+              for (auto& e : *net)
+                if (e.m.type == "ViewReply" && View::parse(e.m.f[0]) == v) r.value = true;
+            return r;
+          }};
+}
+
+}  // namespace pb
+}  // namespace oracle

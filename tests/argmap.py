@@ -1,7 +1,7 @@
 """Maps oracle CLI arguments (tests/golden/*.json "args") onto the engine's Python API, so each
 committed oracle fixture is replayed on the GPU with the same meaning."""
 from dslabs_amd import CLIENTS_DONE, NONE_DECIDED, RESULTS_OK, SearchSettings, clientDone
-from dslabs_amd.protocols import AmoKV, MultiPaxos, PingPong, SIPaxos, Synthetic
+from dslabs_amd.protocols import PB, AmoKV, MultiPaxos, PingPong, SIPaxos, Synthetic
 
 
 def _opt(args, name, default=None):
@@ -20,6 +20,8 @@ def protocol(args):
     if p == "multipaxos":
         return MultiPaxos(int(_opt(args, "--servers", 3)), int(_opt(args, "--clients", 2)),
                           _opt(args, "--workload", "append-xy"))
+    if p == "pb":
+        return PB(int(_opt(args, "--servers", 2)), int(_opt(args, "--clients", 1)), _opt(args, "--workload", "putget"))
     if p == "amokv":
         return AmoKV(int(_opt(args, "--clients", 2)), _opt(args, "--workload", "diffkey3"))
     if p == "synthetic":
@@ -58,6 +60,8 @@ def settings(args, proto, table_log2=24):
             s.maxDepth(int(v))
         elif a == "--no-timers":
             s.deliverTimers(v, False)
+        elif a == "--inactive":
+            s.nodeActive(v, False)
         elif a == "--partition":
             s.partition(*[g.split(",") for g in v.split("|")])
         i += 1

@@ -196,8 +196,32 @@ AMOKV = {
                                            "server,client1|client2"], pinned={}),
 }
 
+PBA = ["--proto", "pb"]
+PBQ = ["--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE", "--prune", "hasViewReply:4"]
+PBF = {
+    # BASELINE C4 (PrimaryBackupTest.test17-style, :680-711): 2 servers + ViewServer, 1 client
+    # putGetWorkload, prunes CLIENTS_DONE and hasViewReply(INITIAL_VIEWNUM + 3), from the start state
+    "pb_2s1c_d15": dict(args=PBA + ["--servers", "2", "--clients", "1", "--workload", "putget"] + PBQ +
+                        ["--max-depth", "15"], pinned={}),
+    "pb_2s1c_goal": dict(args=PBA + ["--servers", "2", "--clients", "1", "--workload", "putget", "--inv",
+                                     "RESULTS_OK", "--goal", "CLIENTS_DONE", "--prune", "hasViewReply:4",
+                                     "--finish-level"], pinned={}),
+    # test17's third server, inactive (nodeActive(server(3), false))
+    "pb_3s1c_inactive_d12": dict(args=PBA + ["--servers", "3", "--clients", "1", "--workload", "putget"] + PBQ +
+                                 ["--inactive", "server3", "--max-depth", "12"], pinned={}),
+    "pb_2s2c_d11": dict(args=PBA + ["--servers", "2", "--clients", "2", "--workload", "putget"] + PBQ +
+                        ["--max-depth", "11"], pinned={}),
+    # a view change is reachable: ViewReply for view 3
+    "pb_view3_goal": dict(args=PBA + ["--servers", "2", "--clients", "1", "--workload", "putget", "--goal",
+                                      "hasViewReply:3", "--finish-level"], pinned={}),
+    # two clients appending to one key with expected results: RESULTS_OK is violated
+    "pb_2c_results_violation": dict(args=PBA + ["--servers", "2", "--clients", "2", "--workload",
+                                                "appendappendget", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE",
+                                                "--prune", "hasViewReply:3", "--finish-level"], pinned={}),
+}
+
 if __name__ == "__main__":
-    which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic", "amokv"}
+    which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic", "amokv", "pb"}
     if "lab0" in which or "sipaxos" in which:
         gen_lab0_sip()
     if "multipaxos" in which:
@@ -206,3 +230,9 @@ if __name__ == "__main__":
         gen(SYNTHETIC, "synthetic.json")
     if "amokv" in which:
         gen(AMOKV, "amokv.json")
+    if "pb" in which:
+        gen(PBF, "pb.json")
+        vs = oracle_util.run("vstest", [])
+        with open(os.path.join(HERE, "viewserver.json"), "w") as f:
+            json.dump({"source": "labs/lab2-primarybackup/tst/dslabs/primarybackup/ViewServerTest.java:156-303",
+                       "results": vs["results"]}, f, indent=1)

@@ -149,7 +149,87 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   return 0;
 }
 
+// ViewServerTest (labs/lab2-primarybackup/tst/dslabs/primarybackup/ViewServerTest.java:156-303)
+// against the DEVICE ViewServer handler (PB node 0), the same scenarios the oracle replays.
+static int vstest() {
+  struct H {
+    PB::Params p{};
+    uint32_t w[PB::kNodeWords] = {0, 0, 0};
+    bool ok = true;
+    H() { p.servers = 3; p.clients = 1; p.ncmds = 1; }
+    void ping(int n, int from) {
+      Sender<PB> out;
+      PB::on_message(0, w, PB::msg(PB::M_PING, from, 0, (uint64_t)n), out, p);
+    }
+    void timeout() {
+      Sender<PB> out;
+      PB::on_timer(0, w, 0, out, p);
+    }
+    int get() {  // GetView: the ViewReply's view (num | p << 4 | b << 6)
+      Sender<PB> out;
+      PB::on_message(0, w, PB::msg(PB::M_GETVIEW, 4, 0, 0), out, p);
+      return (int)(out.r[0] & 0xff);
+    }
+    void check(int pr, int b, int n) {
+      const int v = get();
+      if (PB::v_p(v) != pr || PB::v_b(v) != b || (n >= 0 && PB::v_num(v) != n)) ok = false;
+    }
+    void setup(int pr, int b, bool ack) {
+      ping(0, pr);
+      check(pr, 0, 1);
+      if (b) {
+        ping(1, pr);
+        ping(0, b);
+        check(pr, b, 2);
+      }
+      if (ack) ping(b ? 2 : 1, pr);
+    }
+    void full(std::vector<int> ps) {
+      const int n = PB::v_num(get());
+      for (int i = 0; i < 2; i++) {
+        for (int x : ps) ping(n, x);
+        timeout();
+      }
+    }
+  };
+  std::vector<std::pair<const char*, void (*)(H&)>> t = {
+      {"test01StartupViewCorrect", [](H& h) { h.check(0, 0, 0); }},
+      {"test02firstPrimary", [](H& h) { h.setup(1, 0, false); }},
+      {"test03FirstBackup", [](H& h) { h.setup(1, 2, false); }},
+      {"test04BackupPingsFirst", [](H& h) { h.setup(1, 0, false); h.ping(0, 2); h.ping(1, 1); h.check(1, 2, 2); }},
+      {"test05BackupTakesOver", [](H& h) {
+         h.setup(1, 2, true); h.ping(2, 2); h.check(1, 2, 2); h.timeout(); h.ping(2, 2); h.check(1, 2, 2);
+         h.timeout(); h.check(2, 0, 3); }},
+      {"test06OldServerBecomesBackup", [](H& h) {
+         h.setup(1, 2, true); h.full({2}); h.check(2, 0, 3); h.ping(3, 2); h.ping(2, 1); h.check(2, 1, 4); }},
+      {"test07IdleThirdServerBecomesBackup", [](H& h) { h.setup(1, 2, true); h.full({2, 3}); h.check(2, 3, 3); }},
+      {"test08WaitForPrimaryAck", [](H& h) {
+         h.ping(0, 1); h.ping(0, 2); h.check(1, 0, 1); h.ping(1, 1); h.check(1, 2, 2); h.ping(1, 2); h.full({2});
+         h.check(1, 2, 2); }},
+      {"test09DeadBackupRemoved", [](H& h) { h.setup(1, 2, true); h.full({1}); h.check(1, 0, 3); }},
+      {"test10UninitializedNotPromoted", [](H& h) {
+         h.setup(1, 2, true); h.full({2, 3}); h.check(2, 3, 3); h.full({3}); h.check(2, 3, 3); }},
+      {"test11DeadServerNotMadeBackup", [](H& h) {
+         h.setup(1, 0, false); h.ping(0, 2); h.full({}); h.ping(1, 1); h.check(1, 0, 1); }},
+      {"test12NewViewNotStarted", [](H& h) {
+         h.setup(1, 0, false); h.full({1}); h.check(1, 0, 1); h.full({}); h.check(1, 0, 1); h.ping(1, 1);
+         h.full({1}); h.check(1, 0, 1); h.full({}); h.check(1, 0, 1); h.ping(0, 2); h.check(1, 2, 2); h.ping(2, 1);
+         h.check(1, 2, 2); h.full({1, 2}); h.check(1, 2, 2); h.full({});
+         const int v = h.get();
+         if (PB::v_p(v) == 1 && PB::v_b(v) == 2 && PB::v_num(v) != 2) h.ok = false; }},
+  };
+  printf("{\"results\":[");
+  for (size_t i = 0; i < t.size(); i++) {
+    H h;
+    t[i].second(h);
+    printf("%s{\"name\":\"%s\",\"ok\":%s}", i ? "," : "", t[i].first, h.ok ? "true" : "false");
+  }
+  printf("]}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && strcmp(argv[1], "vstest") == 0) return vstest();
   dsl_protocol_desc d{};
   int i = 1;
   d.protocol = atoi(argv[i++]);
@@ -167,10 +247,15 @@ int main(int argc, char** argv) {
       which++;
       continue;
     }
-    int id = atoi(argv[i]);
+    // predicate token: [-]id[:arg0[:arg1]] (leading '-' = negated)
+    int id = 0;
+    long long a0 = 0, a1 = 0;
+    sscanf(argv[i], "%d:%lld:%lld", &id, &a0, &a1);
     DevPred p{};
     p.negate = id < 0;
     p.id = id < 0 ? -id : id;
+    p.arg0 = a0;
+    p.arg1 = a1;
     lists[which][(*counts[which])++] = p;
   }
   set.max_depth = atoi(argv[argc - 1]);
@@ -180,6 +265,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, set);
     case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
     case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
+    case DSL_PROTO_PB: return run<PB>(d, set);
   }
   return 2;
 }

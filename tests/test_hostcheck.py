@@ -82,6 +82,13 @@ CASES = {
     "kv_putappendget": ([4, 1, 3, 1, 0, 0, 3, 2, 0, 1, 264, 0, 0, 0, 265, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, -1],
                         ["--proto", "amokv", "--clients", "1", "--workload", "putappendget", "--inv", "RESULTS_OK",
                          "--prune", "CLIENTS_DONE"]),
+    # lab2 PB + ViewServer (C4): params from dslabs_amd.protocols.PB(servers, clients, workload)
+    "pb_2s1c_d14": ([6, 2, 1, 2, 1, 0, 0, 3, 0, 0, 0, 5, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, "500:4", 14],
+                    ["--proto", "pb", "--servers", "2", "--clients", "1", "--workload", "putget", "--inv", "RESULTS_OK",
+                     "--prune", "CLIENTS_DONE", "--prune", "hasViewReply:4", "--max-depth", "14"]),
+    "pb_3s1c_d10": ([6, 3, 1, 2, 1, 0, 0, 3, 0, 0, 0, 5, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, "500:3", 10],
+                    ["--proto", "pb", "--servers", "3", "--clients", "1", "--workload", "putget", "--inv", "RESULTS_OK",
+                     "--prune", "CLIENTS_DONE", "--prune", "hasViewReply:3", "--max-depth", "10"]),
 }
 
 
@@ -93,3 +100,10 @@ def test_encoding_matches_oracle(protocheck, name):
     assert got["end"] == want["end"]
     assert got["per_depth"] == want["per_depth"]
     assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
+
+
+def test_device_viewserver_passes_reference_unit_tests(protocheck):
+    """The packed ViewServer handler (PB node 0) against ViewServerTest test01-test12."""
+    out = subprocess.run([protocheck, "vstest"], check=True, capture_output=True, text=True, timeout=60)
+    res = json.loads(out.stdout)["results"]
+    assert len(res) == 12 and all(r["ok"] for r in res), res

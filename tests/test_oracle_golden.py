@@ -88,3 +88,22 @@ def test_amokv_oracle_matches_fixture(name):
     r = oracle_util.run("bfs", case["args"], timeout=300)
     assert r["end"] == case["end"]
     assert r["per_depth"] == case["per_depth"]
+
+
+PBG = _load("pb.json")
+
+
+@pytest.mark.parametrize("name", sorted(PBG))
+def test_pb_oracle_matches_fixture(name):
+    case = PBG[name]
+    r = oracle_util.run("bfs", case["args"], timeout=300)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
+
+
+def test_viewserver_passes_reference_unit_tests():
+    """The oracle's ViewServer against the reference's own ViewServerTest scenarios (test01-12)."""
+    r = oracle_util.run("vstest", [])
+    names = [x["name"] for x in r["results"]]
+    assert len(names) == 12 and names[0] == "test01StartupViewCorrect"
+    assert all(x["ok"] for x in r["results"]), [x for x in r["results"] if not x["ok"]]
