@@ -69,7 +69,9 @@ def build_search(name: str, depth: int):
         s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
         s.addInvariant(proto.predicate("APPENDS_LINEARIZABLE"))
         s.maxDepth(depth)
-        s.table_log2_slots = 28
+        # visited table sized for a load factor <= ~1/8 (1.11M states at d12, x2.8 per level):
+        # clearing an oversized table is part of every timed search
+        s.table_log2_slots = max(20, min(32, 23 + (3 * (depth - 12) + 1) // 2))
         return proto, s, ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
                           "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
     if name == "pb":

@@ -106,7 +106,13 @@ struct BfsEngine : EngineBase {
     uint64_t F = 0;
     uint64_t work = 0;        // enabled events of the current frontier (exact)
     std::vector<uint64_t> seg_base, seg_cnt;  // row ranges of the current frontier
-    unsigned long long* seg_ctr = nullptr;    // kSegs reservation counters
+    unsigned long long* seg_ctr = nullptr;    // kSegs reservation counters (inside the current set)
+    // Two counter sets (LevelCounters + segment counters, kCtrSet bytes each): a level uses set
+    // cset, and its k_level zeroes the other set for the next level, so no per-level memset;
+    // the host reads the whole set with ONE copy into pinned memory.
+    unsigned char* ctrbuf = nullptr;
+    unsigned char* hctr = nullptr;
+    int cset = 0;
     uint64_t segcap = 0;
     int nseg = 1;
     std::vector<uint64_t> level_base, level_size;
@@ -153,14 +159,16 @@ struct BfsEngine : EngineBase {
   ~BfsEngine() override {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,    s.cur,   s.next,   s.cur_fp,    s.next_fp, s.hist_parent,
-                      s.hist_event, s.ctr, s.terms,  s.rc,        s.seed,    s.out_fp,
-                      s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.seg_ctr};
+                      s.hist_event, s.terms,  s.rc,        s.seed,    s.out_fp,
+                      s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.ctrbuf};
       for (void* q : ptrs) (void)hipFree(q);
+      if (s.hctr) (void)hipHostFree(s.hctr);
     }
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     comm.reset();
     if (stream) (void)hipStreamDestroy(stream);
+    (void)hipGetLastError();
   }
 
   int state_bytes() const override { return (int)sizeof(typename P::State); }
@@ -291,6 +299,7 @@ struct BfsEngine : EngineBase {
 
   int run(dsl_result** out) override {
     auto t_start = std::chrono::steady_clock::now();
+    (void)hipGetLastError();  // the per-thread sticky error must not blame this search for an older call
     if (!stream) {
       if (cfg.device >= 0) DSL_HIP(hipSetDevice(cfg.device));
       DSL_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -315,11 +324,15 @@ struct BfsEngine : EngineBase {
         DSL_HIP(hipMalloc(&S.table, buckets * 64));
       }
       DSL_HIP(hipMemsetAsync(S.table, 0, buckets * 64, stream));
-      if (!S.ctr) DSL_HIP(hipMalloc(&S.ctr, sizeof(LevelCounters)));
+      if (!S.ctrbuf) DSL_HIP(hipMalloc(&S.ctrbuf, 2 * kCtrSet));
+      if (!S.hctr) DSL_HIP(hipHostMalloc(&S.hctr, kCtrSet));
+      DSL_HIP(hipMemsetAsync(S.ctrbuf, 0, 2 * kCtrSet, stream));
+      S.cset = 0;
+      S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf);
+      S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + kCtrSegOff);
       if (!S.terms) DSL_HIP(hipMalloc(&S.terms, sizeof(TerminalRec) * kTermCap));
       if (!S.rc) DSL_HIP(hipMalloc(&S.rc, sizeof(RouteCounters)));
       if (!S.seed) DSL_HIP(hipMalloc(&S.seed, 4 * sizeof(int32_t)));
-      if (!S.seg_ctr) DSL_HIP(hipMalloc(&S.seg_ctr, sizeof(unsigned long long) * kSegs * kSegStride));
       S.seg_base.clear();
       S.seg_cnt.clear();
       DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
@@ -431,8 +444,10 @@ struct BfsEngine : EngineBase {
           DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + rows, true, hbase));
           DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + rows, true, hbase));
           DSL_TRY(grow(&S.spill, &S.spill_cap, std::max<uint64_t>(S.work, 1), false, 0));
-          DSL_HIP(hipMemsetAsync(S.ctr, 0, sizeof(LevelCounters), stream));
-          DSL_HIP(hipMemsetAsync(S.seg_ctr, 0, sizeof(unsigned long long) * S.nseg * kSegStride, stream));
+          S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf + S.cset * kCtrSet);
+          S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + S.cset * kCtrSet + kCtrSegOff);
+          // a shard that launches no k_level this level zeroes its next set here
+          if (S.F == 0) DSL_HIP(hipMemsetAsync(S.ctrbuf + (S.cset ^ 1) * kCtrSet, 0, kCtrSet, stream));
           if (route) {
             S.cap_fp = std::max<uint64_t>(S.work, 1);
             DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
@@ -461,6 +476,7 @@ struct BfsEngine : EngineBase {
           a.next_parent = S.hist_parent + hbase;
           a.next_event = S.hist_event + hbase;
           a.seg_ctr = S.seg_ctr;
+          a.zero_next = reinterpret_cast<uint4*>(S.ctrbuf + (S.cset ^ 1) * kCtrSet);
           a.nseg = S.nseg;
           a.segcap = S.segcap;
           a.spill = S.spill;
@@ -488,11 +504,15 @@ struct BfsEngine : EngineBase {
         std::vector<std::vector<unsigned long long>> segc(L, std::vector<unsigned long long>(kSegs * kSegStride));
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
-          DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
-          DSL_HIP(hipMemcpyAsync(segc[l].data(), S.seg_ctr, sizeof(unsigned long long) * S.nseg * kSegStride,
+          DSL_HIP(hipMemcpyAsync(S.hctr, S.ctrbuf + S.cset * kCtrSet, kCtrSegOff + 8 * S.nseg * kSegStride,
                                  hipMemcpyDeviceToHost, stream));
         }
         DSL_HIP(hipStreamSynchronize(stream));
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
+          std::memcpy(segc[l].data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
+        }
         // next frontier: the filled part of each segment, then the spill range (then received)
         std::vector<std::vector<uint64_t>> nbase(L), ncnt(L);
         std::vector<uint64_t> span(L);
@@ -598,8 +618,9 @@ struct BfsEngine : EngineBase {
           }
         }
         if (route || unspilled) {  // counters changed after the first read
-          for (auto& S : sh) DSL_HIP(hipMemcpyAsync(&S.lc, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+          for (auto& S : sh) DSL_HIP(hipMemcpyAsync(S.hctr, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
           DSL_HIP(hipStreamSynchronize(stream));
+          for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
         }
         {
           float kms = 0;
@@ -734,6 +755,7 @@ struct BfsEngine : EngineBase {
           S.F = 0;
           for (uint64_t c : ncnt[l]) S.F += c;
           S.work = S.lc.next_work;
+          S.cset ^= 1;
         }
       }
     }

@@ -35,6 +35,8 @@ constexpr int kWin = 1024;  // work items per class-sorted window of k_level
 constexpr int kSegs = 32;
 constexpr int kMaxSegs = kSegs + 2;
 constexpr int kSegStride = 16;  // u64 words between segment counters (one 128-byte line each)
+constexpr int kCtrSegOff = 4096;                                  // segment counters inside a counter set
+constexpr int kCtrSet = kCtrSegOff + kSegs * kSegStride * 8;      // bytes of one counter set
 
 struct SegTable {
   int32_t n;
@@ -68,6 +70,8 @@ struct LevelCounters {
 #define PH_MARK(i) do { } while (0)
 #define PH_FLUSH(red, ctr) do { } while (0)
 #endif
+
+static_assert(sizeof(LevelCounters) <= kCtrSegOff, "LevelCounters must fit before the segment counters");
 
 struct TerminalRec {
   int32_t verdict;  // V_TERM_*
@@ -214,6 +218,7 @@ struct LevelArgs {
   uint64_t* next_parent;     // history arena slice of the next level
   uint32_t* next_event;
   unsigned long long* seg_ctr;  // nseg counters, kSegStride apart
+  uint4* zero_next;             // the next level's counter set (kCtrSet bytes), zeroed by workgroup 0
   int32_t nseg;
   uint64_t segcap;              // rows per next-frontier segment
   LevelCounters* ctr;
@@ -250,6 +255,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
   unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
   PH_DECL
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < kCtrSet / 16; i += blockDim.x) a.zero_next[i] = make_uint4(0, 0, 0, 0);
 
   const uint64_t nchunks = a.segs.chunk0[a.segs.n];
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
