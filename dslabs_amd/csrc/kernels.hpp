@@ -180,6 +180,15 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
 #pragma unroll
     for (int i = 0; i < P::kNodeWords; i++) nw[i] = __shfl(d.nw[i], src);
     const int n = Net<P>::size(pw);
+    // the parent's records, one per lane (kNetCap <= 64 * TR): a send's lower bound in the sorted
+    // record array is then one ballot + popcount instead of a dependent binary-search chain
+    constexpr int TR = (P::kNetCap + 63) / 64;
+    Rec pr[TR];
+#pragma unroll
+    for (int t = 0; t < TR; t++) {
+      const int q = lane + 64 * t;
+      pr[t] = q < n ? Net<P>::at(pw, q) : ~(Rec)0;
+    }
     EmitAcc acc[T];
 #pragma unroll
     for (int t = 0; t < T; t++) acc[t] = EmitAcc{0u, 0, 0};
@@ -192,7 +201,10 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
         } else {
           r = (Rec)__shfl((unsigned)d.out.r[i], src);
         }
-        const int pos = net_lower_bound<P>(pw, n, r) + i;
+        int lb = 0;
+#pragma unroll
+        for (int t = 0; t < TR; t++) lb += __popcll(__ballot(pr[t] < r));
+        const int pos = lb + i;
 #pragma unroll
         for (int t = 0; t < T; t++) emit_acc_send<P>(acc[t], lane + 64 * t, r, pos);
       }

@@ -381,6 +381,13 @@ struct MultiPaxos {
   }
 
   // ---- predicates -----------------------------------------------------------------------------------
+  // Predicates read node words that live in LDS (parent rows, the changed node's copy) or in host
+  // memory, never in a per-lane array: direct indexing (the select chain of get() would load every
+  // word of a node for a run-time field index).
+  static DSL_HD int getd(const uint32_t* w, int bit, int width) {
+    return (int)((w[bit >> 5] >> (bit & 31)) & ((1u << width) - 1u));
+  }
+  static DSL_HD uint32_t entryd(const uint32_t* w, int slot) { return (uint32_t)getd(w, 32 + 16 * (slot - 1), 16); }
   static DSL_HD int value_of(const Params& p, int cmd) { return cmd ? p.vals[cmd_client(cmd)][cmd_seq(cmd) - 1] : 0; }
 
   // PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (slotValid, PaxosTest.java:215-322); MARKERS_VALID holds by
@@ -389,12 +396,12 @@ struct MultiPaxos {
     int max_ne = 0;
     for (int s = 0; s < p.servers; s++)
       for (int k = 1; k <= kSlots; k++)
-        if (e_status(entry(v.node(s), k)) != EMPTY && k > max_ne) max_ne = k;
+        if (e_status(entryd(v.node(s), k)) != EMPTY && k > max_ne) max_ne = k;
     for (int slot = 1; slot <= max_ne; slot++) {
       bool is_chosen = false;
       int chosen = 0;
       for (int s = 0; s < p.servers; s++) {
-        const uint32_t e = entry(v.node(s), slot);
+        const uint32_t e = entryd(v.node(s), slot);
         if (e_status(e) == CHOSEN) {
           const int x = value_of(p, e_cmd(e));
           if (is_chosen && x != chosen) return PV_FALSE;
@@ -405,7 +412,7 @@ struct MultiPaxos {
       if (!is_chosen) continue;
       int count = 0;
       for (int s = 0; s < p.servers; s++) {
-        const uint32_t e = entry(v.node(s), slot);
+        const uint32_t e = entryd(v.node(s), slot);
         if (e_status(e) != EMPTY && (e_status(e) != ACCEPTED || value_of(p, e_cmd(e)) == chosen)) count++;
       }
       if (2 * count <= p.servers) return PV_FALSE;
@@ -419,9 +426,9 @@ struct MultiPaxos {
     int n = 0;
     for (int c = 0; c < p.clients; c++) {
       const uint32_t* w = v.node(p.servers + c);
-      const int nres = get(w, 15, 2);
+      const int nres = getd(w, 15, 2);
       for (int k = 0; k < nres; k++) {
-        const uint32_t r = (uint32_t)get(w, 32 + 12 * k, 12);
+        const uint32_t r = (uint32_t)getd(w, 32 + 12 * k, 12);
         const int len = r & 7;
         if (len == 0 || (int)((r >> (3 + 2 * (len - 1))) & 3) != p.vals[c][k]) return PV_FALSE;  // endsWith
         all[n++] = r;
@@ -447,28 +454,28 @@ struct MultiPaxos {
       case DSL_PRED_RESULTS_OK:
         for (int c = 0; c < p.clients; c++) {
           const uint32_t* w = v.node(p.servers + c);
-          const int nres = get(w, 15, 2);
+          const int nres = getd(w, 15, 2);
           for (int k = 0; k < nres; k++)
-            if (p.expected[c][k] >= 0 && get(w, 32 + 12 * k, 12) != p.expected[c][k]) return PV_FALSE;
+            if (p.expected[c][k] >= 0 && getd(w, 32 + 12 * k, 12) != p.expected[c][k]) return PV_FALSE;
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
         for (int c = 0; c < p.clients; c++)
-          if (get(v.node(p.servers + c), 15, 2) < p.ncmds[c]) return PV_FALSE;
+          if (getd(v.node(p.servers + c), 15, 2) < p.ncmds[c]) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_DONE: {
         const int c = (int)pr.arg0 - p.servers;
         if (c < 0 || c >= p.clients) return PV_THREW;
-        return get(v.node(p.servers + c), 15, 2) >= p.ncmds[c] ? PV_TRUE : PV_FALSE;
+        return getd(v.node(p.servers + c), 15, 2) >= p.ncmds[c] ? PV_TRUE : PV_FALSE;
       }
       case DSL_PRED_NONE_DECIDED:
         for (int c = 0; c < p.clients; c++)
-          if (get(v.node(p.servers + c), 15, 2) > 0) return PV_FALSE;
+          if (getd(v.node(p.servers + c), 15, 2) > 0) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_HAS_RESULTS: {
         const int c = (int)pr.arg0 - p.servers;
         if (c < 0 || c >= p.clients) return PV_THREW;
-        return get(v.node(p.servers + c), 15, 2) == pr.arg1 ? PV_TRUE : PV_FALSE;
+        return getd(v.node(p.servers + c), 15, 2) == pr.arg1 ? PV_TRUE : PV_FALSE;
       }
       case DSL_PRED_LOGS_CONSISTENT:
         return logs_consistent(v, p);
