@@ -63,6 +63,7 @@ struct EngineBase {
   virtual int set_initial(const uint8_t* p, size_t len, int depth) = 0;
   virtual int get_initial(uint8_t* p, size_t len) = 0;
   virtual int run(dsl_result** out) = 0;
+  virtual int run_dfs(const dsl_dfs_config& c, dsl_result** out) = 0;
   virtual int state_bytes() const = 0;
   volatile unsigned long long progress_states = 0;
   volatile int progress_depth = 0;
@@ -791,6 +792,148 @@ struct BfsEngine : EngineBase {
       std::memcpy(r->terminal_state, &s, sizeof(init));
       trace_events.clear();
     }
+    *out = r;
+    return DSL_OK;
+  }
+
+  // Search.dfs on the device (k_dfs): see dsl_run_dfs in include/dslabs_hip.h.
+  int run_dfs(const dsl_dfs_config& c, dsl_result** out) override {
+    auto t_start = std::chrono::steady_clock::now();
+    (void)hipGetLastError();
+    if (W != 1) {
+      set_error("random DFS runs on a single shard");
+      return DSL_ERR_ARG;
+    }
+    if (!stream) {
+      if (cfg.device >= 0) DSL_HIP(hipSetDevice(cfg.device));
+      DSL_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+      DSL_HIP(hipEventCreate(&ev0));
+      DSL_HIP(hipEventCreate(&ev1));
+    }
+    if (!have_init) {
+      uint8_t tmp[sizeof(init)];
+      DSL_TRY(get_initial(tmp, sizeof(init)));
+    }
+    const uint64_t np = c.probes > 0 ? (uint64_t)c.probes : 65536;
+    const int steps = c.steps_per_launch > 0 ? c.steps_per_launch : 64;
+    const int tcap = hset.max_depth >= 0 ? std::max(1, hset.max_depth - init_depth + 1)
+                                         : (c.max_trace > 0 ? c.max_trace : 4096);
+    struct Bufs {
+      void* p[8] = {};
+      ~Bufs() {
+        for (void* q : p) (void)hipFree(q);
+      }
+    } b;
+    uint32_t *rows, *trace, *dinit;
+    int32_t *pdepth, *pcur, *found, *term;
+    uint64_t* rng;
+    unsigned long long* ctr;
+    DSL_HIP(hipMalloc(&b.p[0], np * 2 * NW * 4));
+    DSL_HIP(hipMalloc(&b.p[1], np * (uint64_t)tcap * 4));
+    DSL_HIP(hipMalloc(&b.p[2], np * 4));
+    DSL_HIP(hipMalloc(&b.p[3], np * 4));
+    DSL_HIP(hipMalloc(&b.p[4], np * 8));
+    DSL_HIP(hipMalloc(&b.p[5], 64));
+    DSL_HIP(hipMalloc(&b.p[6], NW * 4));
+    rows = (uint32_t*)b.p[0];
+    trace = (uint32_t*)b.p[1];
+    pdepth = (int32_t*)b.p[2];
+    pcur = (int32_t*)b.p[3];
+    rng = (uint64_t*)b.p[4];
+    ctr = (unsigned long long*)b.p[5];
+    found = (int32_t*)((char*)b.p[5] + 32);
+    term = (int32_t*)((char*)b.p[5] + 36);
+    dinit = (uint32_t*)b.p[6];
+    std::vector<uint64_t> seeds(np);
+    uint64_t x = c.seed ^ 0x9E3779B97F4A7C15ull;
+    for (uint64_t i = 0; i < np; i++) {  // splitmix64 per probe, never zero
+      uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+      seeds[i] = (z ^ (z >> 31)) | 1;
+    }
+    DSL_HIP(hipMemcpyAsync(rng, seeds.data(), np * 8, hipMemcpyHostToDevice, stream));
+    DSL_HIP(hipMemsetAsync(pdepth, 0xff, np * 4, stream));
+    DSL_HIP(hipMemsetAsync(pcur, 0, np * 4, stream));
+    DSL_HIP(hipMemsetAsync(b.p[5], 0, 64, stream));
+    DSL_HIP(hipMemcpyAsync(dinit, init.w, NW * 4, hipMemcpyHostToDevice, stream));
+    DfsArgs a{dinit, init_depth, tcap, rows, trace, pdepth, pcur, rng, np, steps, ctr, found, term};
+    unsigned long long hc[3] = {0, 0, 0};
+    int32_t hf[4] = {0, 0, 0, 0};
+    int end = DSL_TIME_EXHAUSTED;
+    // the initial state is checked once, as BFS does (RandomDFS.initSearch + the first probe)
+    {
+      int pi = -1;
+      const NodeView v0{init.w, P::kNodeWords, -1, nullptr};
+      const int v = judge_view<P>(v0, prm, dset, init_depth, &pi);
+      if (v >= V_TERM_EXCEPTION) {
+        dsl_result* r = (dsl_result*)calloc(1, sizeof(dsl_result));
+        r->end_condition = v == V_TERM_INVARIANT ? DSL_INVARIANT_VIOLATED : DSL_GOAL_FOUND;
+        r->terminal_depth = init_depth;
+        r->predicate_index = pi;
+        r->states = 1;
+        r->initial_depth = init_depth;
+        r->state_bytes = sizeof(init);
+        r->trace = (dsl_event*)calloc(1, sizeof(dsl_event));
+        r->terminal_state = (uint8_t*)malloc(sizeof(init));
+        std::memcpy(r->terminal_state, &init, sizeof(init));
+        *out = r;
+        return DSL_OK;
+      }
+    }
+    const int blocks = (int)((np + kBlock - 1) / kBlock);
+    while (true) {
+      hipLaunchKernelGGL(k_dfs<P>, dim3(blocks), dim3(kBlock), 0, stream, a, prm, dset);
+      DSL_HIP(hipGetLastError());
+      DSL_HIP(hipMemcpyAsync(hc, ctr, 24, hipMemcpyDeviceToHost, stream));
+      DSL_HIP(hipMemcpyAsync(hf, found, 16, hipMemcpyDeviceToHost, stream));
+      DSL_HIP(hipStreamSynchronize(stream));
+      progress_states = hc[0];
+      if (hc[2]) {
+        set_error("a successor exceeded the packed state's bounds");
+        return DSL_ERR_STATE_OVERFLOW;
+      }
+      if (hf[0]) break;
+      if (c.max_probes > 0 && hc[1] >= (uint64_t)c.max_probes) break;
+      const double el = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+      if (hset.max_time_ms > 0 && el > hset.max_time_ms) break;
+      if (hset.max_time_ms <= 0 && c.max_probes <= 0) {
+        set_error("random DFS needs a time limit (maxTimeSecs) or a probe budget");
+        return DSL_ERR_ARG;
+      }
+    }
+    const double elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
+    dsl_result* r = (dsl_result*)calloc(1, sizeof(dsl_result));
+    r->states = hc[0];
+    r->initial_depth = init_depth;
+    r->elapsed_s = elapsed;
+    r->successors = hc[0];
+    r->state_bytes = sizeof(init);
+    r->terminal_depth = -1;
+    r->predicate_index = -1;
+    if (hf[0]) {
+      const int v = hf[1], depth = hf[3];
+      end = v == V_TERM_EXCEPTION ? DSL_EXCEPTION_THROWN : v == V_TERM_INVARIANT ? DSL_INVARIANT_VIOLATED
+                                                                                 : DSL_GOAL_FOUND;
+      r->predicate_index = v == V_TERM_EXCEPTION ? -1 : hf[2];
+      const uint64_t who = (uint64_t)(hf[0] - 1);
+      std::vector<uint32_t> evs(std::min(depth, tcap));
+      DSL_HIP(hipMemcpy(evs.data(), trace + who * tcap, evs.size() * 4, hipMemcpyDeviceToHost));
+      r->terminal_depth = init_depth + depth;
+      r->max_depth = r->terminal_depth;
+      r->trace_len = (int)evs.size();
+      r->trace = (dsl_event*)calloc(evs.size() + 1, sizeof(dsl_event));
+      typename P::State s = init, n;
+      for (size_t i = 0; i < evs.size(); i++) {  // replayed on the host with the same transitions
+        describe_event<P>(s.w, (int)evs[i], prm, dset, &r->trace[i]);
+        full_step<P>(s.w, (int)evs[i], n.w, prm, dset);
+        s = n;
+      }
+      r->terminal_state = (uint8_t*)malloc(sizeof(init));
+      std::memcpy(r->terminal_state, &s, sizeof(init));
+    }
+    r->end_condition = end;
+    r->new_states_inserted = hc[1];  // probes started
     *out = r;
     return DSL_OK;
   }

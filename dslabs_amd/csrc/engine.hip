@@ -349,6 +349,14 @@ int dsl_run(dsl_engine* e, dsl_result** out) {
   return e->impl->run(out);
 }
 
+int dsl_run_dfs(dsl_engine* e, const dsl_dfs_config* cfg, dsl_result** out) {
+  if (!e || !out) return DSL_ERR_ARG;
+  *out = nullptr;
+  dsl_dfs_config c{};
+  if (cfg) c = *cfg;
+  return e->impl->run_dfs(c, out);
+}
+
 int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth) {
   if (!e) return DSL_ERR_ARG;
   if (states) *states = e->impl->progress_states;

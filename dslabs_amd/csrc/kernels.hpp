@@ -633,3 +633,115 @@ __global__ void __launch_bounds__(kBlock) k_append_received(const StateRec<P>* i
 }
 
 }  // namespace dsl
+
+namespace dsl {
+
+// ---- random depth-first search (RandomDFS.runProbe, Search.java:507-583) -------------------------
+// One probe per lane: from the initial state, repeatedly try the current state's enabled events in
+// a random order (a random rotation of SearchState.events: Collections.shuffle's role) and move to
+// the first successor that is not null and not PRUNED (counting every non-null successor, as
+// states.incrementAndGet()); a TERMINAL successor ends the whole search (first lane wins a CAS); a
+// state with no such successor ends the probe and the lane starts a new one. There is no visited
+// set. Each launch runs a bounded number of steps per lane, so every wavefront exits.
+struct DfsArgs {
+  const uint32_t* init;
+  int32_t init_depth;
+  int32_t tcap;              // events a probe may record (longer probes are restarted)
+  uint32_t* rows;            // 2 rows per probe (current / successor)
+  uint32_t* trace;           // tcap events per probe
+  int32_t* pdepth;           // steps taken by the probe; -1 = start a new probe
+  int32_t* pcur;             // which of its two rows is current
+  uint64_t* rng;
+  uint64_t nprobe;
+  int32_t steps;
+  unsigned long long* ctr;   // [states, probes, overflow]
+  int32_t* found;            // 0, or 1 + the winning probe
+  int32_t* term;             // winner: [verdict, predicate index, depth]
+};
+
+__device__ __forceinline__ uint64_t xorshift64s(uint64_t& x) {
+  x ^= x >> 12;
+  x ^= x << 25;
+  x ^= x >> 27;
+  return x * 0x2545F4914F6CDD1Dull;
+}
+
+template <class P>
+__global__ void __launch_bounds__(kBlock) k_dfs(DfsArgs a, typename P::Params prm, DevSettings set) {
+  constexpr int NW = Layout<P>::kWords;
+  const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned long long c_states = 0, c_probes = 0, c_err = 0;
+  if (lane < a.nprobe) {
+    int dep = a.pdepth[lane], cur = a.pcur[lane];
+    uint64_t rng = a.rng[lane];
+    uint32_t* const base = a.rows + lane * 2 * NW;
+    for (int step = 0; step < a.steps; step++) {
+      if (__hip_atomic_load(a.found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      if (dep < 0) {  // runProbe: a new probe from the initial state (counted once)
+        for (int i = 0; i < NW; i++) base[i] = a.init[i];
+        cur = 0;
+        dep = 0;
+        c_probes++;
+        c_states++;
+      }
+      const uint32_t* w = base + cur * NW;
+      uint32_t* nxt = base + (cur ^ 1) * NW;
+      const int ne = count_events<P>(w, prm, set);
+      bool advanced = false, ended = false;
+      const int r0 = ne ? (int)(xorshift64s(rng) % (uint64_t)ne) : 0;
+      for (int i = 0; i < ne && !advanced && !ended; i++) {
+        const int k = r0 + i < ne ? r0 + i : r0 + i - ne;
+        Delta<P> d;
+        const int rc = delta_step<P>(w, k, d, prm, set);
+        if (rc == STEP_NULL) continue;
+        c_states++;
+        int v, pi = -1;
+        if (rc == STEP_EXCEPTION) {
+          v = V_TERM_EXCEPTION;
+        } else if (rc == STEP_OVERFLOW || !emit_row<P>(w, d, nxt)) {
+          c_err++;
+          ended = true;
+          break;
+        } else {
+          const NodeView view{nxt, P::kNodeWords, -1, nullptr};
+          v = judge_view<P>(view, prm, set, a.init_depth + dep + 1, &pi);
+        }
+        if (v >= V_TERM_EXCEPTION) {
+          if (dep < a.tcap) a.trace[lane * a.tcap + dep] = (uint32_t)k;
+          if (atomicCAS(a.found, 0, (int)(lane + 1)) == 0) {
+            a.term[0] = v;
+            a.term[1] = pi;
+            a.term[2] = dep + 1;
+          }
+          ended = true;
+          break;
+        }
+        if (v == V_PRUNED) continue;
+        if (dep >= a.tcap) {  // too long to record: restart
+          ended = true;
+          break;
+        }
+        a.trace[lane * a.tcap + dep] = (uint32_t)k;
+        dep++;
+        cur ^= 1;
+        advanced = true;
+      }
+      if (!advanced) dep = -1;  // no non-pruned successor (or ended): the probe is over
+    }
+    a.pdepth[lane] = dep;
+    a.pcur[lane] = cur;
+    a.rng[lane] = rng;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    c_states += __shfl_xor(c_states, o);
+    c_probes += __shfl_xor(c_probes, o);
+    c_err += __shfl_xor(c_err, o);
+  }
+  if (__lane_id() == 0) {
+    if (c_states) atomicAdd(&a.ctr[0], c_states);
+    if (c_probes) atomicAdd(&a.ctr[1], c_probes);
+    if (c_err) atomicAdd(&a.ctr[2], c_err);
+  }
+}
+
+}  // namespace dsl

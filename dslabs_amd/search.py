@@ -377,17 +377,36 @@ class Engine:
         check(self.lib.dsl_kernel_stats(self.handle, ctypes.byref(st)), "dsl_kernel_stats")
         return {name: getattr(st, name) for name, _ in st._fields_}
 
-    def bfs(self, state: SearchState, settings: Optional[SearchSettings] = None) -> SearchResults:
-        if settings is None:
-            settings = SearchSettings()
+    def _prepare(self, state: SearchState, settings: SearchSettings):
         lib = self.lib
         enc = settings._encode(state)
         check(lib.dsl_set_settings(self.handle, ctypes.byref(enc)), "dsl_set_settings")
         if state.packed is not None:
             buf = (ctypes.c_uint8 * len(state.packed)).from_buffer_copy(state.packed)
             check(lib.dsl_set_initial(self.handle, buf, len(state.packed), state.depth()), "dsl_set_initial")
+
+    def bfs(self, state: SearchState, settings: Optional[SearchSettings] = None) -> SearchResults:
+        if settings is None:
+            settings = SearchSettings()
+        self._prepare(state, settings)
         res_p = ctypes.POINTER(_lib.dsl_result)()
-        check(lib.dsl_run(self.handle, ctypes.byref(res_p)), "dsl_run")
+        check(self.lib.dsl_run(self.handle, ctypes.byref(res_p)), "dsl_run")
+        return self._results(state, settings, res_p)
+
+    def dfs(self, state: SearchState, settings: Optional[SearchSettings] = None, probes: int = 65536,
+            seed: int = 0, max_probes: int = 0) -> SearchResults:
+        """Search.dfs / RandomDFS (Search.java:397-402, :507-583) on the device: `probes` random
+        walks at once until a terminal state, settings.maxTimeSecs, or `max_probes` probes."""
+        if settings is None:
+            settings = SearchSettings()
+        self._prepare(state, settings)
+        c = _lib.dsl_dfs_config(probes, seed & ((1 << 64) - 1), max_probes, 0, 0)
+        res_p = ctypes.POINTER(_lib.dsl_result)()
+        check(self.lib.dsl_run_dfs(self.handle, ctypes.byref(c), ctypes.byref(res_p)), "dsl_run_dfs")
+        return self._results(state, settings, res_p)
+
+    def _results(self, state: SearchState, settings: SearchSettings, res_p) -> SearchResults:
+        lib = self.lib
         try:
             r = res_p.contents
             per_depth = [r.per_depth[i] for i in range(r.n_levels)]
@@ -418,5 +437,15 @@ class Search:
         eng = Engine(initialState.protocol, device=device)
         try:
             return eng.bfs(initialState, settings)
+        finally:
+            eng.close()
+
+    @staticmethod
+    def dfs(initialState: SearchState, settings: Optional[SearchSettings] = None, device: int = -1,
+            **kw) -> SearchResults:
+        """Search.dfs (Search.java:397-402): random depth-first probes on the MI355X engine."""
+        eng = Engine(initialState.protocol, device=device)
+        try:
+            return eng.dfs(initialState, settings, **kw)
         finally:
             eng.close()

@@ -178,6 +178,23 @@ int dsl_set_initial(dsl_engine* e, const uint8_t* packed, size_t len, int32_t de
 int dsl_get_initial(dsl_engine* e, uint8_t* packed, size_t len);
 int dsl_run(dsl_engine* e, dsl_result** out);
 int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth);
+
+/* Random depth-first search (Search.dfs / RandomDFS, Search.java:397-402, :507-583): `probes`
+ * independent random walks run concurrently on the device (one per lane), each restarted from
+ * the initial state when it ends, until a terminal state is found (EXCEPTION / INVARIANT / GOAL,
+ * with its replayable trace) or the time (settings.max_time_ms) or probe budget is spent
+ * (end condition TIME_EXHAUSTED: RandomDFS never exhausts the space). result->states counts the
+ * initial state once per probe plus every non-null successor, as RandomDFS does; per_depth is
+ * empty. Single shard only. */
+typedef struct {
+  int64_t probes;           /* concurrent walks (0 = 65536) */
+  uint64_t seed;
+  int64_t max_probes;       /* stop after this many probes were started (0 = no limit) */
+  int32_t steps_per_launch; /* 0 = 64 */
+  int32_t max_trace;        /* events recorded per probe when maxDepth is unbounded (0 = 4096) */
+} dsl_dfs_config;
+
+int dsl_run_dfs(dsl_engine* e, const dsl_dfs_config* cfg, dsl_result** out);
 /* Cumulative kernel statistics of the last dsl_run (HIP events on the engine's stream). The
  * byte model of the expand kernel: parents read once (S bytes each), one 64-byte
  * visited-table bucket line per successor probe, one bucket line written back + 12 bytes of

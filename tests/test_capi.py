@@ -48,3 +48,31 @@ def test_create_fails_loudly_without_device(lib):
     with pytest.raises(_lib.EngineError) as ei:
         Search.bfs(pingpong_state(1, 2))
     assert "DSL_ERR_NO_DEVICE" in str(ei.value)
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """sizeof / offsetof of every ABI struct, compiled from include/dslabs_hip.h with gcc, against
+    the ctypes mirrors in dslabs_amd/_lib.py."""
+    import subprocess
+    from dslabs_amd import _lib
+    structs = {"dsl_protocol_desc": ["protocol", "params"], "dsl_engine_config": ["comm_id", "replicate_below"],
+               "dsl_settings": ["table_log2_slots", "max_frontier_states"], "dsl_event": ["fields"],
+               "dsl_result": ["per_depth", "trace", "terminal_state"], "dsl_stats": ["table_slots"],
+               "dsl_dfs_config": ["max_probes", "max_trace"], "dsl_predicate": ["arg1"]}
+    src = ['#include <stdio.h>', '#include <stddef.h>', '#include "dslabs_hip.h"', "int main(void) {"]
+    for st, fields in structs.items():
+        src.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fields:
+            src.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    src.append("return 0; }")
+    c = tmp_path / "abi.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "abi"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(c)], check=True)
+    got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
+                                                       text=True).stdout.splitlines())
+    for st, fields in structs.items():
+        cls = getattr(_lib, st)
+        assert ctypes.sizeof(cls) == int(got[st]), st
+        for f in fields:
+            assert getattr(cls, f).offset == int(got[f"{st}.{f}"]), (st, f)
