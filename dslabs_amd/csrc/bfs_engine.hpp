@@ -24,6 +24,12 @@
 
 #include "kernels.hpp"
 
+// LDS budget for a k_level chunk's parent rows: with the kernel's ~11 KB of static LDS, 4
+// resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
+#ifndef DSL_ROWS_LDS_KB
+#define DSL_ROWS_LDS_KB 24
+#endif
+
 namespace dsl {
 
 void set_error(const std::string& msg);
@@ -138,6 +144,22 @@ struct BfsEngine : EngineBase {
   uint64_t avg_events_x16 = 16 * 8;  // running estimate of events per state (x16)
   std::vector<uint32_t> trace_events;
 
+  // ---- queued small levels (single local shard) ------------------------------------------------
+  // While the frontier is small, a level's kernel is short and the host round trip between levels
+  // (counter copy, sync, next launch) is a large part of its time. Up to kQueue levels are then
+  // enqueued back to back; each derives its row ranges from the previous level's counters on the
+  // device and stops (with every later one) where the host must act (queue_continues). The host
+  // then walks the queued levels' counters with the ordinary per-level bookkeeping.
+  static constexpr int kQueue = 12;
+  static constexpr uint64_t kQueueF = 16384, kQueueWork = 1u << 19;
+  static constexpr uint64_t kQueueRows = 1u << 16;  // next-frontier rows per queued level (more: spill)
+  unsigned char* qctr = nullptr;   // kQueue + 1 counter sets
+  unsigned char* hq = nullptr;     // pinned copy of the kQueue sets
+  std::vector<hipEvent_t> qev;     // brackets the whole queue (no event packets between its levels)
+  int q_left = 0, q_pos = 0;
+  uint64_t n_reallocs = 0;  // device buffer reallocations (DSL_LEVEL_TRACE)
+  uint64_t q_segcap = 0;
+
   BfsEngine(const typename P::Params& p, const dsl_engine_config& c, int world, Comm* cm)
       : prm(p), cfg(c), W(world), comm(cm) {
     dsl_settings s{};
@@ -165,6 +187,9 @@ struct BfsEngine : EngineBase {
       for (void* q : ptrs) (void)hipFree(q);
       if (s.hctr) (void)hipHostFree(s.hctr);
     }
+    (void)hipFree(qctr);
+    if (hq) (void)hipHostFree(hq);
+    for (auto e : qev) (void)hipEventDestroy(e);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     comm.reset();
@@ -207,6 +232,7 @@ struct BfsEngine : EngineBase {
     if (need <= *cap && *ptr) return DSL_OK;
     const uint64_t ncap = std::max<uint64_t>(std::max<uint64_t>(need, *cap + *cap / 2), 1024);
     T* np = nullptr;
+    n_reallocs++;
     DSL_HIP(hipMalloc(&np, ncap * sizeof(T)));
     if (keep && *ptr && keep_elems)
       DSL_HIP(hipMemcpyAsync(np, *ptr, keep_elems * sizeof(T), hipMemcpyDeviceToDevice, stream));
@@ -291,11 +317,108 @@ struct BfsEngine : EngineBase {
   uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 19) : (uint64_t)cfg.replicate_below; }
   int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
-    int lds_max = (int)((24 * 1024) / per);
+    int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / per);
     int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
     const int spread = (int)std::max<uint64_t>(1, (F + 1023) / 1024);
     int pb = std::max(1, std::min({want, lds_max, kLevelBlock, spread}));
     return pb;
+  }
+
+  // Enqueues up to kQueue levels of shard 0 (see the members above); returns how many ran.
+  int enqueue_queue(int depth, const Table& tbl_proto, int* ran) {
+    Shard& S = sh[0];
+    if (!qctr) {
+      DSL_HIP(hipMalloc(&qctr, (size_t)(kQueue + 1) * kCtrSet));
+      DSL_HIP(hipHostMalloc(&hq, (size_t)kQueue * kCtrSet));
+      qev.resize(2);
+      for (auto& e : qev) DSL_HIP(hipEventCreate(&e));
+    }
+    const int nseg = kSegs;
+    q_segcap = (kQueueRows + nseg - 1) / nseg + 1;
+    const uint64_t span = q_segcap * nseg;
+    uint64_t used = 0;  // rows of the current frontier that must be kept
+    for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
+    DSL_TRY(grow_rows(&S.cur, &S.cur_cap, std::max(span, used), true, used));
+    DSL_TRY(grow(&S.cur_fp, &S.curfp_cap, std::max(span, used), true, used));
+    DSL_TRY(grow_rows(&S.next, &S.next_cap, span, false, 0));
+    DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, span, false, 0));
+    const uint64_t hbase0 = S.level_base.back() + S.level_size.back();
+    DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
+    DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
+    DSL_TRY(grow(&S.spill, &S.spill_cap, kQueueWork, false, 0));
+    const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
+    const int pb_max = std::max(1, std::min({(int)((DSL_ROWS_LDS_KB * 1024) / per), kLevelBlock,
+                                             (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) /
+                                                   std::max<uint64_t>(avg_events_x16, 1))}));
+    const int spread = 1024;
+    SegTable t0{};
+    t0.n = (int32_t)S.seg_cnt.size();
+    t0.pb = (int)std::min<uint64_t>((uint64_t)pb_max, std::max<uint64_t>(1, (S.F + spread - 1) / spread));
+    for (int q = 0; q < t0.n; q++) {
+      t0.base[q] = S.seg_base[q];
+      t0.cnt[q] = S.seg_cnt[q];
+      t0.chunk0[q + 1] = t0.chunk0[q] + (S.seg_cnt[q] + t0.pb - 1) / t0.pb;
+    }
+    // every set starts zeroed: the levels after a stop leave theirs untouched, and read zeros
+    DSL_HIP(hipMemsetAsync(qctr, 0, (size_t)(kQueue + 1) * kCtrSet, stream));
+    const uint64_t flimit = W > 1 ? std::min<uint64_t>(kQueueF, rep_threshold() - 1) : kQueueF;
+    const size_t lds = (size_t)pb_max * per + 16;
+    for (int j = 0; j < kQueue; j++) {
+      unsigned char* set = qctr + (size_t)j * kCtrSet;
+      LevelArgs<P> a{};
+      a.cur = (j & 1) ? S.next : S.cur;
+      a.cur_fp = (j & 1) ? S.next_fp : S.cur_fp;
+      a.segs = t0;
+      a.qprev = j ? reinterpret_cast<const LevelCounters*>(set - kCtrSet) : nullptr;
+      a.qprev_seg = j ? reinterpret_cast<const unsigned long long*>(set - kCtrSet + kCtrSegOff) : nullptr;
+      a.qflimit = flimit;
+      a.qwlimit = kQueueWork;
+      a.qspread = spread;
+      a.PB = pb_max;
+      a.depth = depth + 1 + j;
+      a.incremental = depth + j > init_depth ? 1 : 0;
+      a.next = (j & 1) ? S.cur : S.next;
+      a.next_fp = (j & 1) ? S.cur_fp : S.next_fp;
+      a.next_parent = S.hist_parent + hbase0 + (uint64_t)j * span;
+      a.next_event = S.hist_event + hbase0 + (uint64_t)j * span;
+      a.seg_ctr = reinterpret_cast<unsigned long long*>(set + kCtrSegOff);
+      a.zero_next = reinterpret_cast<uint4*>(set + kCtrSet);
+      a.nseg = nseg;
+      a.segcap = q_segcap;
+      a.spill = S.spill;
+      a.spill_cap = S.spill_cap;
+      a.ctr = reinterpret_cast<LevelCounters*>(set);
+      a.terms = S.terms;
+      a.table = tbl_proto;
+      a.table.slots = S.table;
+      a.W = W;
+      a.me = S.gid;
+      a.owner_filter = 0;
+      if (j == 0) DSL_HIP(hipEventRecord(qev[0], stream));
+      hipLaunchKernelGGL((k_level<P, false>), dim3(1024), dim3(kLevelBlock), lds, stream, a, prm, dset);
+      DSL_HIP(hipGetLastError());
+    }
+    DSL_HIP(hipEventRecord(qev[1], stream));
+    DSL_HIP(hipMemcpyAsync(hq, qctr, (size_t)kQueue * kCtrSet, hipMemcpyDeviceToHost, stream));
+    DSL_HIP(hipStreamSynchronize(stream));
+    // the levels that ran: up to the first whose counters stop the queue (the device's rule)
+    *ran = kQueue;
+    for (int j = 0; j + 1 < kQueue; j++) {
+      const unsigned char* set = hq + (size_t)j * kCtrSet;
+      LevelCounters c;
+      std::memcpy(&c, set, sizeof(c));
+      uint64_t F = 0;
+      for (int q = 0; q < nseg; q++) {
+        unsigned long long v;
+        std::memcpy(&v, set + kCtrSegOff + (size_t)q * kSegStride * 8, 8);
+        F += std::min<uint64_t>(v, q_segcap);
+      }
+      if (!queue_continues(c, F, flimit, kQueueWork)) {
+        *ran = j + 1;
+        break;
+      }
+    }
+    return DSL_OK;
   }
 
   int run(dsl_result** out) override {
@@ -350,6 +473,10 @@ struct BfsEngine : EngineBase {
     }
     table_buckets = buckets;
     stats.table_slots = buckets * 8 * (uint64_t)W;
+    q_left = 0;
+    q_pos = 0;
+    const bool use_queue = !getenv("DSL_NO_QUEUE");
+    const bool trace_levels = getenv("DSL_LEVEL_TRACE") != nullptr;
     const Table tbl_proto{nullptr, buckets - 1, 64};
 
     // Seed: the initial state lives on its owner shard (BFS.initSearch, Search.java:434-440).
@@ -423,6 +550,15 @@ struct BfsEngine : EngineBase {
         }
         if (g[0] == 0) break;
 
+        if (use_queue && q_left == 0 && L == 1 && (W == 1 || rep) && sh[0].F > 0 && sh[0].F <= kQueueF &&
+            sh[0].work <= kQueueWork) {
+          int ran = 0;
+          DSL_TRY(enqueue_queue(depth, tbl_proto, &ran));
+          q_left = ran;
+          q_pos = 0;
+        }
+        const bool queued = q_left > 0;
+
         // Capacity: the level has exactly S.work work items, an upper bound on its new states.
         // The next frontier gets min(work, 4F) rows (typical growth is ~3 new states per
         // parent) split into nseg equal segments; VALID states beyond a segment's rows are
@@ -431,6 +567,10 @@ struct BfsEngine : EngineBase {
         uint64_t Fmax = 0;
         for (auto& S : sh) Fmax = std::max(Fmax, S.F);
         const int PB = chunk_parents(Fmax);
+        if (queued) {
+          sh[0].nseg = kSegs;
+          sh[0].segcap = q_segcap;
+        } else {
         for (auto& S : sh) {
           uint64_t nchunks = 0;
           for (size_t q = 0; q < S.seg_cnt.size(); q++) nchunks += (S.seg_cnt[q] + PB - 1) / PB;
@@ -454,7 +594,9 @@ struct BfsEngine : EngineBase {
             DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
           }
         }
+        }  // !queued (capacity)
         const size_t lds = (size_t)PB * (NW * 4 + sizeof(Fp) + 4) + 16;
+        if (!queued) {
         DSL_HIP(hipEventRecord(ev0, stream));
         for (auto& S : sh) {
           if (S.F == 0) continue;
@@ -492,6 +634,9 @@ struct BfsEngine : EngineBase {
           a.out_fp = S.out_fp;
           a.cap_fp = S.cap_fp;
           a.rc = S.rc;
+          a.qprev = nullptr;
+          a.qprev_seg = nullptr;
+          a.segs.pb = PB;
           const uint64_t nchunks = a.segs.chunk0[a.segs.n];
           const int blocks = (int)std::min<uint64_t>(nchunks, kLevelGrid);
           if (route)
@@ -501,8 +646,14 @@ struct BfsEngine : EngineBase {
           DSL_HIP(hipGetLastError());
         }
         DSL_HIP(hipEventRecord(ev1, stream));
+        }  // !queued (launch)
         // spilled VALID states: grow the next frontier and materialize them after the local rows
         std::vector<std::vector<unsigned long long>> segc(L, std::vector<unsigned long long>(kSegs * kSegStride));
+        if (queued) {  // this level's counters came back with the queue
+          const unsigned char* set = hq + (size_t)q_pos * kCtrSet;
+          std::memcpy(&sh[0].lc, set, sizeof(LevelCounters));
+          std::memcpy(segc[0].data(), set + kCtrSegOff, 8 * kSegs * kSegStride);
+        } else {
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
           DSL_HIP(hipMemcpyAsync(S.hctr, S.ctrbuf + S.cset * kCtrSet, kCtrSegOff + 8 * S.nseg * kSegStride,
@@ -513,6 +664,7 @@ struct BfsEngine : EngineBase {
           Shard& S = sh[l];
           std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
           std::memcpy(segc[l].data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
+        }
         }
         // next frontier: the filled part of each segment, then the spill range (then received)
         std::vector<std::vector<uint64_t>> nbase(L), ncnt(L);
@@ -538,8 +690,9 @@ struct BfsEngine : EngineBase {
           DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + need, true, hbase + keep));
           DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + need, true, hbase + keep));
           const int blocks = (int)std::min<uint64_t>((ns + kBlock - 1) / kBlock, 256ull * 32);
+          LevelCounters* uctr = queued ? reinterpret_cast<LevelCounters*>(qctr + (size_t)q_pos * kCtrSet) : S.ctr;
           hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, ns, S.cur, S.cur_fp, S.next,
-                             S.next_fp, S.hist_parent + hbase, S.hist_event + hbase, keep, S.gid, S.ctr, prm, dset);
+                             S.next_fp, S.hist_parent + hbase, S.hist_event + hbase, keep, S.gid, uctr, prm, dset);
           nbase[l].push_back(keep);
           ncnt[l].push_back(ns);
           span[l] = need;
@@ -619,16 +772,19 @@ struct BfsEngine : EngineBase {
           }
         }
         if (route || unspilled) {  // counters changed after the first read
-          for (auto& S : sh) DSL_HIP(hipMemcpyAsync(S.hctr, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+          for (auto& S : sh) {
+            const void* src = queued ? (const void*)(qctr + (size_t)q_pos * kCtrSet) : (const void*)S.ctr;
+            DSL_HIP(hipMemcpyAsync(S.hctr, src, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
+          }
           DSL_HIP(hipStreamSynchronize(stream));
           for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
         }
-        {
+        if (!queued || q_pos == 0) {  // a queue is timed as a whole, with its launches counted
           float kms = 0;
-          (void)hipEventElapsedTime(&kms, ev0, ev1);
+          (void)hipEventElapsedTime(&kms, queued ? qev[0] : ev0, queued ? qev[1] : ev1);
           stats.expand_ms += kms;
-          stats.expand_launches++;
         }
+        stats.expand_launches++;
 #ifdef DSL_PHASES
         for (auto& S : sh) {
           const auto& q = S.lc.phase;
@@ -699,8 +855,12 @@ struct BfsEngine : EngineBase {
           S.level_base.push_back(hbase);
           S.level_size.push_back(span[l]);
         }
-        level_ms_max = std::max(
-            level_ms_max, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count());
+        const double lms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count();
+        level_ms_max = std::max(level_ms_max, lms);
+        if (trace_levels)
+          fprintf(stderr, "[level] depth %d F=%llu new=%llu queued=%d wall_ms=%.4f reallocs=%llu\n", depth,
+                  (unsigned long long)gsum[7], (unsigned long long)gsum[0], queued ? 1 : 0, lms,
+                  (unsigned long long)n_reallocs);
         if (enc != ~0ull) {
           const int wrank = (int)(enc & 0xff);
           uint64_t rec[4] = {0, 0, 0, 0};
@@ -756,7 +916,11 @@ struct BfsEngine : EngineBase {
           S.F = 0;
           for (uint64_t c : ncnt[l]) S.F += c;
           S.work = S.lc.next_work;
-          S.cset ^= 1;
+          if (!queued) S.cset ^= 1;  // queued levels used the queue's counter sets
+        }
+        if (queued) {
+          q_pos++;
+          q_left--;
         }
       }
     }

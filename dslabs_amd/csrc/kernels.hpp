@@ -40,6 +40,7 @@ constexpr int kCtrSet = kCtrSegOff + kSegs * kSegStride * 8;      // bytes of on
 
 struct SegTable {
   int32_t n;
+  int32_t pb;                     // parents per chunk
   uint64_t base[kMaxSegs];
   uint64_t cnt[kMaxSegs];
   uint64_t chunk0[kMaxSegs + 1];  // first chunk of each segment; chunk0[n] = chunks of the level
@@ -243,7 +244,20 @@ struct LevelArgs {
   FpRec* out_fp;             // W regions of cap_fp records (ROUTE only)
   uint64_t cap_fp;
   RouteCounters* rc;
+  // Queued levels (single shard, BfsEngine::enqueue_queue): the frontier's table is derived from
+  // the previous queued level's counters instead of `segs`, by the rule the host applies.
+  const LevelCounters* qprev;        // null: the table is `segs`
+  const unsigned long long* qprev_seg;
+  uint64_t qflimit, qwlimit;         // the queue stops above these frontier / work sizes
+  int32_t qspread;                   // parents per chunk = ceil(F / qspread), at most PB
 };
+
+// The queue's stop rule: after a level with any of these, the host must act before the next one.
+__host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
+                                                uint64_t wlimit) {
+  return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier) && F > 0 && F <= flimit &&
+         c.next_work <= wlimit;
+}
 
 template <class P, bool ROUTE>
 // Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel; the few values the
@@ -254,10 +268,11 @@ template <class P, bool ROUTE>
 __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   extern __shared__ __align__(16) uint32_t lds[];
-  uint32_t* rows = lds;                                    // PB * NW
-  Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // PB
-  int* off = reinterpret_cast<int*>(fps + a.PB);           // PB + 1
+  uint32_t* rows = lds;                                    // a.PB (max) * NW
+  Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
+  int* off = reinterpret_cast<int*>(fps + a.PB);           // a.PB + 1
   __shared__ int s_total;
+  __shared__ SegTable s_segs;
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
   __shared__ unsigned long long s_red[kLevelBlock / 64];
@@ -267,16 +282,51 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
   unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
   PH_DECL
+  __shared__ int s_stop;
+  if (a.qprev) {
+    // queued level: this frontier is the previous level's segments; every workgroup derives the
+    // table (and whether the queue stopped) from those counters, as the host does afterwards
+    if (threadIdx.x < 64) {
+      const int q = threadIdx.x;
+      const uint64_t c = q < a.nseg ? min<uint64_t>(a.qprev_seg[q * kSegStride], a.segcap) : 0ull;
+      uint64_t F = c;
+      for (int o = 32; o > 0; o >>= 1) F += __shfl_xor(F, o);
+      const int pb = (int)min<uint64_t>((uint64_t)a.PB, max<uint64_t>(1, (F + a.qspread - 1) / a.qspread));
+      uint64_t inc = (c + pb - 1) / pb;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t v = __shfl_up(inc, o);
+        if (q >= o) inc += v;
+      }
+      if (q < a.nseg) {
+        s_segs.base[q] = (uint64_t)q * a.segcap;
+        s_segs.cnt[q] = c;
+        s_segs.chunk0[q + 1] = inc;
+      }
+      if (q == 0) {
+        s_segs.n = a.nseg;
+        s_segs.pb = pb;
+        s_segs.chunk0[0] = 0;
+        s_stop = queue_continues(*a.qprev, F, a.qflimit, a.qwlimit) ? 0 : 1;
+      }
+    }
+  } else {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&a.segs);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&s_segs);
+    for (int i = threadIdx.x; i < (int)(sizeof(SegTable) / 4); i += blockDim.x) dst[i] = src[i];
+    if (threadIdx.x == 0) s_stop = 0;
+  }
+  __syncthreads();
+  if (s_stop) return;  // an earlier queued level stopped the queue
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kCtrSet / 16; i += blockDim.x) a.zero_next[i] = make_uint4(0, 0, 0, 0);
-
-  const uint64_t nchunks = a.segs.chunk0[a.segs.n];
+  const int PB = s_segs.pb;
+  const uint64_t nchunks = s_segs.chunk0[s_segs.n];
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
   int g = 0;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
-    while (chunk >= a.segs.chunk0[g + 1]) g++;  // chunks ascend: the segment index only grows
-    const uint64_t p0 = a.segs.base[g] + (chunk - a.segs.chunk0[g]) * (uint64_t)a.PB;
-    const int pb = (int)min<uint64_t>((uint64_t)a.PB, a.segs.base[g] + a.segs.cnt[g] - p0);
+    while (chunk >= s_segs.chunk0[g + 1]) g++;  // chunks ascend: the segment index only grows
+    const uint64_t p0 = s_segs.base[g] + (chunk - s_segs.chunk0[g]) * (uint64_t)PB;
+    const int pb = (int)min<uint64_t>((uint64_t)PB, s_segs.base[g] + s_segs.cnt[g] - p0);
     // 1. stage the parents (contiguous rows) and their fingerprints in LDS
     {
       const uint4* src = reinterpret_cast<const uint4*>(a.cur + p0 * NW);
