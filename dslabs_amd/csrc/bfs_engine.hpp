@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -150,9 +151,25 @@ struct BfsEngine : EngineBase {
   // enqueued back to back; each derives its row ranges from the previous level's counters on the
   // device and stops (with every later one) where the host must act (queue_continues). The host
   // then walks the queued levels' counters with the ordinary per-level bookkeeping.
+  // A queue's capacity is `span` next-frontier rows per level (32 segments), sized from the
+  // frontier it starts at: 32x its size, at least kQueueRowsMin, at most 1 GiB of rows. It runs
+  // while the frontier stays within span/4 states (a level grows it ~3x) and the next level's
+  // work items fit the spill list (8 span); past a segment's rows a level spills and stops it.
   static constexpr int kQueue = 12;
-  static constexpr uint64_t kQueueF = 16384, kQueueWork = 1u << 19;
-  static constexpr uint64_t kQueueRows = 1u << 16;  // next-frontier rows per queued level (more: spill)
+  static constexpr uint64_t kQueueRowsMin = 1u << 16;
+  uint64_t queue_span_max() const {
+    uint64_t s = 1ull << 24;
+    while (s > kQueueRowsMin && s * NW * 4 > (1ull << 30)) s >>= 1;
+    return s;
+  }
+  uint64_t queue_span(uint64_t F) const {
+    uint64_t s = kQueueRowsMin;
+    while (s < 32 * F && s < queue_span_max()) s <<= 1;
+    return s;
+  }
+  uint64_t queue_flimit(uint64_t span) const {
+    return W > 1 ? std::min<uint64_t>(span / 4, rep_threshold() - 1) : span / 4;
+  }
   unsigned char* qctr = nullptr;   // kQueue + 1 counter sets
   unsigned char* hq = nullptr;     // pinned copy of the kQueue sets
   std::vector<hipEvent_t> qev;     // brackets the whole queue (no event packets between its levels)
@@ -325,7 +342,7 @@ struct BfsEngine : EngineBase {
   }
 
   // Enqueues up to kQueue levels of shard 0 (see the members above); returns how many ran.
-  int enqueue_queue(int depth, const Table& tbl_proto, int* ran) {
+  int enqueue_queue(int depth, const Table& tbl_proto, double growth, int* ran) {
     Shard& S = sh[0];
     if (!qctr) {
       DSL_HIP(hipMalloc(&qctr, (size_t)(kQueue + 1) * kCtrSet));
@@ -334,8 +351,9 @@ struct BfsEngine : EngineBase {
       for (auto& e : qev) DSL_HIP(hipEventCreate(&e));
     }
     const int nseg = kSegs;
-    q_segcap = (kQueueRows + nseg - 1) / nseg + 1;
-    const uint64_t span = q_segcap * nseg;
+    const uint64_t span = queue_span(S.F);
+    q_segcap = span / nseg;
+    const uint64_t flimit = queue_flimit(span), wlimit = 8 * span;
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
     DSL_TRY(grow_rows(&S.cur, &S.cur_cap, std::max(span, used), true, used));
@@ -345,7 +363,7 @@ struct BfsEngine : EngineBase {
     const uint64_t hbase0 = S.level_base.back() + S.level_size.back();
     DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
     DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
-    DSL_TRY(grow(&S.spill, &S.spill_cap, kQueueWork, false, 0));
+    DSL_TRY(grow(&S.spill, &S.spill_cap, wlimit, false, 0));
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     const int pb_max = std::max(1, std::min({(int)((DSL_ROWS_LDS_KB * 1024) / per), kLevelBlock,
                                              (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) /
@@ -361,7 +379,6 @@ struct BfsEngine : EngineBase {
     }
     // every set starts zeroed: the levels after a stop leave theirs untouched, and read zeros
     DSL_HIP(hipMemsetAsync(qctr, 0, (size_t)(kQueue + 1) * kCtrSet, stream));
-    const uint64_t flimit = W > 1 ? std::min<uint64_t>(kQueueF, rep_threshold() - 1) : kQueueF;
     const size_t lds = (size_t)pb_max * per + 16;
     for (int j = 0; j < kQueue; j++) {
       unsigned char* set = qctr + (size_t)j * kCtrSet;
@@ -372,7 +389,7 @@ struct BfsEngine : EngineBase {
       a.qprev = j ? reinterpret_cast<const LevelCounters*>(set - kCtrSet) : nullptr;
       a.qprev_seg = j ? reinterpret_cast<const unsigned long long*>(set - kCtrSet + kCtrSegOff) : nullptr;
       a.qflimit = flimit;
-      a.qwlimit = kQueueWork;
+      a.qwlimit = wlimit;
       a.qspread = spread;
       a.PB = pb_max;
       a.depth = depth + 1 + j;
@@ -395,7 +412,10 @@ struct BfsEngine : EngineBase {
       a.me = S.gid;
       a.owner_filter = 0;
       if (j == 0) DSL_HIP(hipEventRecord(qev[0], stream));
-      hipLaunchKernelGGL((k_level<P, false>), dim3(1024), dim3(kLevelBlock), lds, stream, a, prm, dset);
+      // grid: one chunk per workgroup at the predicted frontier size (the kernel loops over more)
+      const double fpred = (double)S.F * std::pow(growth, (double)j);
+      const int grid = (int)std::min<double>(kLevelGrid, std::max<double>(1024, std::ceil(1.5 * fpred / pb_max)));
+      hipLaunchKernelGGL((k_level<P, false>), dim3(grid), dim3(kLevelBlock), lds, stream, a, prm, dset);
       DSL_HIP(hipGetLastError());
     }
     DSL_HIP(hipEventRecord(qev[1], stream));
@@ -413,7 +433,7 @@ struct BfsEngine : EngineBase {
         std::memcpy(&v, set + kCtrSegOff + (size_t)q * kSegStride * 8, 8);
         F += std::min<uint64_t>(v, q_segcap);
       }
-      if (!queue_continues(c, F, flimit, kQueueWork)) {
+      if (!queue_continues(c, F, flimit, wlimit)) {
         *ran = j + 1;
         break;
       }
@@ -550,10 +570,14 @@ struct BfsEngine : EngineBase {
         }
         if (g[0] == 0) break;
 
-        if (use_queue && q_left == 0 && L == 1 && (W == 1 || rep) && sh[0].F > 0 && sh[0].F <= kQueueF &&
-            sh[0].work <= kQueueWork) {
+        if (use_queue && q_left == 0 && L == 1 && (W == 1 || rep) && sh[0].F > 0 &&
+            sh[0].F <= queue_flimit(queue_span(sh[0].F)) && sh[0].work <= 8 * queue_span(sh[0].F)) {
+          // frontier growth per level, for the queued launches' grid sizes
+          const size_t nd = per_depth.size();
+          const double growth =
+              nd >= 2 && per_depth[nd - 2] ? std::max(1.0, (double)per_depth[nd - 1] / per_depth[nd - 2]) : 3.0;
           int ran = 0;
-          DSL_TRY(enqueue_queue(depth, tbl_proto, &ran));
+          DSL_TRY(enqueue_queue(depth, tbl_proto, growth, &ran));
           q_left = ran;
           q_pos = 0;
         }
