@@ -163,10 +163,13 @@ struct BfsEngine : EngineBase {
     return s;
   }
   uint64_t queue_span(uint64_t F) const {
+    if (q_rows_forced) return q_rows_forced;  // tests: small queues that spill and stop early
     uint64_t s = kQueueRowsMin;
-    while (s < 32 * F && s < queue_span_max()) s <<= 1;
+    while ((s < 32 * F || s < q_span_hint) && s < queue_span_max()) s <<= 1;
     return s;
   }
+  uint64_t q_rows_forced = 0;  // DSL_QUEUE_ROWS (a multiple of 32)
+  uint64_t q_span_hint = 0;  // the largest span an earlier queue of this engine used (buffers exist)
   uint64_t queue_flimit(uint64_t span) const {
     return W > 1 ? std::min<uint64_t>(span / 4, rep_threshold() - 1) : span / 4;
   }
@@ -352,7 +355,10 @@ struct BfsEngine : EngineBase {
     }
     const int nseg = kSegs;
     const uint64_t span = queue_span(S.F);
+    q_span_hint = std::max(q_span_hint, span);
     q_segcap = span / nseg;
+    // levels: up to kQueue, none past max_depth (its level's successors are all pruned)
+    const int nq = hset.max_depth >= 0 ? std::max(1, std::min(kQueue, hset.max_depth - depth)) : kQueue;
     const uint64_t flimit = queue_flimit(span), wlimit = 8 * span;
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
@@ -380,7 +386,7 @@ struct BfsEngine : EngineBase {
     // every set starts zeroed: the levels after a stop leave theirs untouched, and read zeros
     DSL_HIP(hipMemsetAsync(qctr, 0, (size_t)(kQueue + 1) * kCtrSet, stream));
     const size_t lds = (size_t)pb_max * per + 16;
-    for (int j = 0; j < kQueue; j++) {
+    for (int j = 0; j < nq; j++) {
       unsigned char* set = qctr + (size_t)j * kCtrSet;
       LevelArgs<P> a{};
       a.cur = (j & 1) ? S.next : S.cur;
@@ -419,11 +425,11 @@ struct BfsEngine : EngineBase {
       DSL_HIP(hipGetLastError());
     }
     DSL_HIP(hipEventRecord(qev[1], stream));
-    DSL_HIP(hipMemcpyAsync(hq, qctr, (size_t)kQueue * kCtrSet, hipMemcpyDeviceToHost, stream));
+    DSL_HIP(hipMemcpyAsync(hq, qctr, (size_t)nq * kCtrSet, hipMemcpyDeviceToHost, stream));
     DSL_HIP(hipStreamSynchronize(stream));
     // the levels that ran: up to the first whose counters stop the queue (the device's rule)
-    *ran = kQueue;
-    for (int j = 0; j + 1 < kQueue; j++) {
+    *ran = nq;
+    for (int j = 0; j + 1 < nq; j++) {
       const unsigned char* set = hq + (size_t)j * kCtrSet;
       LevelCounters c;
       std::memcpy(&c, set, sizeof(c));
@@ -496,6 +502,7 @@ struct BfsEngine : EngineBase {
     q_left = 0;
     q_pos = 0;
     const bool use_queue = !getenv("DSL_NO_QUEUE");
+    if (const char* qr = getenv("DSL_QUEUE_ROWS")) q_rows_forced = std::max<uint64_t>(kSegs, strtoull(qr, nullptr, 10) / kSegs * kSegs);
     const bool trace_levels = getenv("DSL_LEVEL_TRACE") != nullptr;
     const Table tbl_proto{nullptr, buckets - 1, 64};
 

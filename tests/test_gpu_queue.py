@@ -1,0 +1,52 @@
+"""Queued levels (BfsEngine::enqueue_queue) against one launch per level and the golden vectors.
+
+A queue runs several levels without a host round trip and stops where the host must act: spilled
+rows, a terminal, an error, a frontier past its capacity. DSL_QUEUE_ROWS forces tiny queues so
+every stop reason is taken mid-queue; DSL_NO_QUEUE turns the queue off. Results must not move.
+"""
+import json
+import os
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import Engine
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _gold(fname, name):
+    return json.load(open(os.path.join(HERE, "golden", fname + ".json")))[name]
+
+
+CASES = [("multipaxos", "mp_c5_d8"), ("multipaxos", "mp_expect_violation"), ("multipaxos", "mp_test22_phase1"),
+         ("lab0", "lab0_2c10p_exhaustive"), ("lab0", "lab0_1c10p_goal"), ("synthetic", "synth_3n_k8_d9"),
+         ("amokv", "kv_test09_goal"), ("pb", "pb_2s1c_d15"), ("pb", "pb_2c_results_violation")]
+MODES = [{}, {"DSL_NO_QUEUE": "1"}, {"DSL_QUEUE_ROWS": "64"}, {"DSL_QUEUE_ROWS": "2048"}]
+
+
+@pytest.mark.parametrize("mode", MODES, ids=lambda m: ",".join("%s=%s" % kv for kv in m.items()) or "default")
+@pytest.mark.parametrize("fname,name", CASES)
+def test_queue_modes_match_golden(fname, name, mode, monkeypatch):
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    case = _gold(fname, name)
+    proto = argmap.protocol(case["args"])
+    s = argmap.settings(case["args"], proto)
+    e = Engine(proto)
+    try:
+        for _ in range(2):  # the second run reuses the engine's buffers and queue size
+            r = e.bfs(proto.initial_state(), s)
+            assert r.endCondition().name == case["end"]
+            assert r.per_depth == case["per_depth"]
+            assert r.states == case["states"]
+            st = r.invariantViolatingState() or r.goalMatchingState()
+            if st is not None:
+                args = [a for a in case["args"] if a != "--finish-level"]
+                rep = oracle_util.replay(args, st.trace())
+                assert rep["ok"], rep["error"]
+                assert rep["depth"] == st.depth()
+    finally:
+        e.close()
