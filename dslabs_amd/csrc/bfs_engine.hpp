@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "kernels.hpp"
+#include "replay.hpp"
 
 // LDS budget for a k_level chunk's parent rows: with the kernel's ~11 KB of static LDS, 4
 // resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
@@ -71,6 +72,7 @@ struct EngineBase {
   virtual int get_initial(uint8_t* p, size_t len) = 0;
   virtual int run(dsl_result** out) = 0;
   virtual int run_dfs(const dsl_dfs_config& c, dsl_result** out) = 0;
+  virtual int replay(const dsl_event* trace, int n, int minimize, dsl_result** out) = 0;
   virtual int state_bytes() const = 0;
   volatile unsigned long long progress_states = 0;
   volatile int progress_depth = 0;
@@ -1124,11 +1126,76 @@ struct BfsEngine : EngineBase {
         full_step<P>(s.w, (int)evs[i], n.w, prm, dset);
         s = n;
       }
+      if (!c.no_minimize) {  // RandomDFS reports the minimized trace (checkState(s, true))
+        TraceTool<P> tt(prm, dset);
+        std::vector<dsl_event> ev(r->trace, r->trace + r->trace_len);
+        typename TraceTool<P>::Step last{s, v == V_TERM_EXCEPTION};
+        tt.minimize(typename TraceTool<P>::Step{init, false}, ev, &last,
+                    tt.expected(v, hf[2], s));
+        std::memcpy(r->trace, ev.data(), ev.size() * sizeof(dsl_event));
+        r->trace_len = (int)ev.size();
+        r->terminal_depth = r->max_depth = init_depth + (int)ev.size();
+        s = last.s;
+      }
       r->terminal_state = (uint8_t*)malloc(sizeof(init));
       std::memcpy(r->terminal_state, &s, sizeof(init));
     }
     r->end_condition = end;
     r->new_states_inserted = hc[1];  // probes started
+    *out = r;
+    return DSL_OK;
+  }
+
+  // dsl_replay: TraceReplaySearch on the host (replay.hpp).
+  int replay(const dsl_event* tr, int n, int minimize, dsl_result** out) override {
+    const auto t_start = std::chrono::steady_clock::now();
+    if (!have_init) {
+      uint8_t tmp[sizeof(init)];
+      DSL_TRY(get_initial(tmp, sizeof(init)));
+    }
+    using Step = typename TraceTool<P>::Step;
+    TraceTool<P> tt(prm, dset);
+    Step cur{init, false};
+    std::vector<dsl_event> evs;
+    int pi = -1;
+    uint64_t checked = 1;
+    int v = tt.judge(cur, init_depth, &pi);  // checkState(initial, false)
+    if (v < V_TERM_EXCEPTION) {
+      for (int i = 0; i < n; i++) {
+        Step nx;
+        const int rc = tt.step(dset, cur.s, tr[i], &nx);
+        if (rc < 0) {
+          set_error("a replayed successor exceeded the packed state's bounds");
+          return DSL_ERR_STATE_OVERFLOW;
+        }
+        if (rc == 0) break;  // cannot be delivered: the replay ends (eventsExhausted)
+        cur = nx;
+        evs.push_back(tr[i]);
+        checked++;
+        v = tt.judge(cur, init_depth + (int)evs.size(), &pi);
+        if (v >= V_TERM_EXCEPTION) {
+          if (minimize) tt.minimize(Step{init, false}, evs, &cur, tt.expected(v, pi, cur.s));
+          break;
+        }
+      }
+    }
+    const bool term = v >= V_TERM_EXCEPTION;
+    dsl_result* r = (dsl_result*)calloc(1, sizeof(dsl_result));
+    r->end_condition = !term ? DSL_SPACE_EXHAUSTED
+                             : v == V_TERM_EXCEPTION ? DSL_EXCEPTION_THROWN
+                                                     : v == V_TERM_INVARIANT ? DSL_INVARIANT_VIOLATED : DSL_GOAL_FOUND;
+    r->predicate_index = term && v != V_TERM_EXCEPTION ? pi : -1;
+    r->terminal_depth = term ? init_depth + (int)evs.size() : -1;
+    r->max_depth = init_depth + (int)evs.size();
+    r->initial_depth = init_depth;
+    r->states = checked;
+    r->state_bytes = sizeof(init);
+    r->trace_len = (int)evs.size();
+    r->trace = (dsl_event*)calloc(evs.size() + 1, sizeof(dsl_event));
+    if (!evs.empty()) std::memcpy(r->trace, evs.data(), evs.size() * sizeof(dsl_event));
+    r->terminal_state = (uint8_t*)malloc(sizeof(init));
+    std::memcpy(r->terminal_state, &cur.s, sizeof(init));
+    r->elapsed_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     *out = r;
     return DSL_OK;
   }

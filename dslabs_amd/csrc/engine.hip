@@ -244,6 +244,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_SYNTHETIC: return make_engine<Synthetic>(d, cfg, out);
     case DSL_PROTO_AMOKV: return make_engine<AmoKV>(d, cfg, out);
     case DSL_PROTO_PB: return make_engine<PB>(d, cfg, out);
+    case DSL_PROTO_MINITEST: return make_engine<MiniTest>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -277,6 +278,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_SYNTHETIC: return (int)sizeof(dsl::Synthetic::State);
     case DSL_PROTO_AMOKV: return (int)sizeof(dsl::AmoKV::State);
     case DSL_PROTO_PB: return (int)sizeof(dsl::PB::State);
+    case DSL_PROTO_MINITEST: return (int)sizeof(dsl::MiniTest::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }
@@ -355,6 +357,12 @@ int dsl_run_dfs(dsl_engine* e, const dsl_dfs_config* cfg, dsl_result** out) {
   dsl_dfs_config c{};
   if (cfg) c = *cfg;
   return e->impl->run_dfs(c, out);
+}
+
+int dsl_replay(dsl_engine* e, const dsl_event* trace, int32_t n, int32_t minimize, dsl_result** out) {
+  if (!e || !out || n < 0 || (n > 0 && !trace)) return DSL_ERR_ARG;
+  *out = nullptr;
+  return e->impl->replay(trace, n, minimize, out);
 }
 
 int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth) {

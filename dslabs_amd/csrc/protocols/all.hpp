@@ -1,6 +1,7 @@
 // all.hpp -- every protocol with device transition functions.
 #pragma once
 #include "amokv.hpp"
+#include "minitest.hpp"
 #include "multipaxos.hpp"
 #include "pb.hpp"
 #include "pingpong.hpp"

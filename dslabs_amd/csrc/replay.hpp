@@ -1,0 +1,143 @@
+// replay.hpp -- trace replay and trace minimization on the host, over the same packed
+// transition functions (nodestate.hpp + protocols/) that the device kernels run.
+//
+//   TraceReplaySearch.replayTrace   T/junit/TraceReplaySearch.java:76-101
+//   TraceMinimizer.minimizeTrace    T/search/TraceMinimizer.java:32-49, stateMatches :51-61,
+//                                   minimizeExceptionCausingTrace :70-91, applyEvents :93-108
+//   SearchState.stepEvent(e, settings, skipChecks = false)  T/search/SearchState.java:275-359
+//
+// Events are identified by content (dsl_event), so a trace taken from one state can be applied
+// to another: an event is applied iff it is among the enabled events of the state it meets.
+// Exceptional successors: every handler here throws at dispatch, before changing anything, so a
+// state produced by a throwing step has its parent's content (plus the exception mark).
+#pragma once
+#include <deque>
+#include <vector>
+
+#include "nodestate.hpp"
+
+namespace dsl {
+
+inline bool same_event(const dsl_event& a, const dsl_event& b) {
+  if (a.is_timer != b.is_timer || a.from != b.from || a.to != b.to || a.type != b.type || a.n_fields != b.n_fields ||
+      a.timer_min != b.timer_min || a.timer_max != b.timer_max)
+    return false;
+  for (int i = 0; i < a.n_fields && i < DSL_MAX_EVENT_FIELDS; i++)
+    if (a.fields[i] != b.fields[i]) return false;
+  return true;
+}
+
+template <class P>
+struct TraceTool {
+  using State = typename P::State;
+  struct Step {
+    State s;
+    bool exc;  // the step that produced s threw (SearchState.thrownException)
+  };
+  // What a minimized state must keep (stateMatches): the exception, or the predicate's outcome
+  // (PV_FALSE / PV_TRUE, or PV_THREW).
+  struct Expected {
+    bool exception;
+    const DevPred* pred;
+    int outcome;
+  };
+
+  const typename P::Params& prm;
+  const DevSettings& search;  // the search's settings: delivery filters and predicates
+  DevSettings open;           // default SearchSettings (every message and timer delivered)
+
+  TraceTool(const typename P::Params& p, const DevSettings& s) : prm(p), search(s), open(s) {
+    open.all_deliver = 1;
+    for (int i = 0; i < DSL_MAX_NODES; i++) open.deliver[i] = 0xffffffffu;
+    open.timer_mask = 0xffffffffu;
+  }
+
+  // stepEvent(e, settings, skipChecks = false): 1 = stepped, 0 = null (not deliverable here),
+  // -1 = a bounded container overflowed.
+  int step(const DevSettings& st, const State& s, const dsl_event& e, Step* out) const {
+    const int n = count_events<P>(s.w, prm, st);
+    for (int k = 0; k < n; k++) {
+      dsl_event d;
+      describe_event<P>(s.w, k, prm, st, &d);
+      if (!same_event(d, e)) continue;
+      const int rc = full_step<P>(s.w, k, out->s.w, prm, st);
+      if (rc == STEP_OVERFLOW) return -1;
+      if (rc == STEP_NULL) return 0;
+      out->exc = rc == STEP_EXCEPTION;
+      if (out->exc) out->s = s;
+      return 1;
+    }
+    return 0;
+  }
+
+  int eval(const DevPred& pr, const State& s) const {
+    const NodeView v{s.w, P::kNodeWords, -1, nullptr};
+    int x = P::eval(pr, v, prm);
+    if (x != PV_THREW && pr.negate) x = !x;
+    return x;
+  }
+
+  // checkState (Search.java:162-231) of one state: Verdict and the predicate index.
+  int judge(const Step& x, int depth, int* pi) const {
+    *pi = -1;
+    if (x.exc) return V_TERM_EXCEPTION;
+    const NodeView v{x.s.w, P::kNodeWords, -1, nullptr};
+    return judge_view<P>(v, prm, search, depth, pi);
+  }
+
+  // The result the minimized trace must keep, for a terminal verdict v / predicate pi of `last`.
+  Expected expected(int v, int pi, const State& last) const {
+    if (v == V_TERM_EXCEPTION) return Expected{true, nullptr, 0};
+    const DevPred* pr = v == V_TERM_INVARIANT ? &search.inv[pi] : &search.goal[pi];
+    return Expected{false, pr, eval(*pr, last)};
+  }
+
+  bool matches(const Step& x, const Expected& e) const {
+    if (e.exception) return x.exc;
+    return eval(*e.pred, x.s) == e.outcome;
+  }
+
+  // minimizeTrace from `start` over `evs` (each applicable in turn). On return evs is the
+  // minimized trace and *last the state it reaches.
+  void minimize(const Step& start, std::vector<dsl_event>& evs, Step* last, const Expected& x) const {
+    bool shortened;
+    do {
+      shortened = false;
+      std::vector<Step> chain(1, start);  // chain[i] = state after evs[0..i)
+      for (const auto& e : evs) {
+        Step n;
+        if (step(open, chain.back().s, e, &n) != 1) break;  // cannot happen for a replayed chain
+        chain.push_back(n);
+      }
+      evs.resize(chain.size() - 1);
+      std::deque<dsl_event> kept;  // the suffix of events kept so far
+      std::vector<dsl_event> best;
+      Step best_last{};
+      for (size_t i = evs.size(); i >= 1; i--) {
+        // applyEvents(s.previous, kept): s = chain[i], s.previous = chain[i - 1]
+        Step t = chain[i - 1];
+        std::vector<dsl_event> applied;
+        for (const auto& e : kept) {
+          Step n;
+          if (step(open, t.s, e, &n) != 1) break;
+          t = n;
+          applied.push_back(e);
+        }
+        if (matches(t, x)) {
+          shortened = true;
+          best.assign(evs.begin(), evs.begin() + (i - 1));
+          best.insert(best.end(), applied.begin(), applied.end());
+          best_last = t;
+        } else {
+          kept.push_front(evs[i - 1]);
+        }
+      }
+      if (shortened) {
+        evs = best;
+        *last = best_last;
+      }
+    } while (shortened);
+  }
+};
+
+}  // namespace dsl

@@ -19,6 +19,7 @@ DSL_PROTO_SYNTHETIC = 3
 DSL_PROTO_AMOKV = 4
 DSL_PROTO_MULTIPAXOS = 5
 DSL_PROTO_PB = 6
+DSL_PROTO_MINITEST = 7
 
 
 class Protocol:
@@ -485,3 +486,37 @@ class PB(Protocol):
             name = "Forward" if t == 7 else "ForwardAck"
             body = f"{name}({m & 15}, {(m >> 4) & 7}, {(m >> 7) & 3})"
         return f"Message({a[e.from_]} -> {a[e.to]}, {body})"
+
+
+class MiniTest(Protocol):
+    """The two-node fixture of the reference's trace-minimizer tests
+    (framework/tst-self/dslabs/framework/testing/search/SearchAndTraceMinimizerTest.java:430-471):
+    servers "a" and "b", messages Foo and Bar; predicates ``foo``, ``fooException`` and
+    ``alwaysException`` (:104-126, :255-260)."""
+
+    proto_id = DSL_PROTO_MINITEST
+
+    def __init__(self):
+        self.addresses = ["a", "b"]
+
+    def params(self):
+        return []
+
+    def predicate(self, name):
+        from .search import StatePredicate
+        ids = {"foo": 700, "fooException": 701, "alwaysException": 702}
+        if name not in ids:
+            raise KeyError(name)
+        return StatePredicate(name, ids[name])
+
+    def render_event(self, e) -> str:
+        body = "Foo()" if e.type == 0 else "Bar()"
+        return f"Message({self.addresses[e.from_]} -> {self.addresses[e.to]}, {body})"
+
+    def event(self, frm: str, to: str, name: str):
+        """A dsl_event for Message(frm -> to, name()) (MessageEnvelope of the reference test)."""
+        e = _lib.dsl_event()
+        e.from_ = self.address_index(frm)
+        e.to = self.address_index(to)
+        e.type = {"Foo": 0, "Bar": 1}[name]
+        return e

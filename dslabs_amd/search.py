@@ -277,6 +277,11 @@ class SearchState:
         """Events from the search's initial state to this state (SearchState.trace())."""
         return list(self._events)
 
+    def events(self) -> list:
+        """The trace as decoded events (dsl_event copies) from the state the search started at:
+        the input of ``Engine.replay`` / ``Search.replay``."""
+        return list(self._raw_events)
+
     def addresses(self) -> List[str]:
         return list(self.protocol.addresses)
 
@@ -394,15 +399,33 @@ class Engine:
         return self._results(state, settings, res_p)
 
     def dfs(self, state: SearchState, settings: Optional[SearchSettings] = None, probes: int = 65536,
-            seed: int = 0, max_probes: int = 0) -> SearchResults:
+            seed: int = 0, max_probes: int = 0, minimize: bool = True) -> SearchResults:
         """Search.dfs / RandomDFS (Search.java:397-402, :507-583) on the device: `probes` random
-        walks at once until a terminal state, settings.maxTimeSecs, or `max_probes` probes."""
+        walks at once until a terminal state, settings.maxTimeSecs, or `max_probes` probes. The
+        terminal's trace is minimized as RandomDFS does (TraceMinimizer) unless minimize=False."""
         if settings is None:
             settings = SearchSettings()
         self._prepare(state, settings)
-        c = _lib.dsl_dfs_config(probes, seed & ((1 << 64) - 1), max_probes, 0, 0)
+        c = _lib.dsl_dfs_config(probes, seed & ((1 << 64) - 1), max_probes, 0, 0, 0 if minimize else 1, 0)
         res_p = ctypes.POINTER(_lib.dsl_result)()
         check(self.lib.dsl_run_dfs(self.handle, ctypes.byref(c), ctypes.byref(res_p)), "dsl_run_dfs")
+        return self._results(state, settings, res_p)
+
+    def replay(self, state: SearchState, settings: Optional[SearchSettings], events,
+               minimize: bool = True) -> SearchResults:
+        """TraceReplaySearch (T/junit/TraceReplaySearch.java:76-101): replays `events` (dsl_event
+        list, e.g. ``SearchState.events()`` of an earlier result from the same start state) with
+        checkState after every step; a terminal is minimized (TraceMinimizer) when `minimize`. An
+        event that cannot be delivered, or the end of the trace, ends with SPACE_EXHAUSTED."""
+        if settings is None:
+            settings = SearchSettings()
+        self._prepare(state, settings)
+        arr = (_lib.dsl_event * max(1, len(events)))()
+        for i, e in enumerate(events):
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(e), ctypes.sizeof(_lib.dsl_event))
+        res_p = ctypes.POINTER(_lib.dsl_result)()
+        check(self.lib.dsl_replay(self.handle, arr, len(events), 1 if minimize else 0, ctypes.byref(res_p)),
+              "dsl_replay")
         return self._results(state, settings, res_p)
 
     def _results(self, state: SearchState, settings: SearchSettings, res_p) -> SearchResults:
@@ -419,7 +442,7 @@ class Engine:
                 packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
                 base_events = state.trace() if state.packed is not None else []
                 terminal = SearchState(self.protocol, packed, r.terminal_depth, base_events + events,
-                                       [(e.is_timer, e.from_, e.to, e.type, tuple(e.fields[:e.n_fields])) for e in raw])
+                                       [_lib.dsl_event.from_buffer_copy(e) for e in raw])
                 if end == EndCondition.INVARIANT_VIOLATED:
                     pred = PredicateResult(settings.invariants()[r.predicate_index], False)
                 elif end == EndCondition.GOAL_FOUND:
@@ -437,6 +460,16 @@ class Search:
         eng = Engine(initialState.protocol, device=device)
         try:
             return eng.bfs(initialState, settings)
+        finally:
+            eng.close()
+
+    @staticmethod
+    def replay(initialState: SearchState, settings: Optional[SearchSettings], events, minimize: bool = True,
+               device: int = -1) -> SearchResults:
+        """TraceReplaySearch on the MI355X engine's transitions (host side, see Engine.replay)."""
+        eng = Engine(initialState.protocol, device=device)
+        try:
+            return eng.replay(initialState, settings, events, minimize)
         finally:
             eng.close()
 

@@ -71,7 +71,8 @@ typedef enum {
   DSL_PROTO_SYNTHETIC = 3,  /* table-driven synthetic protocol (BASELINE config C3) */
   DSL_PROTO_AMOKV = 4,      /* lab1 at-most-once KV client/server (BASELINE config C2) */
   DSL_PROTO_MULTIPAXOS = 5, /* lab3 Multi-Paxos (BASELINE config C5) */
-  DSL_PROTO_PB = 6          /* lab2 primary-backup + ViewServer (BASELINE config C4) */
+  DSL_PROTO_PB = 6,         /* lab2 primary-backup + ViewServer (BASELINE config C4) */
+  DSL_PROTO_MINITEST = 7    /* the two-node fixture of SearchAndTraceMinimizerTest (tst-self) */
 } dsl_protocol_id;
 
 typedef struct {
@@ -95,7 +96,10 @@ typedef enum {
   DSL_PRED_SYNTH_COUNTER_LT = 201,  /* synthetic: node word arg0 < arg1 */
   DSL_PRED_APPENDS_LINEARIZABLE = 300, /* KVStoreWorkload.APPENDS_LINEARIZABLE */
   DSL_PRED_LOGS_CONSISTENT = 400,   /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS */
-  DSL_PRED_PB_HAS_VIEW_REPLY = 500  /* PrimaryBackupTest.hasViewReply(n): arg0 = n */
+  DSL_PRED_PB_HAS_VIEW_REPLY = 500, /* PrimaryBackupTest.hasViewReply(n): arg0 = n */
+  DSL_PRED_MINI_FOO = 700,          /* SearchAndTraceMinimizerTest foo: !a.foo */
+  DSL_PRED_MINI_FOO_EXCEPTION = 701,    /* fooException: throws when a.foo, else true */
+  DSL_PRED_MINI_ALWAYS_EXCEPTION = 702  /* alwaysException: always throws */
 } dsl_predicate_id;
 
 typedef struct {
@@ -192,9 +196,23 @@ typedef struct {
   int64_t max_probes;       /* stop after this many probes were started (0 = no limit) */
   int32_t steps_per_launch; /* 0 = 64 */
   int32_t max_trace;        /* events recorded per probe when maxDepth is unbounded (0 = 4096) */
+  int32_t no_minimize;      /* 0: the terminal's trace is minimized, as RandomDFS does
+                               (checkState(s, true), Search.java:570); 1: the probe's raw trace */
+  int32_t reserved;
 } dsl_dfs_config;
 
 int dsl_run_dfs(dsl_engine* e, const dsl_dfs_config* cfg, dsl_result** out);
+
+/* Trace replay (TraceReplaySearch.replayTrace, T/junit/TraceReplaySearch.java:76-101): steps
+ * `trace` from the initial state under the settings -- every event must be deliverable in the
+ * state it is applied to (stepEvent with skipChecks = false, SearchState.java:282-359) -- and runs
+ * checkState after each step. The first TERMINAL state ends the replay; with `minimize` its trace
+ * is minimized (TraceMinimizer.minimizeTrace / minimizeExceptionCausingTrace,
+ * T/search/TraceMinimizer.java:32-108) while the reported predicate stays the one that fired. An
+ * event that cannot be delivered, or the end of the trace, gives SPACE_EXHAUSTED with the last
+ * state reached. Events are matched by content (dsl_event fields, reserved ignored). Runs on the
+ * host over the same packed transition functions as the device kernels. */
+int dsl_replay(dsl_engine* e, const dsl_event* trace, int32_t n, int32_t minimize, dsl_result** out);
 /* Cumulative kernel statistics of the last dsl_run (HIP events on the engine's stream). The
  * byte model of the expand kernel: parents read once (S bytes each), one 64-byte
  * visited-table bucket line per successor probe, one bucket line written back + 12 bytes of

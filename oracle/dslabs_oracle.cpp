@@ -5,6 +5,7 @@
 //   dslabs_oracle bfs --proto pingpong --clients 1 --pings 10 --inv RESULTS_OK --prune CLIENTS_DONE
 //   dslabs_oracle bfs --proto sipaxos --proposers 2 --acceptors 3 --values a,b --max-depth 9
 //   dslabs_oracle replay --proto pingpong ... --trace-file events.txt
+//   dslabs_oracle replaysearch --proto minitest --inv foo --trace-file events.txt [--minimize]
 //   dslabs_oracle timerqueue        (TimerQueueTest.randomTimers truth table)
 //
 // Options common to bfs/replay:
@@ -17,6 +18,7 @@
 
 #include "oracle_core.hpp"
 #include "proto_amokv.hpp"
+#include "proto_minitest.hpp"
 #include "proto_multipaxos.hpp"
 #include "proto_pb.hpp"
 #include "proto_pingpong.hpp"
@@ -159,6 +161,14 @@ static Scenario build(const Args& a) {
         auto parts = split(n, ':');
         return synthetic::counterLt(std::stoi(parts[1]), std::stoi(parts[2]));
       }
+      throw std::runtime_error("unknown predicate " + n);
+    };
+  } else if (a.proto == "minitest") {
+    sc.init = minitest::initial(sc.names);
+    sc.pred = [](const std::string& n) -> Predicate {
+      if (n == "foo") return minitest::foo();
+      if (n == "fooException") return minitest::fooException();
+      if (n == "alwaysException") return minitest::alwaysException();
       throw std::runtime_error("unknown predicate " + n);
     };
   } else {
@@ -410,6 +420,57 @@ static int runReplay(const Args& a) {
   return 0;
 }
 
+// Trace-replay search (TraceReplaySearch.java:76-101 / ReplaySearch): replays the trace's events
+// with checkState after every step; --minimize runs TraceMinimizer on a terminal
+// (Search.checkState(s, true)). An event string names a message in the network or a queued timer;
+// one that names neither, or cannot be delivered, ends the replay (SPACE_EXHAUSTED).
+static int runReplaySearch(const Args& a) {
+  Scenario sc = build(a);
+  Settings st = settingsFrom(a, sc);
+  std::shared_ptr<const State> s0 = replayStart(a, sc);
+  std::vector<std::string> lines;
+  {
+    std::ifstream in(a.get("trace-file"));
+    std::string line;
+    while (std::getline(in, line))
+      if (!line.empty()) lines.push_back(line);
+  }
+  // events are resolved against the state each one is applied to, on an unfiltered replay
+  std::vector<Event> evs;
+  std::shared_ptr<const State> s = s0;
+  for (auto& line : lines) {
+    std::optional<Event> found;
+    for (auto& m : s->network) {
+      Event e;
+      e.msg = m;
+      if (eventStr(e, sc.names) == line) found = e;
+    }
+    for (size_t n = 0; n < s->timers.size() && !found; n++)
+      for (auto& t : s->timers[n].timers) {
+        Event e;
+        e.isTimer = true;
+        e.timer = t;
+        if (eventStr(e, sc.names) == line) found = e;
+      }
+    if (!found) break;
+    evs.push_back(*found);
+    auto n = stepChecked(s, *found, nullptr);
+    if (!n) break;
+    s = n;
+  }
+  ReplayOutcome R = replaySearch(s0, st, evs, a.has("minimize"));
+  std::cout << "{\"end\":\"" << endName(R.end) << "\",\"depth\":" << R.state->depth << ",\"predicate_index\":"
+            << R.predIndex << ",\"predicate\":\"" << jsonEsc(R.predicate) << "\",\"trace\":[";
+  bool first = true;
+  for (auto& x : trace(R.state)) {
+    if (!x->previousEvent || x->depth <= s0->depth) continue;
+    std::cout << (first ? "" : ",") << "\"" << jsonEsc(eventStr(*x->previousEvent, sc.names)) << "\"";
+    first = false;
+  }
+  std::cout << "],\"state\":\"" << jsonEsc(R.state->key()) << "\"}" << std::endl;
+  return 0;
+}
+
 // TimerQueueTest.randomTimers (framework/tst-self/.../search/TimerQueueTest.java:153-175) as a
 // truth table: for te1=(i,j), te2=(k,l) added in order, is te2 deliverable?
 static int runTimerQueue() {
@@ -457,6 +518,7 @@ int main(int argc, char** argv) {
   try {
     if (a.mode == "bfs") return runBfs(a);
     if (a.mode == "replay") return runReplay(a);
+    if (a.mode == "replaysearch") return runReplaySearch(a);
     if (a.mode == "vstest") return runVsTest(a);
     if (a.mode == "timerqueue") return runTimerQueue();
   } catch (const std::exception& e) {

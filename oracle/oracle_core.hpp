@@ -605,6 +605,131 @@ inline std::vector<std::shared_ptr<const State>> trace(std::shared_ptr<const Sta
   return t;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Trace minimization (TraceMinimizer.java:32-108) and trace-replay search
+// (TraceReplaySearch.java:76-101, ReplaySearch in SearchAndTraceMinimizerTest.java:520-548, with
+// Search.checkState(s, shouldMinimize), Search.java:162-231).
+// ---------------------------------------------------------------------------------------------
+// stepEvent(e, settings, skipChecks=false) (SearchState.java:282-303, :316-359): the message must
+// be in the network and pass shouldDeliver / the timer must pass canStepTimer, else null.
+// settings == nullptr: default SearchSettings (everything delivered), as TraceMinimizer uses.
+inline std::shared_ptr<State> stepChecked(const std::shared_ptr<const State>& s, const Event& ev, const Settings* st) {
+  if (ev.isTimer) {
+    const int to = ev.timer.to;
+    if (to < 0 || to >= (int)s->nodes.size()) return nullptr;
+    if ((st && !st->deliverTimers(to)) || !s->timers[to].isDeliverable(ev.timer)) return nullptr;
+  } else {
+    if (ev.msg.to < 0 || ev.msg.to >= (int)s->nodes.size()) return nullptr;
+    if (!s->network.count(ev.msg) || (st && !st->shouldDeliver(ev.msg))) return nullptr;
+  }
+  return stepEvent(s, ev);
+}
+
+// The result a minimized state must keep (TraceMinimizer.stateMatches :51-61): the same
+// exception class (minimizeExceptionCausingTrace :70-91; every handler exception here is one
+// class), or the predicate with the same value / again throwing.
+struct Expected {
+  bool exception = false;
+  const Predicate* pred = nullptr;
+  bool threw = false, value = false;
+};
+
+inline bool stateMatches(const State* s, const Expected& x) {
+  if (!s) return false;
+  if (x.exception) return s->exception;
+  PredResult r = x.pred->test(*s);
+  if (x.threw) return r.threw;
+  return !r.threw && r.value == x.value;
+}
+
+// applyEvents (:93-108): steps until an event cannot be applied; returns the last state reached.
+inline std::shared_ptr<const State> applyEvents(std::shared_ptr<const State> s, const std::deque<Event>& events) {
+  for (auto& e : events) {
+    auto n = stepChecked(s, e, nullptr);
+    if (!n) break;
+    s = n;
+  }
+  return s;
+}
+
+// minimizeTrace (:32-49): walking back from the end, drop an event when replaying the kept
+// suffix from its predecessor still matches; repeat until a pass drops nothing.
+inline std::shared_ptr<const State> minimizeTrace(std::shared_ptr<const State> state, const Expected& x) {
+  bool shortened;
+  do {
+    shortened = false;
+    std::deque<Event> events;
+    for (auto s = state; s->previous; s = s->previous) {
+      auto test = applyEvents(s->previous, events);
+      if (stateMatches(test.get(), x)) {
+        shortened = true;
+        state = test;
+      } else {
+        events.push_front(*s->previousEvent);
+      }
+    }
+  } while (shortened);
+  return state;
+}
+
+struct ReplayOutcome {
+  End end = End::SPACE_EXHAUSTED;
+  std::shared_ptr<const State> state;  // terminal (possibly minimized) or the last state reached
+  int predIndex = -1;
+  std::string predicate;
+};
+
+// Replays events from init with checkState after every step; a terminal is minimized when
+// `minimize` (TraceReplaySearch passes true; ReplaySearch passes its flag). An event that cannot
+// be delivered ends the replay with SPACE_EXHAUSTED (eventsExhausted). PRUNED states do not stop
+// it (TraceReplaySearch only asserts they do not occur).
+inline ReplayOutcome replaySearch(std::shared_ptr<const State> init, const Settings& st, const std::vector<Event>& evs,
+                                  bool minimize) {
+  ReplayOutcome out;
+  auto check = [&](std::shared_ptr<const State> s, bool mini) -> bool {
+    if (s->exception) {
+      Expected x;
+      x.exception = true;
+      out.end = End::EXCEPTION_THROWN;
+      out.state = mini ? minimizeTrace(s, x) : s;
+      return true;
+    }
+    for (size_t i = 0; i < st.invariants.size(); i++) {
+      PredResult r = st.invariants[i].test(*s);
+      if (r.threw || !r.value) {
+        Expected x{false, &st.invariants[i], r.threw, r.value};
+        out.end = End::INVARIANT_VIOLATED;
+        out.predIndex = (int)i;
+        out.predicate = st.invariants[i].name;
+        out.state = mini ? minimizeTrace(s, x) : s;
+        return true;
+      }
+    }
+    for (size_t i = 0; i < st.goals.size(); i++) {
+      PredResult r = st.goals[i].test(*s);
+      if (r.threw || !r.value) continue;
+      Expected x{false, &st.goals[i], false, true};
+      out.end = End::GOAL_FOUND;
+      out.predIndex = (int)i;
+      out.predicate = st.goals[i].name;
+      out.state = mini ? minimizeTrace(s, x) : s;
+      return true;
+    }
+    return false;
+  };
+  std::shared_ptr<const State> s = init;
+  if (check(s, false)) return out;  // the initial state has no trace to minimize
+  for (auto& e : evs) {
+    auto n = stepChecked(s, e, &st);
+    if (!n) break;
+    s = n;
+    if (check(s, minimize)) return out;
+  }
+  out.end = End::SPACE_EXHAUSTED;
+  out.state = s;
+  return out;
+}
+
 // Standard predicates (StatePredicate.java:52-83).
 inline Predicate RESULTS_OK(const Names& n) {
   return {"Clients got expected results", [n](const State& s) {

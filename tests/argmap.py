@@ -1,7 +1,7 @@
 """Maps oracle CLI arguments (tests/golden/*.json "args") onto the engine's Python API, so each
 committed oracle fixture is replayed on the GPU with the same meaning."""
 from dslabs_amd import CLIENTS_DONE, NONE_DECIDED, RESULTS_OK, SearchSettings, clientDone
-from dslabs_amd.protocols import PB, AmoKV, MultiPaxos, PingPong, SIPaxos, Synthetic
+from dslabs_amd.protocols import PB, AmoKV, MiniTest, MultiPaxos, PingPong, SIPaxos, Synthetic
 
 
 def _opt(args, name, default=None):
@@ -27,6 +27,8 @@ def protocol(args):
     if p == "synthetic":
         return Synthetic(int(_opt(args, "--nodes", 5)), int(_opt(args, "--values", 64)), int(_opt(args, "--poke-mod", 7)),
                          int(_opt(args, "--seed", str(Synthetic.SEED)), 0))
+    if p == "minitest":
+        return MiniTest()
     raise ValueError(p)
 
 

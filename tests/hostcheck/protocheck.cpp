@@ -266,6 +266,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, set);
     case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
     case DSL_PROTO_PB: return run<PB>(d, set);
+    case DSL_PROTO_MINITEST: return run<MiniTest>(d, set);
   }
   return 2;
 }

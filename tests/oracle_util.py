@@ -30,3 +30,15 @@ def replay(args, events, timeout: float = 60) -> dict:
         return run("replay", list(args) + ["--trace-file", path], timeout=timeout)
     finally:
         os.unlink(path)
+
+
+def replay_search(args, events, minimize: bool, timeout: float = 60) -> dict:
+    """TraceReplaySearch on the oracle (checkState per step, TraceMinimizer when `minimize`)."""
+    with tempfile.NamedTemporaryFile("w", suffix=".trace", delete=False) as f:
+        f.write("\n".join(events) + "\n")
+        path = f.name
+    try:
+        return run("replaysearch", list(args) + ["--trace-file", path] + (["--minimize"] if minimize else []),
+                   timeout=timeout)
+    finally:
+        os.unlink(path)

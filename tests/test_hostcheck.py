@@ -82,6 +82,9 @@ CASES = {
     "kv_putappendget": ([4, 1, 3, 1, 0, 0, 3, 2, 0, 1, 264, 0, 0, 0, 265, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, -1],
                         ["--proto", "amokv", "--clients", "1", "--workload", "putappendget", "--inv", "RESULTS_OK",
                          "--prune", "CLIENTS_DONE"]),
+    # the minimizer fixture of SearchAndTraceMinimizerTest (no parameters)
+    "mini_inv_foo": ([7, "--", 700, "/", "/", -1], ["--proto", "minitest", "--inv", "foo", "--finish-level"]),
+    "mini_goal_notfoo": ([7, "--", "/", -700, "/", -1], ["--proto", "minitest", "--goal", "!foo", "--finish-level"]),
     # lab2 PB + ViewServer (C4): params from dslabs_amd.protocols.PB(servers, clients, workload)
     "pb_2s1c_d14": ([6, 2, 1, 2, 1, 0, 0, 3, 0, 0, 0, 5, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, 0, 0, 0, -1, "--", 1, "/", "/", 2, "500:4", 14],
                     ["--proto", "pb", "--servers", "2", "--clients", "1", "--workload", "putget", "--inv", "RESULTS_OK",

@@ -107,3 +107,27 @@ def test_viewserver_passes_reference_unit_tests():
     names = [x["name"] for x in r["results"]]
     assert len(names) == 12 and names[0] == "test01StartupViewCorrect"
     assert all(x["ok"] for x in r["results"]), [x for x in r["results"] if not x["ok"]]
+
+
+# SearchAndTraceMinimizerTest (framework/tst-self/dslabs/framework/testing/search/
+# SearchAndTraceMinimizerTest.java): the reference's known answers for trace minimization.
+MINI_TRACE = ["Message(a -> b, Foo())", "Message(a -> b, Foo())", "Message(b -> a, Bar())"]
+MINI_TRACE2 = ["Message(a -> b, Foo())", "Message(a -> b, Foo())", "Message(b -> a, Foo())"]
+MINI_CASES = [  # (name, settings args, trace, end, depth minimized, depth not minimized)
+    ("testSearchMinimizesInvariantViolation", ["--inv", "foo"], MINI_TRACE, "INVARIANT_VIOLATED", 2, 3),
+    ("testSearchMinimizesExceptionThrown", ["--inv", "foo"], MINI_TRACE2, "EXCEPTION_THROWN", 2, 3),
+    ("testSearchMinimizesExceptionalPredicate", ["--inv", "fooException"], MINI_TRACE, "INVARIANT_VIOLATED", 2, 3),
+    ("goalMinimization", ["--goal", "!foo"], MINI_TRACE, "GOAL_FOUND", 2, 3),
+    ("exceptionsInGoal", ["--goal", "alwaysException"], MINI_TRACE, "SPACE_EXHAUSTED", 3, 3),
+]
+
+
+@pytest.mark.parametrize("case", MINI_CASES, ids=[c[0] for c in MINI_CASES])
+def test_oracle_minimizer_reference_cases(case):
+    _, sargs, trace, end, dmin, draw = case
+    args = ["--proto", "minitest"] + sargs
+    for minimize, depth in ((True, dmin), (False, draw)):
+        r = oracle_util.replay_search(args, trace, minimize)
+        assert r["end"] == end
+        assert r["depth"] == depth
+        assert len(r["trace"]) == depth
