@@ -118,10 +118,11 @@ def cpu_baseline(oracle_args, depth: int) -> dict:
                       f"oracle/dslabs_oracle single-threaded)"}
 
 
-def pmc_traffic(workload: str, depth: int):
+def pmc_traffic(workload: str, depth: int, launches: int):
     """HBM bytes per k_level launch from the committed rocprofv3 PMC summary of the same
     workload (tools/gpu_prof.sh + tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950 16-B/lane
-    correction) + WRITE_SIZE, separate --pmc passes), or None if this workload has none."""
+    correction) + WRITE_SIZE, separate --pmc passes over one search), divided by this run's
+    launches per search; None if this workload has no summary."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_d{depth}.json"))):
@@ -129,6 +130,8 @@ def pmc_traffic(workload: str, depth: int):
     if best is None:
         return None, None
     d = json.load(open(best))
+    if d.get("hbm_bytes_per_step"):
+        return int(d["hbm_bytes_per_step"] / max(1, launches)), os.path.relpath(best, ROOT)
     v = d.get("hbm_bytes_per_launch")
     return (int(v) if v else None), os.path.relpath(best, ROOT)
 
@@ -143,7 +146,7 @@ def roofline(stats: dict, workload: str, depth: int) -> dict:
     t = stats["expand_ms"] / 1e3
     achieved = alg / t / 1e9 if t > 0 else 0.0
     launches = max(1, stats["expand_launches"])
-    traffic, src = pmc_traffic(workload, depth)
+    traffic, src = pmc_traffic(workload, depth, launches)
     out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
            "kernel": "k_level", "launches": stats["expand_launches"],

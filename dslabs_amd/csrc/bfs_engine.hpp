@@ -427,6 +427,7 @@ struct BfsEngine : EngineBase {
       DSL_HIP(hipGetLastError());
     }
     DSL_HIP(hipEventRecord(qev[1], stream));
+    stats.expand_launches += nq;  // every dispatch, also those after the stop (they return at once)
     DSL_HIP(hipMemcpyAsync(hq, qctr, (size_t)nq * kCtrSet, hipMemcpyDeviceToHost, stream));
     DSL_HIP(hipStreamSynchronize(stream));
     // the levels that ran: up to the first whose counters stop the queue (the device's rule)
@@ -812,12 +813,12 @@ struct BfsEngine : EngineBase {
           DSL_HIP(hipStreamSynchronize(stream));
           for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
         }
-        if (!queued || q_pos == 0) {  // a queue is timed as a whole, with its launches counted
+        if (!queued || q_pos == 0) {  // a queue is timed as a whole (its dispatches counted there)
           float kms = 0;
           (void)hipEventElapsedTime(&kms, queued ? qev[0] : ev0, queued ? qev[1] : ev1);
           stats.expand_ms += kms;
         }
-        stats.expand_launches++;
+        if (!queued) stats.expand_launches++;
 #ifdef DSL_PHASES
         for (auto& S : sh) {
           const auto& q = S.lc.phase;

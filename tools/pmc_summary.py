@@ -54,6 +54,10 @@ def main(d):
         out["write_bytes_per_launch"] = write / n
         # gfx950: FETCH_SIZE counts half the bytes of 16-B/lane reads (the staging and bucket loads)
         out["hbm_bytes_per_launch"] = (2 * fetch + write) / n
+        # the PMC passes run one search (bench.py --steps 1 --warmup 0): totals are per step, and
+        # bench.py divides them by its own launches per step (queued levels that stopped early are
+        # dispatched but do no work)
+        out["hbm_bytes_per_step"] = 2 * fetch + write
         if "SQ_WAVE_CYCLES" in tot and tot.get("SQ_WAVE_CYCLES"):
             out["wait_frac"] = tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in tot else None
     json.dump(out, sys.stdout, indent=1)
