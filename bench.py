@@ -118,11 +118,14 @@ def cpu_baseline(oracle_args, depth: int) -> dict:
                       f"oracle/dslabs_oracle single-threaded)"}
 
 
-def pmc_traffic(workload: str, depth: int, launches: int):
+def pmc_traffic(workload: str, depth: int, launches: int, staged_bytes: int = 0):
     """HBM bytes per k_level launch from the committed rocprofv3 PMC summary of the same
-    workload (tools/gpu_prof.sh + tools/pmc_summary.py: FETCH_SIZE x 2 (gfx950 16-B/lane
-    correction) + WRITE_SIZE, separate --pmc passes over one search), divided by this run's
-    launches per search; None if this workload has no summary."""
+    workload (tools/gpu_prof.sh + tools/pmc_summary.py, separate --pmc passes over one search),
+    divided by this run's launches per search; None if this workload has no summary.
+    Calibrated on gfx950 with tools/hbm_calib.hip (profiles/r01_hbm_calibration.json):
+    FETCH_SIZE counts the random 64-B bucket-line reads exactly but only half of the 16-B/lane
+    streaming reads, i.e. the staging of the frontier rows and fingerprints (`staged_bytes` per
+    search), so traffic = FETCH_SIZE + staged_bytes / 2 + WRITE_SIZE."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_d{depth}.json"))):
@@ -130,6 +133,9 @@ def pmc_traffic(workload: str, depth: int, launches: int):
     if best is None:
         return None, None
     d = json.load(open(best))
+    if d.get("fetch_bytes_per_step") is not None and d.get("write_bytes_per_step") is not None:
+        t = d["fetch_bytes_per_step"] + staged_bytes / 2 + d["write_bytes_per_step"]
+        return int(t / max(1, launches)), os.path.relpath(best, ROOT)
     if d.get("hbm_bytes_per_step"):
         return int(d["hbm_bytes_per_step"] / max(1, launches)), os.path.relpath(best, ROOT)
     v = d.get("hbm_bytes_per_launch")
@@ -146,7 +152,7 @@ def roofline(stats: dict, workload: str, depth: int) -> dict:
     t = stats["expand_ms"] / 1e3
     achieved = alg / t / 1e9 if t > 0 else 0.0
     launches = max(1, stats["expand_launches"])
-    traffic, src = pmc_traffic(workload, depth, launches)
+    traffic, src = pmc_traffic(workload, depth, launches, stats["parents"] * (S + 16))
     out = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
            "kernel": "k_level", "launches": stats["expand_launches"],

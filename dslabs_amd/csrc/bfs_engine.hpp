@@ -521,17 +521,25 @@ struct BfsEngine : EngineBase {
     // level pays only once it has enough work.
     bool rep_active = W > 1 && rep_threshold() > 0;
     bool first_sharded = W > 1 && !rep_active;
+    // checkState of the initial state: the same judge, on the host (no round trip before the
+    // first level); k_seed only inserts its fingerprint
+    {
+      int pi = -1;
+      const NodeView v0{init.w, P::kNodeWords, -1, nullptr};
+      const int v = judge_view<P>(v0, prm, dset, init_depth, &pi);
+      init_enc = ((uint64_t)v << 32) | (uint32_t)(pi + 1);
+    }
     for (auto& S : sh) {
       if (S.gid != init_owner && !rep_active) continue;
-      DSL_HIP(hipMemcpyAsync(S.cur, init.w, NW * 4, hipMemcpyHostToDevice, stream));
-      DSL_HIP(hipMemcpyAsync(S.cur_fp, &init_fp, sizeof(Fp), hipMemcpyHostToDevice, stream));
+      // staged through the pinned counter buffer: a pageable source would make the copies synchronous
+      static_assert(sizeof(init) + sizeof(Fp) <= (size_t)kCtrSet, "initial state larger than the staging buffer");
+      std::memcpy(S.hctr, init.w, NW * 4);
+      std::memcpy(S.hctr + NW * 4, &init_fp, sizeof(Fp));
+      DSL_HIP(hipMemcpyAsync(S.cur, S.hctr, NW * 4, hipMemcpyHostToDevice, stream));
+      DSL_HIP(hipMemcpyAsync(S.cur_fp, S.hctr + NW * 4, sizeof(Fp), hipMemcpyHostToDevice, stream));
       Table t = tbl_proto;
       t.slots = S.table;
       hipLaunchKernelGGL(k_seed<P>, dim3(1), dim3(64), 0, stream, S.cur, S.cur_fp, prm, dset, t, init_depth, S.seed);
-      int32_t seed[4];
-      DSL_HIP(hipMemcpyAsync(seed, S.seed, sizeof(seed), hipMemcpyDeviceToHost, stream));
-      DSL_HIP(hipStreamSynchronize(stream));
-      init_enc = ((uint64_t)seed[0] << 32) | (uint32_t)(seed[1] + 1);
       S.F = 1;
       S.seg_base.assign(1, 0);
       S.seg_cnt.assign(1, 1);

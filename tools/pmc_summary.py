@@ -58,6 +58,11 @@ def main(d):
         # bench.py divides them by its own launches per step (queued levels that stopped early are
         # dispatched but do no work)
         out["hbm_bytes_per_step"] = 2 * fetch + write
+        # raw per-search counters: bench.py applies the calibrated correction
+        # (profiles/r01_hbm_calibration.json: FETCH_SIZE is exact for the random 64-B bucket lines
+        # and half of the 16-B/lane streaming staging reads; WRITE_SIZE is exact)
+        out["fetch_bytes_per_step"] = fetch
+        out["write_bytes_per_step"] = write
         if "SQ_WAVE_CYCLES" in tot and tot.get("SQ_WAVE_CYCLES"):
             out["wait_frac"] = tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in tot else None
     json.dump(out, sys.stdout, indent=1)
