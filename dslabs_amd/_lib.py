@@ -32,7 +32,7 @@ EXPORTED = [
     "dsl_abi_version", "dsl_device_count", "dsl_state_bytes", "dsl_comm_unique_id", "dsl_create",
     "dsl_set_settings", "dsl_set_initial", "dsl_get_initial", "dsl_run", "dsl_progress",
     "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
-    "dsl_run_dfs", "dsl_replay",
+    "dsl_run_dfs", "dsl_replay", "dsl_human_readable_trace",
 ]
 
 
@@ -128,6 +128,7 @@ def load() -> ctypes.CDLL:
     lib.dsl_run.argtypes = [ctypes.c_void_p, P(P(dsl_result))]
     lib.dsl_run_dfs.argtypes = [ctypes.c_void_p, P(dsl_dfs_config), P(P(dsl_result))]
     lib.dsl_replay.argtypes = [ctypes.c_void_p, P(dsl_event), ctypes.c_int32, ctypes.c_int32, P(P(dsl_result))]
+    lib.dsl_human_readable_trace.argtypes = [ctypes.c_void_p, P(dsl_event), ctypes.c_int32, P(P(dsl_result))]
     lib.dsl_progress.argtypes = [ctypes.c_void_p, P(ctypes.c_uint64), P(ctypes.c_int32)]
     lib.dsl_kernel_stats.argtypes = [ctypes.c_void_p, P(dsl_stats)]
     lib.dsl_create_with_host_comm.argtypes = [P(dsl_protocol_desc), P(dsl_engine_config), ctypes.c_void_p,

@@ -73,6 +73,7 @@ struct EngineBase {
   virtual int run(dsl_result** out) = 0;
   virtual int run_dfs(const dsl_dfs_config& c, dsl_result** out) = 0;
   virtual int replay(const dsl_event* trace, int n, int minimize, dsl_result** out) = 0;
+  virtual int human_readable(const dsl_event* trace, int n, dsl_result** out) = 0;
   virtual int state_bytes() const = 0;
   volatile unsigned long long progress_states = 0;
   volatile int progress_depth = 0;
@@ -1151,6 +1152,43 @@ struct BfsEngine : EngineBase {
     }
     r->end_condition = end;
     r->new_states_inserted = hc[1];  // probes started
+    *out = r;
+    return DSL_OK;
+  }
+
+  // dsl_human_readable_trace: SearchState.humanReadableTrace on the host (replay.hpp).
+  int human_readable(const dsl_event* tr, int n, dsl_result** out) override {
+    if (!have_init) {
+      uint8_t tmp[sizeof(init)];
+      DSL_TRY(get_initial(tmp, sizeof(init)));
+    }
+    TraceTool<P> tt(prm, dset);
+    std::vector<dsl_event> evs(tr, tr + n);
+    typename P::State last = init;
+    {  // the end state of the trace as given (kept if the reordering cannot be replayed)
+      typename TraceTool<P>::Step cur{init, false};
+      for (const auto& e : evs) {
+        typename TraceTool<P>::Step nx;
+        if (tt.step(tt.open, cur.s, e, &nx) != 1) {
+          set_error("the trace does not apply to the initial state");
+          return DSL_ERR_ARG;
+        }
+        cur = nx;
+      }
+      last = cur.s;
+    }
+    tt.human_readable(init, evs, &last);
+    dsl_result* r = (dsl_result*)calloc(1, sizeof(dsl_result));
+    r->end_condition = DSL_SPACE_EXHAUSTED;
+    r->predicate_index = -1;
+    r->terminal_depth = r->max_depth = init_depth + (int)evs.size();
+    r->initial_depth = init_depth;
+    r->state_bytes = sizeof(init);
+    r->trace_len = (int)evs.size();
+    r->trace = (dsl_event*)calloc(evs.size() + 1, sizeof(dsl_event));
+    if (!evs.empty()) std::memcpy(r->trace, evs.data(), evs.size() * sizeof(dsl_event));
+    r->terminal_state = (uint8_t*)malloc(sizeof(init));
+    std::memcpy(r->terminal_state, &last, sizeof(init));
     *out = r;
     return DSL_OK;
   }

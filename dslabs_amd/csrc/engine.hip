@@ -365,6 +365,12 @@ int dsl_replay(dsl_engine* e, const dsl_event* trace, int32_t n, int32_t minimiz
   return e->impl->replay(trace, n, minimize, out);
 }
 
+int dsl_human_readable_trace(dsl_engine* e, const dsl_event* trace, int32_t n, dsl_result** out) {
+  if (!e || !out || n < 0 || (n > 0 && !trace)) return DSL_ERR_ARG;
+  *out = nullptr;
+  return e->impl->human_readable(trace, n, out);
+}
+
 int dsl_progress(dsl_engine* e, uint64_t* states, int32_t* depth) {
   if (!e) return DSL_ERR_ARG;
   if (states) *states = e->impl->progress_states;

@@ -428,6 +428,27 @@ class Engine:
               "dsl_replay")
         return self._results(state, settings, res_p)
 
+    def human_readable_trace(self, state: SearchState, settings: Optional[SearchSettings], events) -> SearchState:
+        """SearchState.humanReadableTraceEndState (SearchState.java:373-470): the state reached by
+        `events` from `state`, whose trace() is the causally reordered, no-op-free trace."""
+        if settings is None:
+            settings = SearchSettings()
+        self._prepare(state, settings)
+        arr = (_lib.dsl_event * max(1, len(events)))()
+        for i, e in enumerate(events):
+            ctypes.memmove(ctypes.byref(arr[i]), ctypes.byref(e), ctypes.sizeof(_lib.dsl_event))
+        res_p = ctypes.POINTER(_lib.dsl_result)()
+        check(self.lib.dsl_human_readable_trace(self.handle, arr, len(events), ctypes.byref(res_p)),
+              "dsl_human_readable_trace")
+        try:
+            r = res_p.contents
+            raw = [r.trace[i] for i in range(r.trace_len)]
+            packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
+            return SearchState(self.protocol, packed, r.terminal_depth, [self.protocol.render_event(e) for e in raw],
+                               [_lib.dsl_event.from_buffer_copy(e) for e in raw])
+        finally:
+            self.lib.dsl_result_free(res_p)
+
     def _results(self, state: SearchState, settings: SearchSettings, res_p) -> SearchResults:
         lib = self.lib
         try:

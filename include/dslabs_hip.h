@@ -213,6 +213,14 @@ int dsl_run_dfs(dsl_engine* e, const dsl_dfs_config* cfg, dsl_result** out);
  * state reached. Events are matched by content (dsl_event fields, reserved ignored). Runs on the
  * host over the same packed transition functions as the device kernels. */
 int dsl_replay(dsl_engine* e, const dsl_event* trace, int32_t n, int32_t minimize, dsl_result** out);
+
+/* SearchState.humanReadableTrace (T/search/SearchState.java:373-470): the events of `trace` (from
+ * the initial state) reordered along their causal graph -- a message's first sender before its
+ * delivery, each node's steps in order -- depth-first, replayed without delivery checks, steps
+ * that leave the state unchanged dropped. Where the reference iterates a HashSet (unspecified
+ * order), ready successors are taken in trace order. out->trace is the new trace, terminal_state
+ * its end state (equal to the original end state); end_condition is SPACE_EXHAUSTED. Host side. */
+int dsl_human_readable_trace(dsl_engine* e, const dsl_event* trace, int32_t n, dsl_result** out);
 /* Cumulative kernel statistics of the last dsl_run (HIP events on the engine's stream). The
  * byte model of the expand kernel: parents read once (S bytes each), one 64-byte
  * visited-table bucket line per successor probe, one bucket line written back + 12 bytes of

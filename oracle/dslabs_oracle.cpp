@@ -6,6 +6,7 @@
 //   dslabs_oracle bfs --proto sipaxos --proposers 2 --acceptors 3 --values a,b --max-depth 9
 //   dslabs_oracle replay --proto pingpong ... --trace-file events.txt
 //   dslabs_oracle replaysearch --proto minitest --inv foo --trace-file events.txt [--minimize]
+//                [--human-readable]   (the reported state's trace reordered, SearchState.humanReadableTrace)
 //   dslabs_oracle timerqueue        (TimerQueueTest.randomTimers truth table)
 //
 // Options common to bfs/replay:
@@ -459,6 +460,7 @@ static int runReplaySearch(const Args& a) {
     s = n;
   }
   ReplayOutcome R = replaySearch(s0, st, evs, a.has("minimize"));
+  if (a.has("human-readable")) R.state = humanReadableTrace(R.state);
   std::cout << "{\"end\":\"" << endName(R.end) << "\",\"depth\":" << R.state->depth << ",\"predicate_index\":"
             << R.predIndex << ",\"predicate\":\"" << jsonEsc(R.predicate) << "\",\"trace\":[";
   bool first = true;

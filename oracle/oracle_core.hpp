@@ -291,6 +291,7 @@ struct State {
   uint64_t exceptionId = 0;  // Throwable identity: exceptional states never merge
   std::shared_ptr<const State> previous;
   std::optional<Event> previousEvent;
+  std::vector<Envelope> newMessages;  // every send of the step that made this state (SearchState.newMessages)
 
   const ClientWorker* cw(int a) const { return dynamic_cast<const ClientWorker*>(nodes[a].get()); }
   std::vector<int> clientWorkers() const {
@@ -299,8 +300,15 @@ struct State {
       if (kinds[a] == Kind::ClientWorker) v.push_back((int)a);
     return v;
   }
-  // Search-equivalence key (SearchState.java:575-619 + AbstractState/SearchState equality).
+  // Search-equivalence key (SearchState.java:575-619 + AbstractState/SearchState equality):
+  // SearchState equality plus Throwable identity.
   std::string key() const {
+    std::string k = contentKey();
+    if (exception) k += "EXC#" + std::to_string(exceptionId);
+    return k;
+  }
+  // SearchState.equals (nodes, network, timers; thrownException is transient, SearchState.java:67-89)
+  std::string contentKey() const {
     std::string k;
     for (size_t a = 0; a < nodes.size(); a++) {
       k += "N" + std::to_string(a) + ":";
@@ -319,7 +327,6 @@ struct State {
       k += "]";
     }
     k += "}";
-    if (exception) k += "EXC#" + std::to_string(exceptionId);
     if (!dropped.empty()) {
       k += "UNDROPPED{";
       for (auto& e : network) k += std::to_string(e.from) + ">" + std::to_string(e.to) + ":" + e.m.str() + ",";
@@ -422,6 +429,7 @@ inline std::vector<Event> events(const State& s, const Settings& st) {
 }
 
 inline void applyCtx(State& ns, const Ctx& ctx) {
+  ns.newMessages = ctx.sent;
   for (auto& e : ctx.sent) ns.network.insert(e);
   for (auto& t : ctx.timers) ns.timers[t.to].add(t);
 }
@@ -670,6 +678,62 @@ inline std::shared_ptr<const State> minimizeTrace(std::shared_ptr<const State> s
     }
   } while (shortened);
   return state;
+}
+
+// humanReadableTrace (SearchState.java:373-470): the trace's events as a causal graph -- an edge
+// from the step that first sent a message to its delivery, and from each step of a node to its
+// next step -- emitted in depth-first topological order, then replayed (skipChecks = true) from
+// the initial state, dropping steps that leave the state unchanged. Where the reference iterates
+// a HashSet of successors (order unspecified), successors are pushed in trace order here; the
+// engine (csrc/replay.hpp) uses the same rule. Returns the new end state (its trace is the
+// human-readable one), or `end` itself if a reordered event cannot be taken.
+inline std::shared_ptr<const State> humanReadableTrace(const std::shared_ptr<const State>& end) {
+  std::vector<std::shared_ptr<const State>> orig;
+  for (auto s = end; s; s = s->previous) orig.push_back(s);
+  std::reverse(orig.begin(), orig.end());
+  const int L = (int)orig.size() - 1;  // events 1..L
+  std::vector<std::set<int>> next(L + 1), prev(L + 1);
+  std::map<Envelope, int> whenSent;
+  std::map<int, int> lastStep;
+  std::vector<int> initSteps;
+  for (int i = 1; i <= L; i++) {
+    const Event& ev = *orig[i]->previousEvent;
+    if (!ev.isTimer) {
+      auto it = whenSent.find(ev.msg);
+      if (it != whenSent.end()) {
+        next[it->second].insert(i);
+        prev[i].insert(it->second);
+      }
+    }
+    const int a = ev.isTimer ? ev.timer.to : ev.msg.to;  // locationRootAddress
+    auto ls = lastStep.find(a);
+    if (ls != lastStep.end()) {
+      next[ls->second].insert(i);
+      prev[i].insert(ls->second);
+    }
+    lastStep[a] = i;
+    for (auto& me : orig[i]->newMessages) whenSent.emplace(me, i);
+    if (prev[i].empty()) initSteps.push_back(i);
+  }
+  std::vector<int> order, stack(initSteps.rbegin(), initSteps.rend());
+  while (!stack.empty()) {
+    const int n = stack.back();
+    stack.pop_back();
+    order.push_back(n);
+    for (int x : next[n]) {  // ascending trace order
+      prev[x].erase(n);
+      if (prev[x].empty()) stack.push_back(x);
+    }
+  }
+  std::shared_ptr<const State> s = orig[0];
+  for (int n : order) {
+    const Event& ev = *orig[n]->previousEvent;
+    auto nx = stepEvent(s, ev);
+    if (!nx) return end;
+    if (nx->contentKey() == s->contentKey()) continue;  // next.equals(previous): a step that changes nothing
+    s = nx;
+  }
+  return s;
 }
 
 struct ReplayOutcome {

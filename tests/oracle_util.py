@@ -33,7 +33,8 @@ def replay(args, events, timeout: float = 60) -> dict:
 
 
 def replay_search(args, events, minimize: bool, timeout: float = 60) -> dict:
-    """TraceReplaySearch on the oracle (checkState per step, TraceMinimizer when `minimize`)."""
+    """TraceReplaySearch on the oracle (checkState per step, TraceMinimizer when `minimize`;
+    with "--human-readable" in args the reported state's trace is SearchState.humanReadableTrace)."""
     with tempfile.NamedTemporaryFile("w", suffix=".trace", delete=False) as f:
         f.write("\n".join(events) + "\n")
         path = f.name

@@ -100,3 +100,27 @@ def test_dfs_minimization_matches_oracle_minimizer(fname, name, depth):
         assert again["trace"] == mt.trace()
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("fname,name,depth", DFS_CASES)
+def test_human_readable_trace_matches_oracle(fname, name, depth):
+    """SearchState.humanReadableTrace on raw random-DFS traces (long, with no-op steps): the
+    engine's reordering equals the oracle's and ends in the same state."""
+    case = _gold(fname, name)
+    args = [a for a in case["args"] if a != "--finish-level"]
+    proto = argmap.protocol(args)
+    s = argmap.settings(args, proto)
+    s.maxDepth(depth)
+    s.maxTimeSecs(60)
+    e = Engine(proto)
+    try:
+        raw = e.dfs(proto.initial_state(), s, probes=8192, seed=5, minimize=False)
+        st = raw.invariantViolatingState()
+        hr = e.human_readable_trace(proto.initial_state(), s, st.events())
+        want = oracle_util.replay_search(args + ["--human-readable"], st.trace(), False)
+        assert want["end"] == "INVARIANT_VIOLATED"  # the raw trace replays to its violation
+        assert hr.trace() == want["trace"]
+        assert hr.depth() == want["depth"] == len(want["trace"]) <= st.depth()
+        assert hr.packed == st.packed  # same end state
+    finally:
+        e.close()

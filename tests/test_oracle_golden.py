@@ -131,3 +131,11 @@ def test_oracle_minimizer_reference_cases(case):
         assert r["end"] == end
         assert r["depth"] == depth
         assert len(r["trace"]) == depth
+
+
+def test_oracle_human_readable_trace_drops_noop_steps():
+    """SearchState.humanReadableTrace: the repeated Foo delivery changes nothing and is dropped;
+    the causal order (b's Bar after a's Foo reached b) is kept."""
+    r = oracle_util.replay_search(["--proto", "minitest", "--inv", "foo", "--human-readable"], MINI_TRACE, False)
+    assert r["trace"] == ["Message(a -> b, Foo())", "Message(b -> a, Bar())"]
+    assert r["depth"] == 2
