@@ -93,9 +93,13 @@ struct BfsEngine : EngineBase {
     Fp* cur_fp = nullptr;
     Fp* next_fp = nullptr;
     uint64_t cur_cap = 0, next_cap = 0, curfp_cap = 0, nextfp_cap = 0;
-    uint64_t* hist_parent = nullptr;
-    uint32_t* hist_event = nullptr;
-    uint64_t hp_cap = 0, he_cap = 0;
+    // history: per BFS level of the search (index = depth - initial depth), parent pointer and
+    // event of every row of that level's frontier; one buffer pair per level, kept across
+    // searches, so a repeated search neither reallocates nor copies history
+    std::vector<uint64_t*> hpar;
+    std::vector<uint32_t*> hev;
+    std::vector<uint64_t> hcap;
+    bool flip = false;  // cur/next swapped an odd number of times since the search started
     LevelCounters* ctr = nullptr;
     TerminalRec* terms = nullptr;
     RouteCounters* rc = nullptr;
@@ -126,7 +130,7 @@ struct BfsEngine : EngineBase {
     int cset = 0;
     uint64_t segcap = 0;
     int nseg = 1;
-    std::vector<uint64_t> level_base, level_size;
+    std::vector<uint64_t> level_size;  // rows of each level's frontier (history entries)
     uint64_t cap_fp = 0, cap_v = 0, cap_s = 0;
     uint64_t n_in_fp = 0, n_in_items = 0, n_in_st = 0;
     LevelCounters lc{};
@@ -204,10 +208,11 @@ struct BfsEngine : EngineBase {
 
   ~BfsEngine() override {
     for (auto& s : sh) {
-      void* ptrs[] = {s.table,    s.cur,   s.next,   s.cur_fp,    s.next_fp, s.hist_parent,
-                      s.hist_event, s.terms,  s.rc,        s.seed,    s.out_fp,
-                      s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.ctrbuf};
+      void* ptrs[] = {s.table, s.cur,  s.next,      s.cur_fp,   s.next_fp, s.terms, s.rc,   s.seed,
+                      s.out_fp, s.in_fp, s.out_items, s.in_items, s.out_st,  s.in_st, s.spill, s.ctrbuf};
       for (void* q : ptrs) (void)hipFree(q);
+      for (auto* q : s.hpar) (void)hipFree(q);
+      for (auto* q : s.hev) (void)hipFree(q);
       if (s.hctr) (void)hipHostFree(s.hctr);
     }
     (void)hipFree(qctr);
@@ -256,6 +261,9 @@ struct BfsEngine : EngineBase {
     const uint64_t ncap = std::max<uint64_t>(std::max<uint64_t>(need, *cap + *cap / 2), 1024);
     T* np = nullptr;
     n_reallocs++;
+    if (getenv("DSL_LEVEL_TRACE"))
+      fprintf(stderr, "[grow] %zu-byte elements: %llu -> %llu (keep %llu)\n", sizeof(T), (unsigned long long)*cap,
+              (unsigned long long)ncap, (unsigned long long)(keep ? keep_elems : 0));
     DSL_HIP(hipMalloc(&np, ncap * sizeof(T)));
     if (keep && *ptr && keep_elems)
       DSL_HIP(hipMemcpyAsync(np, *ptr, keep_elems * sizeof(T), hipMemcpyDeviceToDevice, stream));
@@ -269,6 +277,21 @@ struct BfsEngine : EngineBase {
     uint64_t cw = *cap * NW;
     DSL_TRY(grow(ptr, &cw, rows * NW, keep, keep_rows * NW));
     *cap = cw / NW;
+    return DSL_OK;
+  }
+
+  // History of level `lev` with room for `rows` entries, the first `keep` preserved.
+  int hist_grow(Shard& S, size_t lev, uint64_t rows, uint64_t keep) {
+    if (S.hpar.size() <= lev) {
+      S.hpar.resize(lev + 1, nullptr);
+      S.hev.resize(lev + 1, nullptr);
+      S.hcap.resize(lev + 1, 0);
+    }
+    uint64_t c = S.hcap[lev];
+    DSL_TRY(grow(&S.hpar[lev], &c, rows, keep > 0, keep));
+    c = S.hcap[lev];
+    DSL_TRY(grow(&S.hev[lev], &c, rows, keep > 0, keep));
+    S.hcap[lev] = c;
     return DSL_OK;
   }
 
@@ -358,7 +381,13 @@ struct BfsEngine : EngineBase {
     }
     const int nseg = kSegs;
     const uint64_t span = queue_span(S.F);
-    q_span_hint = std::max(q_span_hint, span);
+    if (span > q_span_hint) {
+      // the next search's first queue starts with this span at level 1: size those history
+      // levels now, so that a repeated search allocates nothing (the live rows are kept)
+      q_span_hint = span;
+      for (size_t lv = 1; lv <= (size_t)kQueue; lv++)
+        DSL_TRY(hist_grow(S, lv, span, lv < S.level_size.size() ? S.level_size[lv] : 0));
+    }
     q_segcap = span / nseg;
     // levels: up to kQueue, none past max_depth (its level's successors are all pruned)
     const int nq = hset.max_depth >= 0 ? std::max(1, std::min(kQueue, hset.max_depth - depth)) : kQueue;
@@ -369,9 +398,8 @@ struct BfsEngine : EngineBase {
     DSL_TRY(grow(&S.cur_fp, &S.curfp_cap, std::max(span, used), true, used));
     DSL_TRY(grow_rows(&S.next, &S.next_cap, span, false, 0));
     DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, span, false, 0));
-    const uint64_t hbase0 = S.level_base.back() + S.level_size.back();
-    DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
-    DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase0 + (uint64_t)kQueue * span, true, hbase0));
+    const size_t lev0 = S.level_size.size();  // the history level of the first queued level's rows
+    for (int j = 0; j < nq; j++) DSL_TRY(hist_grow(S, lev0 + j, span, 0));
     DSL_TRY(grow(&S.spill, &S.spill_cap, wlimit, false, 0));
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     const int pb_max = std::max(1, std::min({(int)((DSL_ROWS_LDS_KB * 1024) / per), kLevelBlock,
@@ -405,8 +433,8 @@ struct BfsEngine : EngineBase {
       a.incremental = depth + j > init_depth ? 1 : 0;
       a.next = (j & 1) ? S.cur : S.next;
       a.next_fp = (j & 1) ? S.cur_fp : S.next_fp;
-      a.next_parent = S.hist_parent + hbase0 + (uint64_t)j * span;
-      a.next_event = S.hist_event + hbase0 + (uint64_t)j * span;
+      a.next_parent = S.hpar[lev0 + j];
+      a.next_event = S.hev[lev0 + j];
       a.seg_ctr = reinterpret_cast<unsigned long long*>(set + kCtrSegOff);
       a.zero_next = reinterpret_cast<uint4*>(set + kCtrSet);
       a.nseg = nseg;
@@ -494,9 +522,16 @@ struct BfsEngine : EngineBase {
       DSL_TRY(grow_rows(&S.next, &S.next_cap, 1024, false, 0));
       DSL_TRY(grow(&S.cur_fp, &S.curfp_cap, 1024, false, 0));
       DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, 1024, false, 0));
-      DSL_TRY(grow(&S.hist_parent, &S.hp_cap, 1024, false, 0));
-      DSL_TRY(grow(&S.hist_event, &S.he_cap, 1024, false, 0));
-      S.level_base.assign(1, 0);
+      // every search starts with the same buffer of each pair as `cur`: the two then take the
+      // same roles level by level in every search, so a repeated search reallocates nothing
+      if (S.flip) {
+        std::swap(S.cur, S.next);
+        std::swap(S.cur_cap, S.next_cap);
+        std::swap(S.cur_fp, S.next_fp);
+        std::swap(S.curfp_cap, S.nextfp_cap);
+        S.flip = false;
+      }
+      DSL_TRY(hist_grow(S, 0, 1, 0));
       S.level_size.assign(1, 0);
       S.F = 0;
       S.work = 0;
@@ -549,6 +584,9 @@ struct BfsEngine : EngineBase {
     }
     if (comm) DSL_TRY(comm->allreduce_u64(&init_enc, 1, true, stream));
     const int init_verdict = (int)(init_enc >> 32);
+    if (trace_levels)
+      fprintf(stderr, "[setup] %.4f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
 
     std::vector<uint64_t> per_depth{1};
     uint64_t total_states = 1, successors = 0, exchanged = 0;
@@ -596,7 +634,12 @@ struct BfsEngine : EngineBase {
           const double growth =
               nd >= 2 && per_depth[nd - 2] ? std::max(1.0, (double)per_depth[nd - 1] / per_depth[nd - 2]) : 3.0;
           int ran = 0;
+          const auto tq0 = std::chrono::steady_clock::now();
           DSL_TRY(enqueue_queue(depth, tbl_proto, growth, &ran));
+          if (trace_levels)
+            fprintf(stderr, "[queue] enqueue+run %.4f ms (loop entry %.4f ms after start)\n",
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count(),
+                    std::chrono::duration<double, std::milli>(tq0 - t_start).count());
           q_left = ran;
           q_pos = 0;
         }
@@ -622,11 +665,9 @@ struct BfsEngine : EngineBase {
           const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 8192)) + 1;
           S.segcap = (want + S.nseg - 1) / S.nseg + 1;
           const uint64_t rows = S.segcap * S.nseg;
-          const uint64_t hbase = S.level_base.back() + S.level_size.back();
           DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
           DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
-          DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + rows, true, hbase));
-          DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + rows, true, hbase));
+          DSL_TRY(hist_grow(S, S.level_size.size(), rows, 0));
           DSL_TRY(grow(&S.spill, &S.spill_cap, std::max<uint64_t>(S.work, 1), false, 0));
           S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf + S.cset * kCtrSet);
           S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + S.cset * kCtrSet + kCtrSegOff);
@@ -658,9 +699,8 @@ struct BfsEngine : EngineBase {
           a.incremental = depth > init_depth ? 1 : 0;
           a.next = S.next;
           a.next_fp = S.next_fp;
-          const uint64_t hbase = S.level_base.back() + S.level_size.back();
-          a.next_parent = S.hist_parent + hbase;
-          a.next_event = S.hist_event + hbase;
+          a.next_parent = S.hpar[S.level_size.size()];
+          a.next_event = S.hev[S.level_size.size()];
           a.seg_ctr = S.seg_ctr;
           a.zero_next = reinterpret_cast<uint4*>(S.ctrbuf + (S.cset ^ 1) * kCtrSet);
           a.nseg = S.nseg;
@@ -727,15 +767,14 @@ struct BfsEngine : EngineBase {
           if (!ns || S.lc.err_frontier || S.lc.err_overflow) continue;
           unspilled = true;
           const uint64_t keep = span[l], need = keep + ns;
-          const uint64_t hbase = S.level_base.back() + S.level_size.back();
+          const size_t lv = S.level_size.size();
           DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
           DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
-          DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + need, true, hbase + keep));
-          DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + need, true, hbase + keep));
+          DSL_TRY(hist_grow(S, lv, need, keep));
           const int blocks = (int)std::min<uint64_t>((ns + kBlock - 1) / kBlock, 256ull * 32);
           LevelCounters* uctr = queued ? reinterpret_cast<LevelCounters*>(qctr + (size_t)q_pos * kCtrSet) : S.ctr;
           hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, ns, S.cur, S.cur_fp, S.next,
-                             S.next_fp, S.hist_parent + hbase, S.hist_event + hbase, keep, S.gid, uctr, prm, dset);
+                             S.next_fp, S.hpar[lv], S.hev[lv], keep, S.gid, uctr, prm, dset);
           nbase[l].push_back(keep);
           ncnt[l].push_back(ns);
           span[l] = need;
@@ -802,13 +841,12 @@ struct BfsEngine : EngineBase {
             const uint64_t keep = span[l], need = keep + S.n_in_st;
             DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
             DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
-            const uint64_t hbase = S.level_base.back() + S.level_size.back();
-            DSL_TRY(grow(&S.hist_parent, &S.hp_cap, hbase + need, true, hbase + keep));
-            DSL_TRY(grow(&S.hist_event, &S.he_cap, hbase + need, true, hbase + keep));
+            const size_t lv = S.level_size.size();
+            DSL_TRY(hist_grow(S, lv, need, keep));
             const int blocks = (int)std::min<uint64_t>((S.n_in_st + kBlock - 1) / kBlock, 256ull * 32);
             hipLaunchKernelGGL(k_append_received<P>, dim3(blocks), dim3(kBlock), 0, stream, S.in_st, S.n_in_st,
-                               S.next + keep * NW, S.next_fp + keep, S.hist_parent + hbase + keep,
-                               S.hist_event + hbase + keep, S.n_in_st, S.ctr);
+                               S.next + keep * NW, S.next_fp + keep, S.hpar[lv] + keep,
+                               S.hev[lv] + keep, S.n_in_st, S.ctr);
             nbase[l].push_back(keep);
             ncnt[l].push_back(S.n_in_st);
             span[l] = need;
@@ -894,8 +932,6 @@ struct BfsEngine : EngineBase {
         progress_depth = depth;
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
-          const uint64_t hbase = S.level_base.back() + S.level_size.back();
-          S.level_base.push_back(hbase);
           S.level_size.push_back(span[l]);
         }
         const double lms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count();
@@ -924,7 +960,7 @@ struct BfsEngine : EngineBase {
           // walk parent pointers back level by level (across shards)
           std::vector<uint32_t> evs{(uint32_t)rec[1]};
           uint64_t ref = rec[0];
-          const int nlev = (int)sh[0].level_base.size();
+          const int nlev = (int)sh[0].level_size.size();
           for (int lev = nlev - 2; lev >= 1; lev--) {
             const int r = (int)(ref >> 48);
             const uint64_t idx = ref & ((1ull << 48) - 1);
@@ -933,8 +969,8 @@ struct BfsEngine : EngineBase {
               if (sh[l].gid == r) {
                 uint64_t p;
                 uint32_t e;
-                DSL_HIP(hipMemcpy(&p, sh[l].hist_parent + sh[l].level_base[lev] + idx, 8, hipMemcpyDeviceToHost));
-                DSL_HIP(hipMemcpy(&e, sh[l].hist_event + sh[l].level_base[lev] + idx, 4, hipMemcpyDeviceToHost));
+                DSL_HIP(hipMemcpy(&p, sh[l].hpar[lev] + idx, 8, hipMemcpyDeviceToHost));
+                DSL_HIP(hipMemcpy(&e, sh[l].hev[lev] + idx, 4, hipMemcpyDeviceToHost));
                 hop[0] = p;
                 hop[1] = e;
               }
@@ -954,6 +990,7 @@ struct BfsEngine : EngineBase {
           std::swap(S.cur_cap, S.next_cap);
           std::swap(S.cur_fp, S.next_fp);
           std::swap(S.curfp_cap, S.nextfp_cap);
+          S.flip = !S.flip;
           S.seg_base = nbase[l];
           S.seg_cnt = ncnt[l];
           S.F = 0;
@@ -999,6 +1036,9 @@ struct BfsEngine : EngineBase {
       std::memcpy(r->terminal_state, &s, sizeof(init));
       trace_events.clear();
     }
+    if (trace_levels)
+      fprintf(stderr, "[run] %.4f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     *out = r;
     return DSL_OK;
   }
