@@ -261,7 +261,9 @@ __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t
 
 template <class P, bool ROUTE>
 // Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel; the few values the
-// register allocator then spills are cold (measured: 2 waves/SIMD at 175 VGPRs is 1.5x slower).
+// register allocator then spills are cold (measured on C5 Multi-Paxos, which spills 160 B/lane
+// here: 2 waves/SIMD at 175 VGPRs is 1.5x slower; 3 waves/SIMD is 7-11 % slower at d12/d14;
+// 5 waves/SIMD is 1.5-1.65x slower).
 #ifndef DSL_KLEVEL_ATTR
 #define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
