@@ -24,7 +24,7 @@ DSL_OK = 0
 STATUS_NAMES = {
     -1: "DSL_ERR_ARG", -2: "DSL_ERR_HIP", -3: "DSL_ERR_TABLE_FULL", -4: "DSL_ERR_FRONTIER_FULL",
     -5: "DSL_ERR_STATE_OVERFLOW", -6: "DSL_ERR_UNKNOWN_PROTOCOL", -7: "DSL_ERR_UNKNOWN_PREDICATE",
-    -8: "DSL_ERR_COMM", -9: "DSL_ERR_NO_DEVICE", -10: "DSL_ERR_PROBE_LIMIT",
+    -8: "DSL_ERR_COMM", -9: "DSL_ERR_NO_DEVICE",
 }
 
 # Exported symbols declared in include/dslabs_hip.h (checked by tests/test_capi.py).
@@ -96,11 +96,12 @@ class dsl_result(ctypes.Structure):
 
 
 class dsl_stats(ctypes.Structure):
-    _fields_ = [("expand_ms", ctypes.c_double), ("count_ms", ctypes.c_double), ("scan_ms", ctypes.c_double),
+    _fields_ = [("expand_ms", ctypes.c_double), ("exchange_ms", ctypes.c_double),
                 ("expand_launches", ctypes.c_uint64), ("parents", ctypes.c_uint64),
                 ("work_items", ctypes.c_uint64), ("new_states", ctypes.c_uint64), ("appended", ctypes.c_uint64),
                 ("exchanged", ctypes.c_uint64), ("state_bytes", ctypes.c_uint32), ("world_size", ctypes.c_uint32),
-                ("table_slots", ctypes.c_uint64)]
+                ("table_slots", ctypes.c_uint64), ("terminal_finds", ctypes.c_uint64),
+                ("sharded_levels", ctypes.c_uint64), ("probes", ctypes.c_uint64)]
 
 
 _lib = None

@@ -102,6 +102,7 @@ struct BfsEngine : EngineBase {
     bool flip = false;  // cur/next swapped an odd number of times since the search started
     LevelCounters* ctr = nullptr;
     TerminalRec* terms = nullptr;
+    unsigned char* find_ctr = nullptr;  // scratch counter sets of a find-mode k_level
     RouteCounters* rc = nullptr;
     int32_t* seed = nullptr;
     FpRec* out_fp = nullptr;
@@ -150,6 +151,8 @@ struct BfsEngine : EngineBase {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   uint64_t table_buckets = 0;
   uint64_t avg_events_x16 = 16 * 8;  // running estimate of events per state (x16)
+  uint32_t term_cap = kTermCap;      // TerminalRec entries per shard (DSL_TERM_CAP)
+  uint32_t terms_alloc = 0;
   std::vector<uint32_t> trace_events;
 
   // ---- queued small levels (single local shard) ------------------------------------------------
@@ -208,8 +211,9 @@ struct BfsEngine : EngineBase {
 
   ~BfsEngine() override {
     for (auto& s : sh) {
-      void* ptrs[] = {s.table, s.cur,  s.next,      s.cur_fp,   s.next_fp, s.terms, s.rc,   s.seed,
-                      s.out_fp, s.in_fp, s.out_items, s.in_items, s.out_st,  s.in_st, s.spill, s.ctrbuf};
+      void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,     s.seed,
+                      s.out_fp,    s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.ctrbuf,
+                      s.find_ctr};
       for (void* q : ptrs) (void)hipFree(q);
       for (auto* q : s.hpar) (void)hipFree(q);
       for (auto* q : s.hev) (void)hipFree(q);
@@ -443,6 +447,7 @@ struct BfsEngine : EngineBase {
       a.spill_cap = S.spill_cap;
       a.ctr = reinterpret_cast<LevelCounters*>(set);
       a.terms = S.terms;
+      a.term_cap = term_cap;
       a.table = tbl_proto;
       a.table.slots = S.table;
       a.W = W;
@@ -479,6 +484,69 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
+  // The TerminalRec of the level's best terminal key: from the list of improvements, or (the list
+  // overflowed) by re-running the level's expansion in find mode over the current frontier.
+  int resolve_terminal(Shard& S, uint64_t key, int succ_depth, bool incremental, TerminalRec* out) {
+    const uint64_t n = std::min<uint64_t>(S.lc.n_term_rec, term_cap);
+    std::vector<TerminalRec> recs(n);
+    if (n) {
+      DSL_HIP(hipMemcpyAsync(recs.data(), S.terms, n * sizeof(TerminalRec), hipMemcpyDeviceToHost, stream));
+      DSL_HIP(hipStreamSynchronize(stream));
+    }
+    for (const auto& r : recs)
+      if (r.key == key) {
+        *out = r;
+        return DSL_OK;
+      }
+    stats.terminal_finds++;
+    if (!S.find_ctr) DSL_HIP(hipMalloc(&S.find_ctr, 2 * kCtrSet));
+    DSL_HIP(hipMemsetAsync(S.find_ctr, 0, 2 * kCtrSet, stream));
+    DSL_HIP(hipMemsetAsync(S.terms, 0, sizeof(TerminalRec), stream));
+    uint64_t F = 0;
+    for (uint64_t c : S.seg_cnt) F += c;
+    const int PB = chunk_parents(F);
+    LevelArgs<P> a{};
+    a.cur = S.cur;
+    a.cur_fp = S.cur_fp;
+    a.segs.n = (int32_t)S.seg_cnt.size();
+    a.segs.pb = PB;
+    for (int q = 0; q < a.segs.n; q++) {
+      a.segs.base[q] = S.seg_base[q];
+      a.segs.cnt[q] = S.seg_cnt[q];
+      a.segs.chunk0[q + 1] = a.segs.chunk0[q] + (S.seg_cnt[q] + PB - 1) / PB;
+    }
+    a.PB = PB;
+    a.depth = succ_depth;
+    a.incremental = incremental ? 1 : 0;
+    a.next = S.next;
+    a.next_fp = S.next_fp;
+    a.next_parent = S.hpar[0];
+    a.next_event = S.hev[0];
+    a.seg_ctr = reinterpret_cast<unsigned long long*>(S.find_ctr + kCtrSegOff);
+    a.zero_next = reinterpret_cast<uint4*>(S.find_ctr + kCtrSet);
+    a.nseg = 1;
+    a.segcap = 0;
+    a.ctr = reinterpret_cast<LevelCounters*>(S.find_ctr);
+    a.terms = S.terms;
+    a.term_cap = 1;
+    a.W = W;
+    a.me = S.gid;
+    a.find = 1;
+    a.find_key = key;
+    const uint64_t nchunks = a.segs.chunk0[a.segs.n];
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, kLevelGrid));
+    const size_t lds = (size_t)PB * (NW * 4 + sizeof(Fp) + 4) + 16;
+    hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
+    DSL_HIP(hipGetLastError());
+    DSL_HIP(hipMemcpyAsync(out, S.terms, sizeof(TerminalRec), hipMemcpyDeviceToHost, stream));
+    DSL_HIP(hipStreamSynchronize(stream));
+    if (out->key != key) {
+      set_error("terminal state of the level could not be resolved");
+      return DSL_ERR_ARG;
+    }
+    return DSL_OK;
+  }
+
   int run(dsl_result** out) override {
     auto t_start = std::chrono::steady_clock::now();
     (void)hipGetLastError();  // the per-thread sticky error must not blame this search for an older call
@@ -496,6 +564,7 @@ struct BfsEngine : EngineBase {
       DSL_TRY(get_initial(tmp, sizeof(init)));
     }
     const int L = (int)sh.size();
+    if (const char* tc = getenv("DSL_TERM_CAP")) term_cap = (uint32_t)std::max(1l, strtol(tc, nullptr, 10));
     const int log2 = hset.table_log2_slots > 0 ? hset.table_log2_slots : 26;
     if (log2 < 10 || log2 > 40) return DSL_ERR_ARG;
     const uint64_t buckets = (1ull << log2) / 8;
@@ -512,7 +581,11 @@ struct BfsEngine : EngineBase {
       S.cset = 0;
       S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf);
       S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + kCtrSegOff);
-      if (!S.terms) DSL_HIP(hipMalloc(&S.terms, sizeof(TerminalRec) * kTermCap));
+      if (!S.terms || terms_alloc != term_cap) {
+        (void)hipFree(S.terms);
+        S.terms = nullptr;
+        DSL_HIP(hipMalloc(&S.terms, sizeof(TerminalRec) * term_cap));
+      }
       if (!S.rc) DSL_HIP(hipMalloc(&S.rc, sizeof(RouteCounters)));
       if (!S.seed) DSL_HIP(hipMalloc(&S.seed, 4 * sizeof(int32_t)));
       S.seg_base.clear();
@@ -537,6 +610,7 @@ struct BfsEngine : EngineBase {
       S.work = 0;
     }
     table_buckets = buckets;
+    terms_alloc = term_cap;
     stats.table_slots = buckets * 8 * (uint64_t)W;
     q_left = 0;
     q_pos = 0;
@@ -684,7 +758,7 @@ struct BfsEngine : EngineBase {
         DSL_HIP(hipEventRecord(ev0, stream));
         for (auto& S : sh) {
           if (S.F == 0) continue;
-          LevelArgs<P> a;
+          LevelArgs<P> a{};
           a.cur = S.cur;
           a.cur_fp = S.cur_fp;
           a.segs.n = (int32_t)S.seg_cnt.size();
@@ -709,6 +783,7 @@ struct BfsEngine : EngineBase {
           a.spill_cap = S.spill_cap;
           a.ctr = S.ctr;
           a.terms = S.terms;
+          a.term_cap = term_cap;
           a.table = tbl_proto;
           a.table.slots = S.table;
           a.W = W;
@@ -829,6 +904,7 @@ struct BfsEngine : EngineBase {
             ma.rc = S.rc;
             ma.ctr = S.ctr;
             ma.terms = S.terms;
+            ma.term_cap = term_cap;
             const int blocks = (int)std::min<uint64_t>((S.n_in_items + kBlock - 1) / kBlock, 256ull * 32);
             hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
           }
@@ -894,16 +970,12 @@ struct BfsEngine : EngineBase {
           stats.parents += S.F;
           stats.work_items += S.lc.work_items;
           stats.new_states += S.lc.new_states;
+          stats.probes += S.lc.probes;
           stats.appended += fn;
-          if (S.lc.n_terminals) {
-            const uint32_t nt = (uint32_t)std::min<unsigned long long>(S.lc.n_terminals, kTermCap);
-            std::vector<TerminalRec> terms(nt);
-            DSL_HIP(hipMemcpy(terms.data(), S.terms, nt * sizeof(TerminalRec), hipMemcpyDeviceToHost));
-            TerminalRec b = terms[0];
-            for (auto& t : terms)
-              if (t.verdict < b.verdict || (t.verdict == b.verdict && t.key < b.key)) b = t;
-            local_best[l] = b;
-            enc = std::min(enc, ((uint64_t)b.verdict << 60) | ((b.key >> 12) << 8) | (uint64_t)S.gid);
+          if (S.lc.term_best) {  // the level's exact best terminal (fold_terminals)
+            const uint64_t key = ~(uint64_t)S.lc.term_best;
+            DSL_TRY(resolve_terminal(S, key, depth + 1, depth > init_depth, &local_best[l]));
+            enc = std::min<uint64_t>(enc, (key & ~(uint64_t)0xff) | (uint64_t)S.gid);
           }
         }
         if (!rep) {

@@ -6,14 +6,19 @@
 //      16-byte coalesced loads -- every parent is read from HBM exactly once;
 //   2. one lane per parent counts its enabled events (SearchState.events), a workgroup-local
 //      exclusive scan turns the counts into work-item offsets (no global scan pass);
-//   3. every lane takes work items (parent j, event k): the successor is computed as a DELTA
-//      in registers (one node's words + a short send list), its fingerprint incrementally from
-//      the parent's (nodestate.hpp), then one 64-byte visited-table bucket probe / CAS insert
-//      (discovered.add, Search.java:485). Only a NEW successor is judged (checkState over a node
-//      view: parent words in LDS + the changed node) and, if VALID, materialized straight into
-//      the next frontier (row + fingerprint + parent pointer + event index).
+//   3. the chunk's work items (parent j, event k) are listed per parent and counting-sorted by
+//      handler class (ballots), so a wavefront mostly runs one handler; every lane takes one:
+//      the successor is computed as a DELTA in registers (one node's words + a short send
+//      list), its fingerprint incrementally from the parent's (nodestate.hpp), then one 64-byte
+//      visited-table bucket probe / CAS insert (discovered.add, Search.java:485). Only a NEW
+//      successor is judged (checkState over a node view: parent words in LDS + the changed
+//      node); terminal candidates fold into the level's exact best (fold_terminals);
+//      An event that changes neither its node nor the network (most redeliveries: the network
+//      is a set, every message stays deliverable) leads back to the parent: no fingerprint, no
+//      probe. A VALID successor reserves a row (one returning atomic per wavefront) and the
+//      wavefront writes its rows cooperatively (row + fingerprint + parent pointer + event).
 //   ROUTE (multi-shard): a successor owned by another shard is not probed here; a 24-byte
-//      FpRec goes to its owner's outgoing region instead (sharded.hpp for the other phases).
+//      FpRec goes to its owner's outgoing region instead (bfs_engine.hpp runs the other phases).
 #pragma once
 #include "nodestate.hpp"
 
@@ -24,7 +29,7 @@ constexpr int kBlock = 256;
 // wavefront per workgroup is slower -- its smaller chunks sort into more handler classes per
 // wavefront -- despite having no cross-wavefront barrier waits).
 constexpr int kLevelBlock = 256;
-constexpr uint32_t kTermCap = 1024;
+constexpr uint32_t kTermCap = 1024;  // default TerminalRec entries per shard (DSL_TERM_CAP)
 constexpr int kMaxShards = 16;
 constexpr int kWin = 1024;  // work items per class-sorted window of k_level
 // The next frontier is written into up to kSegs segments, one reservation counter each (a
@@ -50,13 +55,16 @@ struct LevelCounters {
   unsigned long long new_states;    // newly discovered successors (all verdicts)
   unsigned long long next_size;     // VALID successors appended to the next frontier
   unsigned long long successors;    // events applied (non-null successors)
-  unsigned long long n_terminals;   // terminal candidates recorded
+  unsigned long long n_terminals;   // terminal candidates of the level
   unsigned long long err_overflow;  // STEP_OVERFLOW count
   unsigned long long err_table;     // INS_FULL count
   unsigned long long err_frontier;  // appends beyond capacity
   unsigned long long work_items;    // (state, event) pairs of this level
   unsigned long long next_work;     // enabled events of the appended states (= next level's work)
   unsigned long long spilled;       // VALID states beyond the next frontier's capacity (spill list)
+  unsigned long long term_best;     // ~(best terminal key) of the level (atomicMax; 0 = none)
+  unsigned long long n_term_rec;    // TerminalRec entries written (improvements of term_best)
+  unsigned long long probes;        // visited-table probes (successors that are not no-ops)
   unsigned long long phase[8];      // DSL_PHASES builds only: shader cycles per k_level phase
 };
 
@@ -80,7 +88,7 @@ struct TerminalRec {
   uint32_t event;   // event index within the parent's enabled events
   uint32_t pad;
   uint64_t parent;  // index of the parent in the current frontier
-  uint64_t key;     // fingerprint high word (deterministic tie-break)
+  uint64_t key;     // term_key: priority rank << 62 | fingerprint bits (deterministic tie-break)
 };
 
 struct RouteCounters {
@@ -250,6 +258,9 @@ struct LevelArgs {
   const unsigned long long* qprev_seg;
   uint64_t qflimit, qwlimit;         // the queue stops above these frontier / work sizes
   int32_t qspread;                   // parents per chunk = ceil(F / qspread), at most PB
+  uint32_t term_cap;                 // TerminalRec entries of `terms`
+  int32_t find;                      // find mode (no table, no rows): the successor whose terminal
+  uint64_t find_key;                 // key equals find_key is recorded in terms[0]
 };
 
 // The queue's stop rule: after a level with any of these, the host must act before the next one.
@@ -259,37 +270,83 @@ __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t
          c.next_work <= wlimit;
 }
 
-template <class P, bool ROUTE>
-// Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel; the few values the
-// register allocator then spills are cold (measured on C5 Multi-Paxos, which spills 160 B/lane
-// here: 2 waves/SIMD at 175 VGPRs is 1.5x slower; 3 waves/SIMD is 7-11 % slower at d12/d14;
-// 5 waves/SIMD is 1.5-1.65x slower).
+// Copies n16 16-byte units from global memory to LDS with LDS-DMA: wave w issues units
+// [64 (w + 4 r), +64) for r = 0, 1, ...; the destination of one wave-instruction is its
+// wave-uniform base + lane x 16. No wait here: the caller waits (vmcnt) before its barrier.
+__device__ __forceinline__ void stage_lds(const uint4* src, uint4* dst, int n16) {
+  const int lane = __lane_id();
+  for (int b = (int)(threadIdx.x >> 6) * 64; b < n16; b += (int)blockDim.x) {
+    if (b + lane < n16)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + b + lane),
+                                       (__attribute__((address_space(3))) void*)(dst + b), 16, 0, 0);
+  }
+}
+
+// Terminal candidates of a level are reduced EXACTLY by priority (EXCEPTION > INVARIANT > GOAL,
+// Search.java:370-385), then by the successor's fingerprint (a deterministic tie-break): a wave
+// takes the minimum key of its candidates and folds it into LevelCounters::term_best with one
+// 64-bit atomicMax of the complemented key (counter sets start zeroed); a wave whose key improved
+// the running best records that candidate in the level's TerminalRec list. The final best key was
+// recorded by the last improvement, so it is in the list unless the list overflowed (>term_cap
+// improvements); the host then re-runs the level in find mode (LevelArgs::find_key), which
+// records the successor whose key matches.
+__device__ __forceinline__ uint64_t term_key(int verdict, uint64_t fphi) {
+  return ((uint64_t)(verdict - V_TERM_EXCEPTION) << 62) | (fphi >> 2);
+}
+
+__device__ __forceinline__ void fold_terminals(bool term, uint64_t key, int v, int pi, uint32_t k, uint64_t parent,
+                                               LevelCounters* ctr, TerminalRec* terms, uint32_t cap) {
+  const unsigned long long tm = __ballot(term);
+  if (!tm) return;
+  unsigned long long m = term ? (unsigned long long)key : ~0ull;
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long y = __shfl_xor(m, o);
+    m = y < m ? y : m;
+  }
+  const int who = __ffsll((long long)__ballot(term && key == m)) - 1;
+  if (__lane_id() == who) {
+    atomicAdd(&ctr->n_terminals, (unsigned long long)__popcll(tm));
+    const unsigned long long old = atomicMax(&ctr->term_best, ~m);
+    if (old < ~m) {
+      const unsigned long long slot = atomicAdd(&ctr->n_term_rec, 1ull);
+      if (slot < cap) terms[slot] = TerminalRec{v, pi, k, 0u, parent, (uint64_t)m};
+    }
+  }
+}
+
+// Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel (r01 on C5 Multi-Paxos:
+// 2 waves/SIMD 1.5x slower, 3 waves/SIMD 7-11 % slower at d12/d14, 5 waves/SIMD 1.5-1.65x slower).
 #ifndef DSL_KLEVEL_ATTR
 #define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
+template <class P, bool ROUTE>
 __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
+  constexpr int NWAVE = kLevelBlock / 64;
+  constexpr int NC = P::kMsgClasses + 1;  // handler classes; the last one is the timers'
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // a.PB (max) * NW
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
   int* off = reinterpret_cast<int*>(fps + a.PB);           // a.PB + 1
-  __shared__ int s_total;
   __shared__ SegTable s_segs;
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
-  __shared__ unsigned long long s_red[kLevelBlock / 64];
-  __shared__ int s_hist[16];
+  __shared__ unsigned long long s_red[NWAVE];
+  __shared__ int s_wsum[NWAVE];
+  __shared__ int s_cbase[kWin / 64][NC];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
-  // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
-  unsigned long long c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0;
-  PH_DECL
   __shared__ int s_stop;
+  const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
+  const bool find = a.find != 0;
+  // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
+  uint32_t c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0, c_probe = 0;
+  PH_DECL
   if (a.qprev) {
     // queued level: this frontier is the previous level's segments; every workgroup derives the
     // table (and whether the queue stopped) from those counters, as the host does afterwards
-    if (threadIdx.x < 64) {
-      const int q = threadIdx.x;
+    if (tid < 64) {
+      const int q = tid;
       const uint64_t c = q < a.nseg ? min<uint64_t>(a.qprev_seg[q * kSegStride], a.segcap) : 0ull;
       uint64_t F = c;
       for (int o = 32; o > 0; o >>= 1) F += __shfl_xor(F, o);
@@ -314,13 +371,13 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   } else {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&a.segs);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&s_segs);
-    for (int i = threadIdx.x; i < (int)(sizeof(SegTable) / 4); i += blockDim.x) dst[i] = src[i];
-    if (threadIdx.x == 0) s_stop = 0;
+    for (int i = tid; i < (int)(sizeof(SegTable) / 4); i += blockDim.x) dst[i] = src[i];
+    if (tid == 0) s_stop = 0;
   }
   __syncthreads();
   if (s_stop) return;  // an earlier queued level stopped the queue
   if (blockIdx.x == 0)
-    for (int i = threadIdx.x; i < kCtrSet / 16; i += blockDim.x) a.zero_next[i] = make_uint4(0, 0, 0, 0);
+    for (int i = tid; i < kCtrSet / 16; i += blockDim.x) a.zero_next[i] = make_uint4(0, 0, 0, 0);
   const int PB = s_segs.pb;
   const uint64_t nchunks = s_segs.chunk0[s_segs.n];
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
@@ -329,145 +386,259 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     while (chunk >= s_segs.chunk0[g + 1]) g++;  // chunks ascend: the segment index only grows
     const uint64_t p0 = s_segs.base[g] + (chunk - s_segs.chunk0[g]) * (uint64_t)PB;
     const int pb = (int)min<uint64_t>((uint64_t)PB, s_segs.base[g] + s_segs.cnt[g] - p0);
-    // 1. stage the parents (contiguous rows) and their fingerprints in LDS
+    // 1. stage the parents (contiguous rows) and their fingerprints in LDS: LDS-DMA
+    //    (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs), every load in flight
+    //    before the one wait
+    stage_lds(reinterpret_cast<const uint4*>(a.cur + p0 * NW), reinterpret_cast<uint4*>(rows), pb * NW / 4);
+    stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#ifdef DSL_X2_STAGE  // cost probe (tools/gpu_r02_x2.sh): the staging again
+    stage_lds(reinterpret_cast<const uint4*>(a.cur + p0 * NW), reinterpret_cast<uint4*>(rows), pb * NW / 4);
+    stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+#endif
+    // 2. enabled events per parent (SearchState.events), workgroup exclusive scan (wave scans)
+    int total;
     {
-      const uint4* src = reinterpret_cast<const uint4*>(a.cur + p0 * NW);
-      uint4* dst = reinterpret_cast<uint4*>(rows);
-      const int n16 = pb * NW / 4;
-      for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
-      for (int i = threadIdx.x; i < pb; i += blockDim.x) fps[i] = a.cur_fp[p0 + i];
-    }
-    __syncthreads();
-    // 2. enabled events per parent, workgroup-local exclusive scan
-    if (threadIdx.x < pb)
-      off[threadIdx.x + 1] = (ROUTE && a.owner_filter && owner_of(fps[threadIdx.x], a.W) != a.me)
-                                 ? 0
-                                 : count_events<P>(rows + threadIdx.x * NW, prm, set);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      off[0] = 0;
-      for (int j = 0; j < pb; j++) off[j + 1] += off[j];
-      s_total = off[pb];
-      c_work += (unsigned long long)off[pb];
-    }
-    __syncthreads();
-    const int total = s_total;
-    PH_MARK(0);  // staging + event count + scan
-    // 3. the chunk's work items in windows of kWin: grouped by handler class (LDS counting sort),
-    //    then one lane per (parent, event), so a wavefront mostly runs one handler
-    for (int w0 = 0; w0 < total; w0 += kWin) {
-    const int wn = min(kWin, total - w0);
-    if (threadIdx.x < 16) s_hist[threadIdx.x] = 0;
-    __syncthreads();
-    for (int t = threadIdx.x; t < wn; t += blockDim.x) {
-      const int g = w0 + t;
-      int lo = 0, hi = pb;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (off[mid] <= g) lo = mid; else hi = mid;
+      int x = 0;
+      if (tid < pb)
+        x = (ROUTE && a.owner_filter && owner_of(fps[tid], a.W) != a.me) ? 0
+                                                                        : count_events<P>(rows + tid * NW, prm, set);
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
       }
-      const int c = event_class<P>(rows + lo * NW, prm, set, g - off[lo]);
-      s_par[t] = (uint8_t)lo;
-      s_cls[t] = (uint8_t)c;
-      atomicAdd(&s_hist[c], 1);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int acc = 0;
-      for (int c = 0; c < 16; c++) {
-        const int h = s_hist[c];
-        s_hist[c] = acc;
-        acc += h;
-      }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < wn; t += blockDim.x) s_perm[atomicAdd(&s_hist[s_cls[t]], 1)] = (uint16_t)t;
-    __syncthreads();
-    PH_MARK(7);  // classify + sort
-    for (int base = 0; base < wn; base += blockDim.x) {
-      const int t = base + threadIdx.x;
-      bool is_valid = false, route = false;
-      int dest = 0, j = 0, k = 0;
-      Fp f{0, 0};
-      Delta<P> d;
-      d.out.n = 0;
-      if (t < wn) {
-        const int u = s_perm[t];
-        j = s_par[u];
-        k = w0 + u - off[j];
-        const uint32_t* w = rows + j * NW;
-        const int rc = delta_step<P>(w, k, d, prm, set);
-        PH_MARK(1);  // decode + handler + canonical sends
-        if (rc == STEP_OK) {
-          c_succ++;
-          f = delta_fingerprint<P>(w, fps[j], d);
-          PH_MARK(2);  // fingerprint
-          if (ROUTE) dest = owner_of(f, a.W);
-          if (ROUTE && dest != a.me) {
-            route = true;
-          } else {
-            const int ins = table_insert(a.table, f);
-            PH_MARK(3);  // visited-table probe / insert
-            if (ins == INS_NEW) {
-              c_new++;
-              int pi = -1;
-              // the changed node's words go through LDS: a view pointing at the register array
-              // would take its address and push the whole delta into scratch
-              uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
+      if (lane == 63) s_wsum[wid] = x;
+      __syncthreads();
+      int pre = 0;
+      total = 0;
 #pragma unroll
-              for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
-              const NodeView view{w, P::kNodeWords, d.node, my_nw};
-              const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
-              if (v == V_VALID) {
-                if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = true;
-                else atomicAdd(&a.ctr->err_overflow, 1ull);
-              } else if (v >= V_TERM_EXCEPTION) {
-                const unsigned long long slot = atomicAdd(&a.ctr->n_terminals, 1ull);
-                if (slot < kTermCap) a.terms[slot] = TerminalRec{v, pi, (uint32_t)k, 0u, p0 + j, f.hi};
-              }
-            } else if (ins == INS_FULL) {
-              atomicAdd(&a.ctr->err_table, 1ull);
-            }
-          }
-        } else if (rc == STEP_EXCEPTION) {
-          // exceptional states never equal another (Throwable identity): new and terminal
-          c_succ++;
-          c_new++;
-          const unsigned long long slot = atomicAdd(&a.ctr->n_terminals, 1ull);
-          if (slot < kTermCap) a.terms[slot] = TerminalRec{V_TERM_EXCEPTION, -1, (uint32_t)k, 0u, p0 + j, fps[j].hi};
-        } else if (rc == STEP_OVERFLOW) {
-          atomicAdd(&a.ctr->err_overflow, 1ull);
-        }
+      for (int q = 0; q < NWAVE; q++) {
+        const int v = s_wsum[q];
+        pre += q < wid ? v : 0;
+        total += v;
       }
-      PH_MARK(4);  // judge (+ divergence wait)
-      const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
-      PH_MARK(5);  // reservation
-      const bool fits = is_valid && li < a.segcap;
-      const uint64_t idx = (uint64_t)seg * a.segcap + li;
-      if (fits) {
-        const uint32_t* w = rows + j * NW;
-        a.next_fp[idx] = f;
-        a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
-        a.next_event[idx] = (uint32_t)k;
-        c_next_work += (unsigned long long)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
+      if (tid < pb) off[tid + 1] = pre + x;
+      if (tid == 0) {
+        off[0] = 0;
+        c_work += (uint32_t)total;
       }
-      wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
-      PH_MARK(6);  // history + row emission
-      // beyond the estimated capacity: spill (parent, event); materialized after the level (rare)
-      const bool spill = is_valid && !fits;
-      if (__ballot(spill)) {
-        const unsigned long long sidx = wave_reserve(&a.ctr->spilled, spill);
-        if (spill) {
-          if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
-          else atomicAdd(&a.ctr->err_frontier, 1ull);
-        }
-      }
-      if (ROUTE) {
-        const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out, route, dest, a.W);
-        if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
-      }
+      __syncthreads();
     }
-    __syncthreads();  // the window's LDS arrays are reused by the next window
+    PH_MARK(0);  // staging + event count + scan
+    // 3. the chunk's work items in windows of kWin, grouped by handler class (counting sort in
+    //    LDS) so that a wavefront mostly runs one handler; one lane per (parent, event)
+    for (int w0 = 0; w0 < total; w0 += kWin) {
+      const int wn = min(kWin, total - w0);
+      // 3a. (parent, handler class) of every item of the window: a team of TPP threads per
+      //     parent writes its events' entries (no search, no atomics)
+      {
+        const int tpp = pb > 128 ? 1 : pb > 64 ? 2 : pb > 32 ? 4 : pb > 16 ? 8 : pb > 8 ? 16 : 32;
+        const int j = tid / tpp, sub = tid - j * tpp;
+        if (j < pb) {
+          const int e0 = off[j];
+          const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
+          const uint32_t* w = rows + j * NW;
+          for (int q = lo + sub; q < hi; q += tpp) {
+            s_par[q - w0] = (uint8_t)j;
+            s_cls[q - w0] = (uint8_t)event_class<P>(w, prm, set, q - e0);
+          }
+        }
+      }
+      __syncthreads();
+#ifdef DSL_X2_CLASSIFY  // cost probe: the (parent, class) listing again
+      {
+        const int tpp = pb > 128 ? 1 : pb > 64 ? 2 : pb > 32 ? 4 : pb > 16 ? 8 : pb > 8 ? 16 : 32;
+        int j = tid / tpp;
+        asm volatile("" : "+v"(j));
+        const int sub = tid - j * tpp;
+        if (j < pb) {
+          const int e0 = off[j];
+          const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
+          const uint32_t* w = rows + j * NW;
+          for (int q = lo + sub; q < hi; q += tpp) s_cls[q - w0] = (uint8_t)event_class<P>(w, prm, set, q - e0);
+        }
+      }
+      __syncthreads();
+#endif
+      // 3b. class counts per 64-item group (ballots), bases in class-major order
+      const int ng = (wn + 63) >> 6;
+      for (int gr = wid; gr < ng; gr += NWAVE) {
+        const int t = gr * 64 + lane;
+        const int c = t < wn ? (int)s_cls[t] : -1;
+        int mine = 0;
+#pragma unroll
+        for (int q = 0; q < NC; q++) {
+          const int n = __popcll(__ballot(c == q));
+          if (lane == q) mine = n;
+        }
+        if (lane < NC) s_cbase[gr][lane] = mine;
+      }
+      __syncthreads();
+      if (tid < 64) {
+        int tot = 0;
+        if (lane < NC)
+          for (int gr = 0; gr < ng; gr++) tot += s_cbase[gr][lane];
+        int inc = tot;
+        for (int o = 1; o < 16; o <<= 1) {
+          const int y = __shfl_up(inc, o);
+          if (lane >= o) inc += y;
+        }
+        int run = inc - tot;
+        if (lane < NC)
+          for (int gr = 0; gr < ng; gr++) {
+            const int v = s_cbase[gr][lane];
+            s_cbase[gr][lane] = run;
+            run += v;
+          }
+      }
+      __syncthreads();
+      // 3c. the permutation: class base + rank among the group's lanes of the same class
+      for (int gr = wid; gr < ng; gr += NWAVE) {
+        const int t = gr * 64 + lane;
+        const int c = t < wn ? (int)s_cls[t] : -1;
+        int rank = 0;
+#pragma unroll
+        for (int q = 0; q < NC; q++) {
+          const unsigned long long mq = __ballot(c == q);
+          if (c == q) rank = __popcll(mq & ((1ull << lane) - 1ull));
+        }
+        if (t < wn) s_perm[s_cbase[gr][c] + rank] = (uint16_t)t;
+      }
+      __syncthreads();
+      PH_MARK(7);  // classify + sort
+      for (int base = 0; base < wn; base += kLevelBlock) {
+        const int t = base + tid;
+        bool is_valid = false, route = false;
+        int dest = 0, j = 0, k = 0, tv = 0, tpi = -1;
+        uint64_t tkey = ~0ull;  // terminal candidate
+        Fp f{0, 0};
+        Delta<P> d;
+        d.node = 0;
+        d.out.n = 0;
+        if (t < wn) {
+          const int u = s_perm[t];
+          j = s_par[u];
+          k = w0 + u - off[j];
+          const uint32_t* w = rows + j * NW;
+          const int rc = delta_step<P>(w, k, d, prm, set);
+#ifdef DSL_X2_HANDLER  // cost probe: the handler again (its result feeds a counter, so it runs)
+          {
+            int k2 = k;
+            asm volatile("" : "+v"(k2));
+            Delta<P> d2;
+            const int rc2 = delta_step<P>(w, k2, d2, prm, set);
+            if (rc2 == 77 || d2.out.n == 77 || d2.nw[0] == 0x7777777u) c_succ += 1000000u;
+          }
+#endif
+          PH_MARK(1);  // decode + handler + canonical sends
+          // an event that changes neither its node nor the network (a redelivered message most
+          // often) leads back to the parent, which is in the visited set: no probe
+          const bool noop = rc == STEP_OK && d.out.n == 0 && same_words<P::kNodeWords>(d.nw, w + d.node * P::kNodeWords);
+          if (rc == STEP_OK) c_succ++;
+          if (rc == STEP_OK && !noop) {
+            f = delta_fingerprint<P>(w, fps[j], d);
+#ifdef DSL_X2_FP  // cost probe: the fingerprint again
+            {
+              Fp pf = fps[j];
+              asm volatile("" : "+v"(pf.hi));
+              const Fp f2 = delta_fingerprint<P>(w, pf, d);
+              if (f2.lo == 0x7777777ull) c_succ += 1000000u;
+            }
+#endif
+            PH_MARK(2);  // fingerprint
+            if (ROUTE) dest = owner_of(f, a.W);
+            if (ROUTE && dest != a.me) {
+              route = true;
+            } else {
+              c_probe++;
+              const int ins = find ? INS_NEW : table_insert(a.table, f);
+#ifdef DSL_X2_PROBE  // cost probe: a second probe of the same bucket (finds the key: no CAS)
+              {
+                Fp f2 = f;
+                asm volatile("" : "+v"(f2.lo));
+                if (table_insert(a.table, f2) == 77) c_succ += 1000000u;
+              }
+#endif
+              PH_MARK(3);  // visited-table probe / insert
+              if (ins == INS_NEW) {
+                c_new++;
+                int pi = -1;
+                // the changed node's words go through LDS: a view pointing at the register array
+                // would take its address and push the whole delta into scratch
+                uint32_t* my_nw = s_nodew + tid * P::kNodeWords;
+#pragma unroll
+                for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+                const NodeView view{w, P::kNodeWords, d.node, my_nw};
+                const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
+#ifdef DSL_X2_JUDGE  // cost probe: the judge again
+                {
+                  int dep = a.depth, pi2 = -1;
+                  asm volatile("" : "+v"(dep));
+                  if (judge_view<P>(view, prm, set, dep, &pi2, a.incremental != 0) == 77) c_succ += 1000000u;
+                }
+#endif
+                if (v == V_VALID) {
+                  if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = !find;
+                  else atomicAdd(&a.ctr->err_overflow, 1ull);
+                } else if (v >= V_TERM_EXCEPTION) {
+                  tv = v;
+                  tpi = pi;
+                  tkey = term_key(v, f.hi);
+                }
+              } else if (ins == INS_FULL) {
+                atomicAdd(&a.ctr->err_table, 1ull);
+              }
+            }
+          } else if (rc == STEP_EXCEPTION) {
+            // exceptional states never equal another (Throwable identity): new and terminal
+            c_succ++;
+            c_new++;
+            tv = V_TERM_EXCEPTION;
+            tkey = term_key(V_TERM_EXCEPTION, fps[j].hi);
+          } else if (rc == STEP_OVERFLOW) {
+            atomicAdd(&a.ctr->err_overflow, 1ull);
+          }
+        }
+        PH_MARK(4);  // judge (+ divergence wait)
+        const bool term = tkey != ~0ull;
+        if (find) {
+          if (term && tkey == a.find_key) a.terms[0] = TerminalRec{tv, tpi, (uint32_t)k, 0u, p0 + j, tkey};
+        } else {
+          fold_terminals(term, tkey, tv, tpi, (uint32_t)k, p0 + j, a.ctr, a.terms, a.term_cap);
+        }
+        // a VALID successor reserves a row of its workgroup's segment (one returning atomic per
+        // wavefront), then the wavefront writes its rows cooperatively
+        const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
+        PH_MARK(5);  // terminal fold + reservation
+        const bool fits = is_valid && li < a.segcap;
+        const uint64_t idx = (uint64_t)seg * a.segcap + li;
+        if (fits) {
+          const uint32_t* w = rows + j * NW;
+          a.next_fp[idx] = f;
+          a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
+          a.next_event[idx] = (uint32_t)k;
+          c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
+        }
+        wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+        PH_MARK(6);  // history + row emission
+        // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
+        const bool spill = is_valid && !fits;
+        if (__ballot(spill)) {
+          const unsigned long long sidx = wave_reserve(&a.ctr->spilled, spill);
+          if (spill) {
+            if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
+            else atomicAdd(&a.ctr->err_frontier, 1ull);
+          }
+        }
+        if (ROUTE) {
+          const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out, route, dest, a.W);
+          if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
+        }
+      }
+      __syncthreads();  // the window's LDS arrays are reused by the next window
     }
     __syncthreads();  // LDS is reused by the next chunk
   }
@@ -476,6 +647,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   block_flush<kLevelBlock>(s_red, &a.ctr->new_states, c_new);
   block_flush<kLevelBlock>(s_red, &a.ctr->next_work, c_next_work);
   block_flush<kLevelBlock>(s_red, &a.ctr->work_items, c_work);
+  block_flush<kLevelBlock>(s_red, &a.ctr->probes, c_probe);
 }
 
 // Materializes spilled VALID states (already inserted, counted and judged) at next_size.
@@ -529,7 +701,7 @@ __global__ void k_seed(const uint32_t* init, const Fp* fp, typename P::Params pr
   }
 }
 
-// ---- multi-shard phases (see sharded_engine.hpp) -------------------------------------------------
+// ---- multi-shard phases (see bfs_engine.hpp) -------------------------------------------------
 struct ProbeArgs {
   const FpRec* in;
   uint64_t n;
@@ -592,6 +764,7 @@ struct MaterializeArgs {
   RouteCounters* rc;
   LevelCounters* ctr;
   TerminalRec* terms;
+  uint32_t term_cap;
 };
 
 template <class P>
@@ -603,8 +776,8 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
     const uint64_t i = base + threadIdx.x;
     bool ship = false;
-    int dest = 0;
-    uint64_t parent = 0;
+    int dest = 0, tv = 0, tpi = -1;
+    uint64_t parent = 0, tkey = ~0ull;
     int k = 0;
     Delta<P> d;
     Fp f{0, 0};
@@ -624,10 +797,12 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       if (v == V_VALID) {
         ship = true;
       } else if (v >= V_TERM_EXCEPTION) {
-        const unsigned long long slot = atomicAdd(&a.ctr->n_terminals, 1ull);
-        if (slot < kTermCap) a.terms[slot] = TerminalRec{v, pi, (uint32_t)k, 0u, parent, f.hi};
+        tv = v;
+        tpi = pi;
+        tkey = term_key(v, f.hi);
       }
     }
+    fold_terminals(tkey != ~0ull, tkey, tv, tpi, (uint32_t)k, parent, a.ctr, a.terms, a.term_cap);
     const unsigned long long idx = block_reserve(s_resv, a.rc->out, ship, dest, a.W);
     StateRec<P>* r = a.out + (uint64_t)dest * a.cap_s + idx;
     if (ship) {

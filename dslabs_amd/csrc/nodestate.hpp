@@ -16,6 +16,8 @@
 // share a fingerprint is ~ n^2 / 2^129 (each pair of distinct states differs in a non-empty
 // set of hashed components).
 #pragma once
+#include <type_traits>
+
 #include "common.hpp"
 #include "fingerprint.hpp"
 
@@ -214,11 +216,12 @@ DSL_HD int locate_event(const uint32_t* w, const typename P::Params& prm, const 
   return INT32_MIN;
 }
 
-// Handler class of event k (messages: P::msg_class, timers: 15).
+// Handler class of event k (messages: P::msg_class < P::kMsgClasses, timers: P::kMsgClasses).
 template <class P>
 DSL_HD int event_class(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
+  static_assert(P::kMsgClasses >= 1 && P::kMsgClasses < 16, "at most 15 message classes + the timer class");
   const int e = locate_event<P>(w, prm, set, k);
-  return e >= 0 ? P::msg_class(Net<P>::at(w, e)) : 15;
+  return e >= 0 ? P::msg_class(Net<P>::at(w, e)) : P::kMsgClasses;
 }
 
 // A successor as a delta of its parent.
@@ -438,9 +441,30 @@ void describe_event(const uint32_t* w, int k, const typename P::Params& prm, con
 // when pruned, Search.java:475). A predicate that reads neither the changed node nor the
 // network has the parent's value, so it is skipped with that outcome. tests/hostcheck checks
 // the incremental verdict against the full one on every generated successor.
+// A predicate reading the changed node is also unchanged when the words it reads are: the
+// protocol's pred_same(pr, old, new) says so (e.g. Multi-Paxos LOGS_CONSISTENT reads only the
+// servers' log words); without one, the node's words must all be equal.
+template <int N>
+DSL_HD bool same_words(const uint32_t* a, const uint32_t* b) {
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < N; i++) d |= a[i] ^ b[i];
+  return d == 0;
+}
+template <class P, class = void>
+struct PredSame {
+  static DSL_HD bool same(const DevPred&, const uint32_t* a, const uint32_t* b) { return same_words<P::kNodeWords>(a, b); }
+};
+template <class P>
+struct PredSame<P, std::void_t<decltype(&P::pred_same)>> {
+  static DSL_HD bool same(const DevPred& pr, const uint32_t* a, const uint32_t* b) { return P::pred_same(pr, a, b); }
+};
+
 template <class P>
 DSL_HD bool pred_unchanged(const DevPred& pr, const NodeView& v, bool incremental) {
-  return incremental && v.changed >= 0 && !((pr.reads >> v.changed) & 1u) && !(pr.reads >> 31);
+  if (!incremental || v.changed < 0 || (pr.reads >> 31)) return false;
+  if (!((pr.reads >> v.changed) & 1u)) return true;
+  return PredSame<P>::same(pr, v.base + v.changed * v.nw, v.over);
 }
 
 template <class P>

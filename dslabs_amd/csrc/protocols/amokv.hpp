@@ -23,6 +23,7 @@ namespace dsl {
 struct AmoKV {
   static constexpr int kMaxClients = 3, kMaxCmds = 3, kMaxKeys = 3, kMaxLen = 9, kTimerCap = 4;
   static constexpr int kNodes = 1 + kMaxClients, kNodeWords = 6, kNetCap = 24, kMaxSends = 1;
+  static constexpr int kMsgClasses = 2;  // handler classes of messages (message types 0..1); timers: class 2
   static constexpr int kRetry = 100;
   using Rec = uint64_t;
   using State = StateOf<AmoKV>;

@@ -15,6 +15,7 @@ namespace dsl {
 
 struct MiniTest {
   static constexpr int kNodes = 2, kNodeWords = 1, kNetCap = 4, kMaxSends = 2;
+  static constexpr int kMsgClasses = 2;  // handler classes of messages (Foo, Bar); timers: class 2
   using Rec = uint32_t;
   using State = StateOf<MiniTest>;
 

@@ -34,7 +34,11 @@ namespace dsl {
 
 struct MultiPaxos {
   static constexpr int kMaxServers = 3, kMaxClients = 2, kMaxCmds = 2, kSlots = 4, kMaxRound = 15;
-  static constexpr int kNodes = kMaxServers + kMaxClients, kNodeWords = 6, kNetCap = 64, kMaxSends = 16;
+  // kMaxSends: the most records one handler sends is 12 (P1b completing phase 1: a P2a to both
+  // other servers for each of the 4 slots, plus up to 4 replies from execute); a larger send
+  // list would be a hard STEP_OVERFLOW error, never a truncation.
+  static constexpr int kNodes = kMaxServers + kMaxClients, kNodeWords = 6, kNetCap = 64, kMaxSends = 12;
+  static constexpr int kMsgClasses = 8;  // handler classes of messages (message types 0..7); timers: class 8
   static constexpr int kTick = 100, kClientRetry = 100;
   using Rec = uint64_t;
   using State = StateOf<MultiPaxos>;
@@ -49,7 +53,7 @@ struct MultiPaxos {
   enum { M_REQUEST = 0, M_REPLY, M_P1A, M_P1B, M_P2A, M_P2B, M_DECISION, M_HEARTBEAT, T_TICK = 8, T_CLIENT = 9 };
   enum { EMPTY = 0, ACCEPTED = 1, CHOSEN = 2 };
 
-  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // Handler class of a message (< kMsgClasses; timers are class kMsgClasses): k_level groups a chunk's work items
   // by class so that the lanes of a wavefront run the same handler.
   static DSL_HD int msg_class(Rec r) { return m_type(r); }
   static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
@@ -95,6 +99,16 @@ struct MultiPaxos {
       if (s != from) out.send(msg(type, from, s, payload));
   }
 
+  // Workload parameters by client / command index. Selects, not array indexing: a run-time index
+  // into the kernel-argument struct makes the compiler copy it to scratch memory.
+  static DSL_HD int val(const Params& p, int c, int k) {
+    return c ? (k ? p.vals[1][1] : p.vals[1][0]) : (k ? p.vals[0][1] : p.vals[0][0]);
+  }
+  static DSL_HD int expect(const Params& p, int c, int k) {
+    return c ? (k ? p.expected[1][1] : p.expected[1][0]) : (k ? p.expected[0][1] : p.expected[0][0]);
+  }
+  static DSL_HD int ncmd(const Params& p, int c) { return c ? p.ncmds[1] : p.ncmds[0]; }
+
   // ---- application: the executed prefix ----------------------------------------------------------
   static DSL_HD int cmd_client(int cmd) { return (cmd - 1) >> 1; }
   static DSL_HD int cmd_seq(int cmd) { return ((cmd - 1) & 1) + 1; }
@@ -110,7 +124,7 @@ struct MultiPaxos {
       if (!cmd) continue;
       const int c = cmd_client(cmd), q = cmd_seq(cmd);
       if (last_seq[c] < q) {
-        seqv = res_push(seqv, p.vals[c][q - 1]);
+        seqv = res_push(seqv, val(p, c, q - 1));
         last_seq[c] = q;
       }
     }
@@ -125,7 +139,7 @@ struct MultiPaxos {
       if (cmd) {
         const int c = cmd_client(cmd), q = cmd_seq(cmd);
         if (last_seq[c] < q) {
-          seqv = res_push(seqv, p.vals[c][q - 1]);
+          seqv = res_push(seqv, val(p, c, q - 1));
           last_seq[c] = q;
           if (active(w)) out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)seqv << 2)));
         }
@@ -210,11 +224,11 @@ struct MultiPaxos {
   static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, Out& out) {
     int nres = get(w, 15, 2);
     const int res = get(w, 3, 12);
-    if (nres < p.ncmds[c] && res != 0) {
+    if (nres < ncmd(p, c) && res != 0) {
       put(w, 32 + 12 * nres, 12, res);
       nres++;
       put(w, 15, 2, nres);
-      if (nres < p.ncmds[c]) client_send(c, w, p, nres + 1, out);
+      if (nres < ncmd(p, c)) client_send(c, w, p, nres + 1, out);
     }
   }
 
@@ -388,36 +402,43 @@ struct MultiPaxos {
     return (int)((w[bit >> 5] >> (bit & 31)) & ((1u << width) - 1u));
   }
   static DSL_HD uint32_t entryd(const uint32_t* w, int slot) { return (uint32_t)getd(w, 32 + 16 * (slot - 1), 16); }
-  static DSL_HD int value_of(const Params& p, int cmd) { return cmd ? p.vals[cmd_client(cmd)][cmd_seq(cmd) - 1] : 0; }
+  static DSL_HD int value_of(const Params& p, int cmd) { return cmd ? val(p, cmd_client(cmd), cmd_seq(cmd) - 1) : 0; }
 
   // PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (slotValid, PaxosTest.java:215-322); MARKERS_VALID holds by
-  // construction (firstNonCleared() == 1, lastNonEmpty() = last non-EMPTY slot).
+  // construction (firstNonCleared() == 1, lastNonEmpty() = last non-EMPTY slot). The servers' log
+  // words are read once (independent LDS reads), then everything is register arithmetic.
   static DSL_HD int logs_consistent(const NodeView& v, const Params& p) {
-    int max_ne = 0;
-    for (int s = 0; s < p.servers; s++)
-      for (int k = 1; k <= kSlots; k++)
-        if (e_status(entryd(v.node(s), k)) != EMPTY && k > max_ne) max_ne = k;
-    for (int slot = 1; slot <= max_ne; slot++) {
-      bool is_chosen = false;
-      int chosen = 0;
-      for (int s = 0; s < p.servers; s++) {
-        const uint32_t e = entryd(v.node(s), slot);
+    uint32_t lw[kMaxServers][2];
+#pragma unroll
+    for (int s = 0; s < kMaxServers; s++) {
+      const uint32_t* w = v.node(s < p.servers ? s : 0);
+      lw[s][0] = s < p.servers ? w[1] : 0u;
+      lw[s][1] = s < p.servers ? w[2] : 0u;
+    }
+    bool ok = true;
+#pragma unroll
+    for (int slot = 1; slot <= kSlots; slot++) {
+      bool is_chosen = false, conflict = false;
+      int chosen = 0, count = 0;
+#pragma unroll
+      for (int s = 0; s < kMaxServers; s++) {
+        const uint32_t e = (lw[s][(slot - 1) >> 1] >> (16 * ((slot - 1) & 1))) & 0xffffu;
         if (e_status(e) == CHOSEN) {
           const int x = value_of(p, e_cmd(e));
-          if (is_chosen && x != chosen) return PV_FALSE;
+          conflict |= is_chosen && x != chosen;
           chosen = x;
           is_chosen = true;
         }
       }
-      if (!is_chosen) continue;
-      int count = 0;
-      for (int s = 0; s < p.servers; s++) {
-        const uint32_t e = entryd(v.node(s), slot);
+#pragma unroll
+      for (int s = 0; s < kMaxServers; s++) {
+        const uint32_t e = (lw[s][(slot - 1) >> 1] >> (16 * ((slot - 1) & 1))) & 0xffffu;
         if (e_status(e) != EMPTY && (e_status(e) != ACCEPTED || value_of(p, e_cmd(e)) == chosen)) count++;
       }
-      if (2 * count <= p.servers) return PV_FALSE;
+      // slots past the last non-empty one are empty everywhere: never chosen, never checked
+      ok &= !is_chosen || (!conflict && 2 * count > p.servers);
     }
-    return PV_TRUE;
+    return ok ? PV_TRUE : PV_FALSE;
   }
 
   // KVStoreWorkload.APPENDS_LINEARIZABLE (KVStoreWorkload.java:282-340)
@@ -430,7 +451,7 @@ struct MultiPaxos {
       for (int k = 0; k < nres; k++) {
         const uint32_t r = (uint32_t)getd(w, 32 + 12 * k, 12);
         const int len = r & 7;
-        if (len == 0 || (int)((r >> (3 + 2 * (len - 1))) & 3) != p.vals[c][k]) return PV_FALSE;  // endsWith
+        if (len == 0 || (int)((r >> (3 + 2 * (len - 1))) & 3) != val(p, c, k)) return PV_FALSE;  // endsWith
         all[n++] = r;
       }
     }
@@ -456,17 +477,17 @@ struct MultiPaxos {
           const uint32_t* w = v.node(p.servers + c);
           const int nres = getd(w, 15, 2);
           for (int k = 0; k < nres; k++)
-            if (p.expected[c][k] >= 0 && getd(w, 32 + 12 * k, 12) != p.expected[c][k]) return PV_FALSE;
+            if (expect(p, c, k) >= 0 && getd(w, 32 + 12 * k, 12) != expect(p, c, k)) return PV_FALSE;
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
         for (int c = 0; c < p.clients; c++)
-          if (getd(v.node(p.servers + c), 15, 2) < p.ncmds[c]) return PV_FALSE;
+          if (getd(v.node(p.servers + c), 15, 2) < ncmd(p, c)) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_DONE: {
         const int c = (int)pr.arg0 - p.servers;
         if (c < 0 || c >= p.clients) return PV_THREW;
-        return getd(v.node(p.servers + c), 15, 2) >= p.ncmds[c] ? PV_TRUE : PV_FALSE;
+        return getd(v.node(p.servers + c), 15, 2) >= ncmd(p, c) ? PV_TRUE : PV_FALSE;
       }
       case DSL_PRED_NONE_DECIDED:
         for (int c = 0; c < p.clients; c++)
@@ -486,6 +507,14 @@ struct MultiPaxos {
     }
   }
 
+  // Word-level read sets for the incremental check: a client predicate reads the client's
+  // result count (w0 bits 15-16) and results (w1); LOGS_CONSISTENT reads a server's log (w1-w2).
+  static DSL_HD bool pred_same(const DevPred& pr, const uint32_t* a, const uint32_t* b) {
+    if (pr.id == DSL_PRED_LOGS_CONSISTENT) return ((a[1] ^ b[1]) | (a[2] ^ b[2])) == 0;
+    if ((pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) || pr.id == DSL_PRED_APPENDS_LINEARIZABLE)
+      return (((a[0] ^ b[0]) & (3u << 15)) | (a[1] ^ b[1])) == 0;
+    return same_words<kNodeWords>(a, b);
+  }
   // Read sets (judge_view's incremental check): client predicates read client nodes only,
   // LOGS_CONSISTENT the servers only.
   static uint32_t pred_reads(const DevPred& pr, const Params& p) {

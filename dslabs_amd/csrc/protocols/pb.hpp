@@ -32,6 +32,7 @@ namespace dsl {
 struct PB {
   static constexpr int kMaxServers = 3, kMaxClients = 2, kMaxCmds = 3, kMaxKeys = 2, kTimerCap = 4;
   static constexpr int kNodes = 1 + kMaxServers + kMaxClients, kNodeWords = 3, kNetCap = 64, kMaxSends = 3;
+  static constexpr int kMsgClasses = 9;  // handler classes of messages (message types 0..8); timers: class 9
   static constexpr int kMaxView = 15;
   using Rec = uint64_t;
   using State = StateOf<PB>;

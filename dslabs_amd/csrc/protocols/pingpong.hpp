@@ -25,6 +25,7 @@ namespace dsl {
 struct PingPong {
   static constexpr int kMaxClients = 4, kMaxPings = 15, kRetryMillis = 10;
   static constexpr int kNodes = 1 + kMaxClients, kNodeWords = 5;
+  static constexpr int kMsgClasses = 2;  // handler classes of messages (PingRequest, PongReply); timers: class 2
   static constexpr int kNetCap = 2 * kMaxClients * kMaxPings, kMaxSends = 2;
   using Rec = uint32_t;
   using State = StateOf<PingPong>;
@@ -41,7 +42,7 @@ struct PingPong {
   static DSL_HD int rec_from(Rec r) { return rec_type(r) ? 0 : rec_client(r); }
   static DSL_HD int rec_to(Rec r) { return rec_type(r) ? rec_client(r) : 0; }
 
-  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // Handler class of a message (< kMsgClasses; timers are class kMsgClasses): k_level groups a chunk's work items
   // by class so that the lanes of a wavefront run the same handler.
   static DSL_HD int msg_class(Rec r) { return rec_type(r); }
   static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }

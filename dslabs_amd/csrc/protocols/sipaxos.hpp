@@ -26,6 +26,7 @@ namespace dsl {
 struct SIPaxos {
   static constexpr int kMaxP = 3, kMaxA = 5;
   static constexpr int kNodes = kMaxP + kMaxA, kNodeWords = 3, kNetCap = 48, kMaxSends = kMaxA;
+  static constexpr int kMsgClasses = 4;  // handler classes of messages (message types 0..3); timers: class 4
   using Rec = uint32_t;
   using State = StateOf<SIPaxos>;
 
@@ -44,7 +45,7 @@ struct SIPaxos {
   static DSL_HD int r_an(Rec r) { return (r >> 8) & 0xff; }
   static DSL_HD int r_av(Rec r) { return r & 3; }
 
-  // Handler class of a message (< 15; timers are class 15): k_level groups a chunk's work items
+  // Handler class of a message (< kMsgClasses; timers are class kMsgClasses): k_level groups a chunk's work items
   // by class so that the lanes of a wavefront run the same handler.
   static DSL_HD int msg_class(Rec r) { return r_type(r); }
   static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }

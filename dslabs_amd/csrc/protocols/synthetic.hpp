@@ -21,6 +21,7 @@ namespace dsl {
 struct Synthetic {
   static constexpr int kMaxNodes = 5;
   static constexpr int kNodes = kMaxNodes, kNodeWords = 2, kNetCap = kMaxNodes, kMaxSends = 1;
+  static constexpr int kMsgClasses = 1;  // handler classes of messages (Poke); timers: class 1
   static constexpr int kTimerMin = 1, kTimerMax = 100;
   using Rec = uint32_t;
   using State = StateOf<Synthetic>;

@@ -51,8 +51,7 @@ typedef enum {
   DSL_ERR_UNKNOWN_PROTOCOL = -6,
   DSL_ERR_UNKNOWN_PREDICATE = -7,
   DSL_ERR_COMM = -8,
-  DSL_ERR_NO_DEVICE = -9,
-  DSL_ERR_PROBE_LIMIT = -10       /* a visited-table probe sequence did not settle */
+  DSL_ERR_NO_DEVICE = -9
 } dsl_status;
 
 /* SearchResults.EndCondition (T/search/SearchResults.java:35-41), same order of priority. */
@@ -226,8 +225,8 @@ int dsl_human_readable_trace(dsl_engine* e, const dsl_event* trace, int32_t n, d
  * visited-table bucket line per successor probe, one bucket line written back + 12 bytes of
  * parent/event per newly discovered state, S bytes per successor appended to the next frontier. */
 typedef struct {
-  double expand_ms;          /* sum of k_expand durations */
-  double count_ms, scan_ms;  /* sum of k_count / scan durations */
+  double expand_ms;          /* sum of k_level durations (HIP events on the engine's stream) */
+  double exchange_ms;        /* host wall time of the multi-shard exchange phases (0 on one shard) */
   uint64_t expand_launches;
   uint64_t parents;          /* frontier states expanded */
   uint64_t work_items;       /* (state, event) pairs = successors generated */
@@ -237,6 +236,10 @@ typedef struct {
   uint32_t state_bytes;
   uint32_t world_size;
   uint64_t table_slots;
+  uint64_t terminal_finds;   /* levels whose best terminal was resolved by a find-mode re-run */
+  uint64_t sharded_levels;   /* levels expanded hash-sharded with an exchange (multi-shard) */
+  uint64_t probes;           /* visited-table probes: successors that are not no-ops (an event that
+                                changes neither its node nor the network leads back to its parent) */
 } dsl_stats;
 
 int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);

@@ -56,7 +56,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
-  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0;
+  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
@@ -78,6 +78,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         return 1;
       }
       const int d = n.depth + 1;
+      succ++;
       if (rc == STEP_EXCEPTION) {
         if ((int)per.size() <= d) per.resize(d + 1, 0);
         per[d]++;
@@ -85,6 +86,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         best = std::min(best, (int)V_TERM_EXCEPTION);
         continue;
       }
+      if (dl.out.n == 0 && same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords)) noop++;
       S t;
       if (!materialize<P>(n.s.w, dl, t.w)) {
         printf("{\"error\":\"overflow\"}\n");
@@ -128,7 +130,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
   }
-  printf("],\"states\":%llu", total);
+  printf("],\"states\":%llu,\"successors\":%lld,\"noop_successors\":%lld", total, succ, noop);
   if (first_term_parent >= 0) {
     std::vector<int> evs{first_term_event};
     for (long long id = first_term_parent; id > 0; id = parent[id].first) evs.push_back(parent[id].second);
