@@ -66,6 +66,7 @@ struct LevelCounters {
   unsigned long long n_term_rec;    // TerminalRec entries written (improvements of term_best)
   unsigned long long probes;        // visited-table probes (successors that are not no-ops)
   unsigned long long phase[8];      // DSL_PHASES builds only: shader cycles per k_level phase
+  unsigned long long phcls[32];     // DSL_PHASES: handler cycles per class [0, 16), wave-passes [16, 32)
 };
 
 // Phase timing (instrumented builds, -DDSL_PHASES): wave-level shader-clock deltas per phase of
@@ -74,7 +75,15 @@ struct LevelCounters {
 #define PH_DECL unsigned long long ph_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; unsigned long long ph_t = clock64();
 #define PH_MARK(i) do { const unsigned long long ph_n = clock64(); ph_acc[i] += ph_n - ph_t; ph_t = ph_n; } while (0)
 #define PH_FLUSH(red, ctr) do { for (int ph_i = 0; ph_i < 8; ph_i++) block_flush<kLevelBlock>(red, &(ctr)->phase[ph_i], __lane_id() == 0 ? ph_acc[ph_i] : 0ull); } while (0)
+#define PH_CLS_DECL __shared__ unsigned long long s_phcls[32]; if (threadIdx.x < 32) s_phcls[threadIdx.x] = 0;
+#define PH_CLS_T0 const unsigned long long ph_c0 = clock64();
+#define PH_CLS_ADD(cls, active) do { const unsigned long long ph_c1 = clock64(); if (__lane_id() == 0 && (active)) { atomicAdd(&s_phcls[(cls) & 15], ph_c1 - ph_c0); atomicAdd(&s_phcls[16 + ((cls) & 15)], 1ull); } } while (0)
+#define PH_CLS_FLUSH(ctr) do { __syncthreads(); if (threadIdx.x < 32 && s_phcls[threadIdx.x]) atomicAdd(&(ctr)->phcls[threadIdx.x], s_phcls[threadIdx.x]); } while (0)
 #else
+#define PH_CLS_DECL
+#define PH_CLS_T0
+#define PH_CLS_ADD(cls, active) do { } while (0)
+#define PH_CLS_FLUSH(ctr) do { } while (0)
 #define PH_DECL
 #define PH_MARK(i) do { } while (0)
 #define PH_FLUSH(red, ctr) do { } while (0)
@@ -342,6 +351,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
   uint32_t c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0, c_probe = 0;
   PH_DECL
+  PH_CLS_DECL
   if (a.qprev) {
     // queued level: this frontier is the previous level's segments; every workgroup derives the
     // table (and whether the queue stopped) from those counters, as the host does afterwards
@@ -515,7 +525,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         int dest = 0, j = 0, k = 0, tv = 0, tpi = -1;
         uint64_t tkey = ~0ull;  // terminal candidate
         Fp f{0, 0};
-        Delta<P> d;
+        Delta<P> d;  // the successor as a canonical delta of its parent
         d.node = 0;
         d.out.n = 0;
         if (t < wn) {
@@ -523,31 +533,50 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           j = s_par[u];
           k = w0 + u - off[j];
           const uint32_t* w = rows + j * NW;
-          const int rc = delta_step<P>(w, k, d, prm, set);
-#ifdef DSL_X2_HANDLER  // cost probe: the handler again (its result feeds a counter, so it runs)
-          {
-            int k2 = k;
-            asm volatile("" : "+v"(k2));
-            Delta<P> d2;
-            const int rc2 = delta_step<P>(w, k2, d2, prm, set);
-            if (rc2 == 77 || d2.out.n == 77 || d2.nw[0] == 0x7777777u) c_succ += 1000000u;
-          }
-#endif
-          PH_MARK(1);  // decode + handler + canonical sends
+          uint32_t* my_nw = s_nodew + tid * P::kNodeWords;  // the changed node's words, for the judge
+          int rc, dnode = 0, dn = 0;
+          bool noop = false;
           // an event that changes neither its node nor the network (a redelivered message most
           // often) leads back to the parent, which is in the visited set: no probe
-          const bool noop = rc == STEP_OK && d.out.n == 0 && same_words<P::kNodeWords>(d.nw, w + d.node * P::kNodeWords);
-          if (rc == STEP_OK) c_succ++;
-          if (rc == STEP_OK && !noop) {
-            f = delta_fingerprint<P>(w, fps[j], d);
-#ifdef DSL_X2_FP  // cost probe: the fingerprint again
+          {
+            PH_CLS_T0
+#ifdef DSL_X2_HSEQ  // cost probe: the handler twice in sequence (the first result dead but needed)
             {
-              Fp pf = fps[j];
-              asm volatile("" : "+v"(pf.hi));
-              const Fp f2 = delta_fingerprint<P>(w, pf, d);
-              if (f2.lo == 0x7777777ull) c_succ += 1000000u;
+              int k2 = k;
+              asm volatile("" : "+v"(k2));
+              const int r0 = delta_step<P>(w, k2, d, prm, set);
+              k2 = k + (r0 == 77 ? 1 : 0) + (d.out.n == 77 ? 1 : 0);
+              asm volatile("" : "+v"(k2));
+              k = k2;
             }
 #endif
+            rc = delta_step<P>(w, k, d, prm, set);
+            PH_CLS_ADD(s_cls[u], true);
+            PH_MARK(1);  // decode + handler + canonical sends
+            if (rc == STEP_OK) {
+              dnode = d.node;
+              dn = d.out.n;
+              noop = dn == 0 && same_words<P::kNodeWords>(d.nw, w + dnode * P::kNodeWords);
+              if (!noop) {
+                f = delta_fingerprint<P>(w, fps[j], d);
+                // the changed node's words go through LDS: a view pointing at the register
+                // array would take its address and push the whole delta into scratch
+#pragma unroll
+                for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+              }
+            }
+          }
+#ifdef DSL_X2_FP  // cost probe: the fingerprint again
+          if (rc == STEP_OK && !noop) {
+            Fp pf = fps[j];
+            asm volatile("" : "+v"(pf.hi));
+            Fp f2 = fp_xor(pf, node_hash<P>(dnode, w + dnode * P::kNodeWords));
+            f2 = fp_xor(f2, node_hash<P>(dnode, my_nw));
+            if (f2.lo == 0x7777777ull) c_succ += 1000000u;
+          }
+#endif
+          if (rc == STEP_OK) c_succ++;
+          if (rc == STEP_OK && !noop) {
             PH_MARK(2);  // fingerprint
             if (ROUTE) dest = owner_of(f, a.W);
             if (ROUTE && dest != a.me) {
@@ -566,12 +595,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               if (ins == INS_NEW) {
                 c_new++;
                 int pi = -1;
-                // the changed node's words go through LDS: a view pointing at the register array
-                // would take its address and push the whole delta into scratch
-                uint32_t* my_nw = s_nodew + tid * P::kNodeWords;
-#pragma unroll
-                for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
-                const NodeView view{w, P::kNodeWords, d.node, my_nw};
+                const NodeView view{w, P::kNodeWords, dnode, my_nw};
                 const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
 #ifdef DSL_X2_JUDGE  // cost probe: the judge again
                 {
@@ -581,7 +605,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
                 }
 #endif
                 if (v == V_VALID) {
-                  if (Net<P>::size(w) + d.out.n <= P::kNetCap) is_valid = !find;
+                  if (Net<P>::size(w) + dn <= P::kNetCap) is_valid = !find;
                   else atomicAdd(&a.ctr->err_overflow, 1ull);
                 } else if (v >= V_TERM_EXCEPTION) {
                   tv = v;
@@ -609,28 +633,30 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         } else {
           fold_terminals(term, tkey, tv, tpi, (uint32_t)k, p0 + j, a.ctr, a.terms, a.term_cap);
         }
-        // a VALID successor reserves a row of its workgroup's segment (one returning atomic per
-        // wavefront), then the wavefront writes its rows cooperatively
-        const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
-        PH_MARK(5);  // terminal fold + reservation
-        const bool fits = is_valid && li < a.segcap;
-        const uint64_t idx = (uint64_t)seg * a.segcap + li;
-        if (fits) {
-          const uint32_t* w = rows + j * NW;
-          a.next_fp[idx] = f;
-          a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
-          a.next_event[idx] = (uint32_t)k;
-          c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
-        }
-        wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
-        PH_MARK(6);  // history + row emission
-        // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
-        const bool spill = is_valid && !fits;
-        if (__ballot(spill)) {
-          const unsigned long long sidx = wave_reserve(&a.ctr->spilled, spill);
-          if (spill) {
-            if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
-            else atomicAdd(&a.ctr->err_frontier, 1ull);
+        {
+          // a VALID successor reserves a row of its workgroup's segment (one returning atomic per
+          // wavefront), then the wavefront writes its rows cooperatively
+          const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
+          PH_MARK(5);  // terminal fold + reservation
+          const bool fits = is_valid && li < a.segcap;
+          const uint64_t idx = (uint64_t)seg * a.segcap + li;
+          if (fits) {
+            const uint32_t* w = rows + j * NW;
+            a.next_fp[idx] = f;
+            a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
+            a.next_event[idx] = (uint32_t)k;
+            c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
+          }
+          wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+          PH_MARK(6);  // history + row emission
+          // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
+          const bool spill = is_valid && !fits;
+          if (__ballot(spill)) {
+            const unsigned long long sidx = wave_reserve(&a.ctr->spilled, spill);
+            if (spill) {
+              if (sidx < a.spill_cap) a.spill[sidx] = ((p0 + j) << 20) | (uint64_t)k;
+              else atomicAdd(&a.ctr->err_frontier, 1ull);
+            }
           }
         }
         if (ROUTE) {
@@ -643,6 +669,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     __syncthreads();  // LDS is reused by the next chunk
   }
   PH_FLUSH(s_red, a.ctr);
+  PH_CLS_FLUSH(a.ctr);
   block_flush<kLevelBlock>(s_red, &a.ctr->successors, c_succ);
   block_flush<kLevelBlock>(s_red, &a.ctr->new_states, c_new);
   block_flush<kLevelBlock>(s_red, &a.ctr->next_work, c_next_work);

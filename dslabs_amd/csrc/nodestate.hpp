@@ -81,6 +81,13 @@ struct Net {
   }
 };
 
+// P::kSendsDistinct: no handler of P sends one record twice in one step (tests/hostcheck checks
+// it on every explored step), so Sender needs no duplicate check.
+template <class P, class = void>
+struct SendsDistinct : std::false_type {};
+template <class P>
+struct SendsDistinct<P, std::void_t<decltype(P::kSendsDistinct)>> : std::integral_constant<bool, P::kSendsDistinct> {};
+
 // Sends emitted by one handler invocation (duplicates collapse, as in the network set).
 // Every access to r[] uses a compile-time index (fully unrolled loops predicated on i < n), so
 // the list lives in VGPRs; a dynamically indexed per-lane array would be placed in scratch and
@@ -93,11 +100,13 @@ struct Sender {
   bool overflow = false;
   Rec r[K];
   DSL_HD void send(Rec x) {
-    bool dup = false;
+    if constexpr (!SendsDistinct<P>::value) {
+      bool dup = false;
 #pragma unroll
-    for (int i = 0; i < K; i++)
-      if (i < n && r[i] == x) dup = true;
-    if (dup) return;
+      for (int i = 0; i < K; i++)
+        if (i < n && r[i] == x) dup = true;
+      if (dup) return;
+    }
     if (n >= K) {
       overflow = true;
       return;
@@ -243,6 +252,13 @@ DSL_HD void canon_sends(const uint32_t* w, Delta<P>& d) {
   for (int i = 0; i < K; i++) {
     if (i < n) {
       const auto x = d.out.r[i];
+#ifdef DSL_X2_CONTAINS  // cost probe (tools/gpu_r02_x2.sh): the membership test again
+      {
+        auto x2 = x;
+        asm volatile("" : "+v"(x2));
+        if (Net<P>::contains(w, x2)) d.out.overflow |= (x2 == 0x77);
+      }
+#endif
       if (!Net<P>::contains(w, x)) {
         bool done = false;
 #pragma unroll
@@ -268,6 +284,13 @@ DSL_HD void canon_sends(const uint32_t* w, Delta<P>& d) {
 template <class P>
 DSL_HD int delta_step(const uint32_t* w, int k, Delta<P>& d, const typename P::Params& prm, const DevSettings& set) {
   const int e = locate_event<P>(w, prm, set, k);
+#ifdef DSL_X2_LOCATE  // cost probe: locating the event again
+  {
+    int k2 = k;
+    asm volatile("" : "+v"(k2));
+    if (locate_event<P>(w, prm, set, k2) == 0x777777) d.out.overflow = true;
+  }
+#endif
   if (e == INT32_MIN) return STEP_NULL;
   d.out.n = 0;
   d.out.overflow = false;
@@ -297,6 +320,16 @@ DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
 #pragma unroll
   for (int j = 0; j < P::kMaxSends; j++)
     if (j < d.out.n) f = fp_xor(f, msg_hash<P>(d.out.r[j]));  // canonical: all new
+#ifdef DSL_X2_MSGHASH  // cost probe: the record hashes again
+  Fp g{0, 0};
+#pragma unroll
+  for (int j = 0; j < P::kMaxSends; j++) {
+    auto x = d.out.r[j];
+    asm volatile("" : "+v"(x));
+    if (j < d.out.n) g = fp_xor(g, msg_hash<P>(x));
+  }
+  if (g.lo == 0x777) f.hi ^= 1;
+#endif
   return f;
 }
 

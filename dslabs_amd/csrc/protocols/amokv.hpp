@@ -65,7 +65,8 @@ struct AmoKV {
   static DSL_HD uint32_t r_value(uint32_t r) { return r >> 2; }
 
   // ---- server --------------------------------------------------------------------------------
-  static DSL_HD int server_request(uint32_t* w, Rec m, Sender<AmoKV>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int server_request(uint32_t* w, Rec m, O& out, const Params& p) {
     const int c = rec_from(m) - 1, seq = m_seq(m);
     if (c < 0 || c >= p.clients || seq < 1 || seq > p.ncmds) return STEP_EXCEPTION;
     const uint32_t amo = sel_word<kNodeWords>(w, 3 + c);
@@ -109,7 +110,8 @@ struct AmoKV {
     return true;
   }
   // SimpleClient.sendCommand: seq++, Request(cmd, seq) to the server, ClientTimer(seq)
-  static DSL_HD bool send_command(int i, uint32_t* w, Sender<AmoKV>& out) {
+  template <class O>
+  static DSL_HD bool send_command(int i, uint32_t* w, O& out) {
     const int seq = seq_of(w) + 1;
     put(w, 0, 2, seq);
     put(w, 2, 1, 0);
@@ -118,7 +120,8 @@ struct AmoKV {
     return push_timer(w, seq);
   }
   // ClientWorker.sendNextCommandWhilePossible: harvest the result, then the next command
-  static DSL_HD bool worker_continue(int i, uint32_t* w, Sender<AmoKV>& out, const Params& p) {
+  template <class O>
+  static DSL_HD bool worker_continue(int i, uint32_t* w, O& out, const Params& p) {
     int n = nres(w);
     if (n < seq_of(w) && has_result(w)) {  // waiting on a result and the client has one
       sel_put<kNodeWords>(w, 2 + n, w[1]);
@@ -131,13 +134,15 @@ struct AmoKV {
 
   // ---- protocol interface -------------------------------------------------------------------------
   static DSL_HD int num_nodes(const Params& p) { return 1 + p.clients; }
-  static DSL_HD void init_node(int i, uint32_t* w, Sender<AmoKV>& out, const Params& p) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {
     if (i > 0 && !worker_continue(i, w, out, p)) out.overflow = true;
   }
   // ClientTimers are all (100, 100): only the head of the queue is deliverable
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params&) { return i > 0 && ntim(w) > 0; }
 
-  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Sender<AmoKV>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params& p) {
     if (i == 0) {
       if (m_type(m) != M_REQUEST) return STEP_EXCEPTION;
       return server_request(w, m, out, p);
@@ -149,7 +154,8 @@ struct AmoKV {
     }
     return worker_continue(i, w, out, p) ? STEP_OK : STEP_OVERFLOW;
   }
-  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<AmoKV>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int, O& out, const Params& p) {
     const int t = timer(w, 0);
     if (nres(w) < seq_of(w) && !has_result(w) && t == seq_of(w)) {  // onClientTimer: re-send, re-set
       out.send(msg(M_REQUEST, i, 0, t, 0));

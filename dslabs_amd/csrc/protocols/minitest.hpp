@@ -33,7 +33,8 @@ struct MiniTest {
   static DSL_HD int msg_class(Rec r) { return rec_type(r); }
 
   static DSL_HD int num_nodes(const Params&) { return 2; }
-  static DSL_HD void init_node(int i, uint32_t* w, Sender<MiniTest>& out, const Params&) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params&) {
     w[0] = 0;
     if (i == 0) {  // A.init: send(new Foo(), b) twice
       out.send(rec(M_FOO, 0, 1));
@@ -41,9 +42,11 @@ struct MiniTest {
     }
   }
   static DSL_HD int num_timer_events(int, const uint32_t*, const Params&) { return 0; }
-  static DSL_HD int on_timer(int, uint32_t*, int, Sender<MiniTest>&, const Params&) { return STEP_EXCEPTION; }
+  template <class O>
+  static DSL_HD int on_timer(int, uint32_t*, int, O&, const Params&) { return STEP_EXCEPTION; }
 
-  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Sender<MiniTest>& out, const Params&) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params&) {
     if (i == 0) {
       if (rec_type(m) == M_FOO) return STEP_EXCEPTION;  // A.handleFoo: throw new RuntimeException()
       w[0] = 1;                                         // A.handleBar: foo = true

@@ -30,6 +30,7 @@
 #pragma once
 #include "../nodestate.hpp"
 
+
 namespace dsl {
 
 struct MultiPaxos {
@@ -39,10 +40,13 @@ struct MultiPaxos {
   // list would be a hard STEP_OVERFLOW error, never a truncation.
   static constexpr int kNodes = kMaxServers + kMaxClients, kNodeWords = 6, kNetCap = 64, kMaxSends = 12;
   static constexpr int kMsgClasses = 8;  // handler classes of messages (message types 0..7); timers: class 8
+  // No handler sends one record twice in one step (broadcasts go to distinct servers, execute
+  // replies once per newly executed command, become_leader proposes each slot once), so Sender
+  // skips its duplicate check; tests/hostcheck checks distinctness on every explored step.
+  static constexpr bool kSendsDistinct = true;
   static constexpr int kTick = 100, kClientRetry = 100;
   using Rec = uint64_t;
   using State = StateOf<MultiPaxos>;
-  using Out = Sender<MultiPaxos>;
 
   struct Params {
     int32_t servers, clients;
@@ -94,7 +98,8 @@ struct MultiPaxos {
   static DSL_HD uint64_t ballot_field(int b) { return (uint64_t)(b >> 2) | ((uint64_t)(b & 3) << 4); }
   static DSL_HD int m_ballot(Rec m) { return (int)(((m & 0xf) << 2) | ((m >> 4) & 3)); }
 
-  static DSL_HD void bcast_servers(int from, const Params& p, int type, uint64_t payload, Out& out) {
+  template <class O>
+  static DSL_HD void bcast_servers(int from, const Params& p, int type, uint64_t payload, O& out) {
     for (int s = 0; s < p.servers; s++)
       if (s != from) out.send(msg(type, from, s, payload));
   }
@@ -116,35 +121,66 @@ struct MultiPaxos {
     int len = r & 7;
     return (uint32_t)(len + 1) | (r & ~7u) | ((uint32_t)v << (3 + 2 * len));
   }
+  // The executed prefix: the key's value (append sequence) after slots [1, upto) and each client's
+  // last executed sequence number. Fixed trip counts over the kSlots slots: the loops unroll and
+  // every log access has a constant bit offset (no select chains over the node words).
   static DSL_HD uint32_t executed(const uint32_t* w, const Params& p, int upto, int* last_seq) {
     uint32_t seqv = 0;
-    for (int c = 0; c < kMaxClients; c++) last_seq[c] = 0;
-    for (int slot = 1; slot < upto; slot++) {
+    int ls0 = 0, ls1 = 0;
+#pragma unroll
+    for (int slot = 1; slot <= kSlots; slot++) {
       const int cmd = e_cmd(entry(w, slot));
-      if (!cmd) continue;
       const int c = cmd_client(cmd), q = cmd_seq(cmd);
-      if (last_seq[c] < q) {
+      if (slot < upto && cmd && (c ? ls1 : ls0) < q) {
         seqv = res_push(seqv, val(p, c, q - 1));
-        last_seq[c] = q;
+        if (c) ls1 = q;
+        else ls0 = q;
       }
     }
+    last_seq[0] = ls0;
+    last_seq[1] = ls1;
     return seqv;
   }
-  static DSL_HD void execute(int s, uint32_t* w, const Params& p, Out& out) {
-    int last_seq[kMaxClients];
-    int so = slot_out(w);
-    uint32_t seqv = executed(w, p, so, last_seq);
-    while (so <= kSlots && e_status(entry(w, so)) == CHOSEN) {
-      const int cmd = e_cmd(entry(w, so));
-      if (cmd) {
-        const int c = cmd_client(cmd), q = cmd_seq(cmd);
-        if (last_seq[c] < q) {
-          seqv = res_push(seqv, val(p, c, q - 1));
-          last_seq[c] = q;
-          if (active(w)) out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)seqv << 2)));
-        }
+  // The result a client got for command (c0, q0): the value right after it executed.
+  static DSL_HD uint32_t result_of(const uint32_t* w, const Params& p, int upto, int c0, int q0) {
+    uint32_t seqv = 0, r = 0;
+    int ls0 = 0, ls1 = 0;
+#pragma unroll
+    for (int slot = 1; slot <= kSlots; slot++) {
+      const int cmd = e_cmd(entry(w, slot));
+      const int c = cmd_client(cmd), q = cmd_seq(cmd);
+      if (slot < upto && cmd && (c ? ls1 : ls0) < q) {
+        seqv = res_push(seqv, val(p, c, q - 1));
+        if (c) ls1 = q;
+        else ls0 = q;
+        if (c == c0 && q == q0) r = seqv;
       }
-      so++;
+    }
+    return r;
+  }
+  // Executes the chosen slots from slotOut on, in order (replies from an active leader).
+  template <class O>
+  static DSL_HD void execute(int s, uint32_t* w, const Params& p, O& out) {
+    const int so0 = slot_out(w);
+    const bool act = active(w);
+    uint32_t seqv = 0;
+    int ls0 = 0, ls1 = 0, so = so0;
+    bool run = true;  // every slot from slotOut to here is chosen
+#pragma unroll
+    for (int slot = 1; slot <= kSlots; slot++) {
+      const uint32_t e = entry(w, slot);
+      const int cmd = e_cmd(e);
+      const int c = cmd_client(cmd), q = cmd_seq(cmd);
+      const bool before = slot < so0;
+      const bool now = !before && run && e_status(e) == CHOSEN;
+      run = run && (before || now);
+      if ((before || now) && cmd && (c ? ls1 : ls0) < q) {
+        seqv = res_push(seqv, val(p, c, q - 1));
+        if (c) ls1 = q;
+        else ls0 = q;
+        if (now && act) out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)seqv << 2)));
+      }
+      if (now) so = slot + 1;
     }
     put(w, 14, 3, so);
   }
@@ -159,14 +195,16 @@ struct MultiPaxos {
     }
   }
   static DSL_HD bool majority(const Params& p, int votes) { return __builtin_popcount(votes) * 2 > p.servers; }
-  static DSL_HD void choose(int s, uint32_t* w, const Params& p, int slot, Out& out) {
+  template <class O>
+  static DSL_HD void choose(int s, uint32_t* w, const Params& p, int slot, O& out) {
     const int cmd = e_cmd(entry(w, slot));
     set_entry(w, slot, mk_entry(CHOSEN, 0, cmd));
     set_votes2(w, slot, 0);
     bcast_servers(s, p, M_DECISION, (uint64_t)slot | ((uint64_t)cmd << 3), out);
     execute(s, w, p, out);
   }
-  static DSL_HD void propose(int s, uint32_t* w, const Params& p, int slot, int cmd, Out& out) {
+  template <class O>
+  static DSL_HD void propose(int s, uint32_t* w, const Params& p, int slot, int cmd, O& out) {
     const int b = cmp_ballot(w);
     set_entry(w, slot, mk_entry(ACCEPTED, b, cmd));
     set_votes2(w, slot, 1 << s);
@@ -181,7 +219,8 @@ struct MultiPaxos {
       set_p1entry(w, slot, e);
     }
   }
-  static DSL_HD void become_leader(int s, uint32_t* w, const Params& p, Out& out) {
+  template <class O>
+  static DSL_HD void become_leader(int s, uint32_t* w, const Params& p, O& out) {
     put(w, 6, 1, 1);   // active
     put(w, 7, 1, 0);   // electing
     put(w, 11, 3, 0);  // p1bVotes
@@ -207,7 +246,8 @@ struct MultiPaxos {
   }
 
   // ---- clients (PaxosClient inside a ClientWorker) ------------------------------------------------
-  static DSL_HD void client_send(int c, uint32_t* w, const Params& p, int q, Out& out) {
+  template <class O>
+  static DSL_HD void client_send(int c, uint32_t* w, const Params& p, int q, O& out) {
     put(w, 0, 2, q);
     put(w, 2, 1, 1);
     put(w, 3, 12, 0);
@@ -221,7 +261,8 @@ struct MultiPaxos {
     put(w, 19 + 2 * n, 2, q);
     put(w, 17, 2, n + 1);
   }
-  static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, Out& out) {
+  template <class O>
+  static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, O& out) {
     int nres = get(w, 15, 2);
     const int res = get(w, 3, 12);
     if (nres < ncmd(p, c) && res != 0) {
@@ -234,7 +275,8 @@ struct MultiPaxos {
 
   // ---- protocol interface -------------------------------------------------------------------------
   static DSL_HD int num_nodes(const Params& p) { return p.servers + p.clients; }
-  static DSL_HD void init_node(int i, uint32_t* w, Out& out, const Params& p) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {
     if (i < p.servers) {
       put(w, 14, 3, 1);
       put(w, 17, 3, 1);
@@ -247,7 +289,8 @@ struct MultiPaxos {
     return i < p.servers ? 1 : (get(w, 17, 2) > 0);
   }
 
-  static DSL_HD int on_timer(int i, uint32_t* w, int, Out& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int, O& out, const Params& p) {
     if (i >= p.servers) {  // ClientTimer at the head: onClientTimer, ClientWorker loop, remove head
       const int c = i - p.servers;
       const int t = get(w, 19, 2);
@@ -295,7 +338,8 @@ struct MultiPaxos {
     return STEP_OK;
   }
 
-  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Out& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params& p) {
     const int type = m_type(m), from = rec_from(m);
     if (i >= p.servers) {  // PaxosClient.handlePaxosReply, then the ClientWorker loop
       if (type != M_REPLY) return STEP_EXCEPTION;
@@ -314,12 +358,7 @@ struct MultiPaxos {
       executed(w, p, slot_out(w), last_seq);
       if (last_seq[c] >= q) {  // AMO: already executed; an active leader replies from the cache
         if (active(w) && last_seq[c] == q) {
-          int ls2[kMaxClients];
-          uint32_t r = 0;
-          for (int upto = 1; upto <= slot_out(w); upto++) {
-            r = executed(w, p, upto, ls2);
-            if (ls2[c] == q) break;
-          }
+          const uint32_t r = result_of(w, p, slot_out(w), c, q);
           out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)r << 2)));
         }
         return STEP_OK;

@@ -105,13 +105,15 @@ struct PB {
     put(w, 8, 1, 0);
     return true;
   }
-  static DSL_HD int vs_reply(uint32_t* w, int to, Sender<PB>& out) {
+  template <class O>
+  static DSL_HD int vs_reply(uint32_t* w, int to, O& out) {
     const int view = get(w, 0, 8);
     if (v_num(view) > get(w, 15, 4)) put(w, 15, 4, v_num(view));
     out.send(msg(M_VIEWREPLY, 0, to, (uint64_t)view));
     return STEP_OK;
   }
-  static DSL_HD int vs_ping(uint32_t* w, int from, int n, Sender<PB>& out, const Params& prm) {
+  template <class O>
+  static DSL_HD int vs_ping(uint32_t* w, int from, int n, O& out, const Params& prm) {
     put(w, 9, 3, get(w, 9, 3) | (1 << (from - 1)));
     int view = get(w, 0, 8);
     if (v_num(view) == 0) {  // any server may be the first primary
@@ -147,7 +149,8 @@ struct PB {
   }
 
   // ---- PBServer ---------------------------------------------------------------------------------------
-  static DSL_HD int server_msg(int me, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int server_msg(int me, uint32_t* w, Rec m, O& out, const Params& p) {
     const int type = m_type(m), from = rec_from(m);
     const int view = get(w, 0, 8), P = v_p(view), B = v_b(view);
     const bool primary = P == me, started = get(w, 8, 1);
@@ -236,12 +239,14 @@ struct PB {
     put(w, 11, 3, n + 1);
     return true;
   }
-  static DSL_HD void send_request(int me, const uint32_t* w, Sender<PB>& out) {
+  template <class O>
+  static DSL_HD void send_request(int me, const uint32_t* w, O& out) {
     const int primary = get(w, 4, 2);
     if (primary) out.send(msg(M_REQUEST, me, primary, (uint64_t)seq_of(w)));
     else out.send(msg(M_GETVIEW, me, 0, 0));
   }
-  static DSL_HD bool worker_continue(int me, uint32_t* w, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD bool worker_continue(int me, uint32_t* w, O& out, const Params& p) {
     int n = nres(w);
     if (n < seq_of(w) && has_result(w)) {
       set_result_at(w, n, get(w, 32, 10));
@@ -257,7 +262,8 @@ struct PB {
     }
     return true;
   }
-  static DSL_HD int client_msg(int me, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int client_msg(int me, uint32_t* w, Rec m, O& out, const Params& p) {
     const bool waiting = seq_of(w) > 0 && !has_result(w);
     if (m_type(m) == M_VIEWREPLY) {
       const int v = (int)(m & 0xff);
@@ -280,7 +286,8 @@ struct PB {
   // ---- protocol interface -------------------------------------------------------------------------
   static DSL_HD int num_nodes(const Params& p) { return 1 + p.servers + p.clients; }
   static DSL_HD bool is_client(int i, const Params& p) { return i > p.servers; }
-  static DSL_HD void init_node(int i, uint32_t* w, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {
     if (i == 0) return;                                           // set(PingCheckTimer): constant queue
     if (!is_client(i, p)) {
       out.send(msg(M_PING, i, 0, 0));                             // Ping(STARTUP_VIEWNUM); set(PingTimer)
@@ -291,7 +298,8 @@ struct PB {
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {
     return is_client(i, p) ? (ntim(w) > 0) : 1;
   }
-  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params& p) {
     if (i == 0) {
       if (m_type(m) == M_GETVIEW) return vs_reply(w, rec_from(m), out);
       if (m_type(m) != M_PING) return STEP_EXCEPTION;
@@ -302,7 +310,8 @@ struct PB {
     if (!is_client(i, p)) return server_msg(i, w, m, out, p);
     return client_msg(i, w, m, out, p);
   }
-  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<PB>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int, O& out, const Params& p) {
     if (i == 0) return vs_check(w, p);
     if (!is_client(i, p)) {  // PingTimer: the latest view, unless primary of a view not yet started
       const int view = get(w, 0, 8);

@@ -54,7 +54,8 @@ struct PingPong {
   static DSL_HD int result(const uint32_t* w, int j) { return get(w, 32 + 4 * j, 4); }
   static DSL_HD int timer(const uint32_t* w, int j) { return get(w, 96 + 4 * j, 4); }
 
-  static DSL_HD void push_timer(uint32_t* w, int v, Sender<PingPong>& out) {
+  template <class O>
+  static DSL_HD void push_timer(uint32_t* w, int v, O& out) {
     const int n = ntim(w);
     if (n >= kMaxPings) {
       out.overflow = true;
@@ -64,14 +65,16 @@ struct PingPong {
     put(w, 12, 4, n + 1);
   }
   // PingClient.sendCommand: ping = p, pong = null, send PingRequest, set PingTimer(10 ms).
-  static DSL_HD void send_command(int c, uint32_t* w, int v, Sender<PingPong>& out) {
+  template <class O>
+  static DSL_HD void send_command(int c, uint32_t* w, int v, O& out) {
     put(w, 0, 4, v);
     put(w, 4, 4, 0);
     out.send(rec(0, c, v));
     push_timer(w, v, out);
   }
   // ClientWorker.sendNextCommandWhilePossible; waitingOnResult == (nres < pings).
-  static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, Sender<PingPong>& out) {
+  template <class O>
+  static DSL_HD void client_worker_continue(int c, uint32_t* w, const Params& p, O& out) {
     int n = nres(w);
     if (n < p.pings && pong(w) != 0) {
       put(w, 32 + 4 * n, 4, pong(w));
@@ -82,13 +85,15 @@ struct PingPong {
   }
 
   static DSL_HD int num_nodes(const Params& p) { return 1 + p.clients; }
-  static DSL_HD void init_node(int i, uint32_t* w, Sender<PingPong>& out, const Params& p) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {
     if (i > 0) send_command(i, w, 1, out);  // ClientWorker.init -> first command
   }
   // TimerQueue.deliverable(): all PingTimers are (10,10): only the head is deliverable.
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params&) { return i > 0 && ntim(w) > 0; }
 
-  static DSL_HD int on_message(int i, uint32_t* w, Rec r, Sender<PingPong>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec r, O& out, const Params& p) {
     if (i == 0) {  // PingServer.handlePingRequest: reply Pong(value) to the sender
       if (rec_type(r) != 0) return STEP_EXCEPTION;
       out.send(rec(1, rec_client(r), rec_value(r)));
@@ -101,7 +106,8 @@ struct PingPong {
     return STEP_OK;
   }
   // PingClient.onPingTimer, the ClientWorker loop, then remove the first equal timer (the head).
-  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<PingPong>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int, O& out, const Params& p) {
     const int v = timer(w, 0);
     if (ping(w) == v && pong(w) == 0) {
       out.send(rec(0, i, v));

@@ -63,12 +63,14 @@ struct SIPaxos {
     w[2] = (uint32_t)(v >> 32);
   }
 
-  static DSL_HD void broadcast(int from, const Params& p, Rec proto, Sender<SIPaxos>& out) {
+  template <class O>
+  static DSL_HD void broadcast(int from, const Params& p, Rec proto, O& out) {
     for (int a = 0; a < p.acceptors; a++) out.send((proto & ~(Rec)(0x3f << 24)) | ((Rec)from << 27) | ((Rec)(p.proposers + a) << 24));
   }
 
   static DSL_HD int num_nodes(const Params& p) { return p.proposers + p.acceptors; }
-  static DSL_HD void init_node(int i, uint32_t* w, Sender<SIPaxos>&, const Params& p) {
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O&, const Params& p) {
     if (i < p.proposers) {
       put(w, 2, 2, i + 1);   // proposalValue = values[i]
       put(w, 16, 8, i + 1);  // proposalNumber = i + 1; init(): set(Propose, 100) (constant queue)
@@ -77,7 +79,8 @@ struct SIPaxos {
   static DSL_HD int num_timer_events(int i, const uint32_t*, const Params& p) { return i < p.proposers; }
 
   // Proposer.onPropose (the Propose queue stays [Propose]).
-  static DSL_HD int on_timer(int i, uint32_t* w, int, Sender<SIPaxos>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int, O& out, const Params& p) {
     int n = pnum(w);
     if (has_proposed(w)) n += p.proposers;
     if (n > 255) return STEP_OVERFLOW;
@@ -90,7 +93,8 @@ struct SIPaxos {
     return STEP_OK;
   }
 
-  static DSL_HD int on_message(int i, uint32_t* w, Rec m, Sender<SIPaxos>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params& p) {
     const int from = rec_from(m);
     switch (r_type(m)) {
       case T_PREPARE: {  // Acceptor.handlePrepare

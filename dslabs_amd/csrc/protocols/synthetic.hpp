@@ -51,13 +51,15 @@ struct Synthetic {
   static DSL_HD int timer_at(const uint32_t* w, int j) { return (int)((w[1] >> (2 * j)) & 3); }
 
   static DSL_HD int num_nodes(const Params& p) { return p.nodes; }
-  static DSL_HD void init_node(int, uint32_t* w, Sender<Synthetic>&, const Params&) {
+  template <class O>
+  static DSL_HD void init_node(int, uint32_t* w, O&, const Params&) {
     w[0] = 0;
     w[1] = 0 | (1 << 2) | (2 << 4) | (3 << 6);  // init(): set SynthTimer(0), (1), (2), (3)
   }
   static DSL_HD int num_timer_events(int, const uint32_t*, const Params&) { return 4; }
 
-  static DSL_HD int on_timer(int i, uint32_t* w, int j, Sender<Synthetic>& out, const Params& p) {
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int j, O& out, const Params& p) {
     const int t = timer_at(w, j);
     const int v = mix(p, i, t, v_of(w));
     w[0] = (w[0] & ~0xffffu) | (uint32_t)v;
@@ -68,7 +70,8 @@ struct Synthetic {
     w[1] = (lo | hi | ((uint32_t)t << 6)) & 0xffu;
     return STEP_OK;
   }
-  static DSL_HD int on_message(int i, uint32_t* w, Rec, Sender<Synthetic>&, const Params& p) {
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec, O&, const Params& p) {
     const int k = (pokes_of(w) + 1) & 3;
     const int v = mix(p, i, 4 + k, v_of(w));
     w[0] = (uint32_t)v | ((uint32_t)k << 16);

@@ -21,6 +21,40 @@
 
 using namespace dsl;
 
+// Every send of one step, duplicates kept (the check behind P::kSendsDistinct).
+template <class P>
+struct RawSender {
+  typename P::Rec r[64];
+  int n = 0;
+  bool overflow = false;
+  void send(typename P::Rec x) {
+    if (n < 64) r[n] = x;
+    n++;
+  }
+};
+template <class P>
+static bool sends_distinct(const uint32_t* w, int k, const typename P::Params& prm, const DevSettings& set) {
+  const int e = locate_event<P>(w, prm, set, k);
+  if (e == INT32_MIN) return true;
+  uint32_t nw[P::kNodeWords];
+  RawSender<P> out;
+  if (e >= 0) {
+    const auto r = Net<P>::at(w, e);
+    const int node = P::rec_to(r);
+    if (node >= P::num_nodes(prm)) return true;
+    for (int i = 0; i < P::kNodeWords; i++) nw[i] = w[node * P::kNodeWords + i];
+    P::on_message(node, nw, r, out, prm);
+  } else {
+    const int x = -1 - e, node = x >> 8;
+    for (int i = 0; i < P::kNodeWords; i++) nw[i] = w[node * P::kNodeWords + i];
+    P::on_timer(node, nw, x & 255, out, prm);
+  }
+  for (int a = 0; a < out.n && a < 64; a++)
+    for (int b = a + 1; b < out.n && b < 64; b++)
+      if (out.r[a] == out.r[b]) return false;
+  return true;
+}
+
 template <class P>
 static int run(const dsl_protocol_desc& d, DevSettings set) {
   typename P::Params prm = P::from_desc(d);
@@ -56,7 +90,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
-  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0;
+  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0, dup_sends = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
@@ -87,6 +121,9 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         continue;
       }
       if (dl.out.n == 0 && same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords)) noop++;
+      if constexpr (SendsDistinct<P>::value) {  // P::kSendsDistinct: no record sent twice in one step
+        if (!sends_distinct<P>(n.s.w, k, prm, set)) dup_sends++;
+      }
       S t;
       if (!materialize<P>(n.s.w, dl, t.w)) {
         printf("{\"error\":\"overflow\"}\n");
@@ -124,8 +161,8 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
   unsigned long long total = 0;
   printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"emit_mismatch\":%lld,"
-         "\"judge_mismatch\":%lld,\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch, emit_mismatch,
-         judge_mismatch);
+         "\"judge_mismatch\":%lld,\"dup_sends\":%lld,\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch,
+         emit_mismatch, judge_mismatch, dup_sends);
   for (size_t i = 0; i < per.size(); i++) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
