@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(HERE, "libdslabs_hip%s.so" % ("_" + _VARIANT if _VARIANT
 
 DSL_MAX_NODES = 32
 DSL_MAX_PREDICATES = 16
+DSL_MAX_POOL = 32
 DSL_MAX_PARAMS = 64
 DSL_MAX_EVENT_FIELDS = 8
 
@@ -58,8 +59,9 @@ class dsl_settings(ctypes.Structure):
         ("invariants", dsl_predicate * DSL_MAX_PREDICATES),
         ("goals", dsl_predicate * DSL_MAX_PREDICATES),
         ("prunes", dsl_predicate * DSL_MAX_PREDICATES),
-        ("table_log2_slots", ctypes.c_int32), ("reserved0", ctypes.c_int32),
+        ("table_log2_slots", ctypes.c_int32), ("n_pool", ctypes.c_int32),
         ("max_frontier_states", ctypes.c_uint64), ("memory_budget_bytes", ctypes.c_uint64),
+        ("pool", dsl_predicate * DSL_MAX_POOL),
     ]
 
 

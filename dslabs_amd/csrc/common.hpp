@@ -23,14 +23,26 @@ enum StepRc : int {
 // Predicate value (StatePredicate.test): false / true / threw.
 enum PredVal : int { PV_FALSE = 0, PV_TRUE = 1, PV_THREW = 2 };
 
+// One step of a predicate program: a leaf (a standard or protocol predicate, optionally
+// negated) or a combinator over the values on the program's stack (StatePredicate.and / or /
+// implies / negate, T/StatePredicate.java:382-432). Programs are postfix; resolve_settings
+// compiles the C ABI's predicate trees into them.
 struct DevPred {
-  int32_t id;
-  int32_t negate;
-  int64_t arg0, arg1;
-  uint32_t reads;  // nodes whose words the predicate reads (bit i = node i; bit 31 = the network)
+  int32_t id;      // leaf: dsl_predicate_id (> 0); combinator: kOpAnd / kOpOr / kOpNot
+  int32_t negate;  // leaf: StatePredicate.negate()
+  int32_t arg0, arg1;
+  uint32_t reads;  // leaf: nodes whose words it reads (bit i = node i; bit 31 = the network)
   uint32_t pad;
 };
+constexpr int32_t kOpAnd = -1, kOpOr = -2, kOpNot = -3;
 constexpr uint32_t kReadsAll = 0xffffffffu;
+constexpr int kMaxProgOps = 48;   // ops of all the programs of one search
+constexpr int kMaxProgStack = 16;  // values on a program's stack (2 bits each in one word)
+
+// A top-level predicate (an invariant, goal or prune): ops [start, start + len) of the pool.
+struct DevProg {
+  int16_t start, len;
+};
 
 // Device form of SearchSettings/TestSettings. The tri-state precedence of
 // TestSettings.shouldDeliver (TestSettings.java:224-245) is resolved on the host into a
@@ -40,10 +52,11 @@ struct DevSettings {
   uint32_t timer_mask;
   int32_t all_deliver;  // every (from, to) pair of the protocol's nodes delivers
   int32_t max_depth;
-  int32_t n_inv, n_goal, n_prune;
-  DevPred inv[DSL_MAX_PREDICATES];
-  DevPred goal[DSL_MAX_PREDICATES];
-  DevPred prune[DSL_MAX_PREDICATES];
+  int32_t n_inv, n_goal, n_prune, n_ops;
+  DevProg inv[DSL_MAX_PREDICATES];
+  DevProg goal[DSL_MAX_PREDICATES];
+  DevProg prune[DSL_MAX_PREDICATES];
+  DevPred ops[kMaxProgOps];
 };
 
 DSL_HD bool should_deliver(const DevSettings& s, int from, int to) {

@@ -1,6 +1,7 @@
 // engine.hip -- libdslabs_hip.so: C ABI (include/dslabs_hip.h) over the templated engine.
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <string>
 
 #include "bfs_engine.hpp"
@@ -189,22 +190,52 @@ int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)(int), 
   }
   d.max_depth = in.max_depth;
   if (in.n_invariants < 0 || in.n_invariants > DSL_MAX_PREDICATES || in.n_goals < 0 ||
-      in.n_goals > DSL_MAX_PREDICATES || in.n_prunes < 0 || in.n_prunes > DSL_MAX_PREDICATES)
+      in.n_goals > DSL_MAX_PREDICATES || in.n_prunes < 0 || in.n_prunes > DSL_MAX_PREDICATES || in.n_pool < 0 ||
+      in.n_pool > DSL_MAX_POOL)
     return DSL_ERR_ARG;
   d.n_inv = in.n_invariants;
   d.n_goal = in.n_goals;
   d.n_prune = in.n_prunes;
-  auto copy = [&](const dsl_predicate* src, int n, DevPred* dst) {
+  // predicate trees (leaves + DSL_PRED_AND / _OR / _IMPLIES over pool entries) -> postfix programs
+  std::string why;
+  std::function<bool(const dsl_predicate&, int, int*)> emit = [&](const dsl_predicate& p, int level, int* sp) -> bool {
+    if (level > 16) return why = "predicate nesting too deep", false;
+    const bool comb = p.pred_id == DSL_PRED_AND || p.pred_id == DSL_PRED_OR || p.pred_id == DSL_PRED_IMPLIES;
+    if (comb) {
+      if (p.arg0 < 0 || p.arg0 >= in.n_pool || p.arg1 < 0 || p.arg1 >= in.n_pool)
+        return why = "combinator operand outside dsl_settings.pool", false;
+      if (!emit(in.pool[p.arg0], level + 1, sp)) return false;
+      auto push_op = [&](int32_t op) {
+        if (d.n_ops >= kMaxProgOps) return why = "predicate programs too long", false;
+        d.ops[d.n_ops++] = DevPred{op, 0, 0, 0, 0u, 0u};
+        return true;
+      };
+      if (p.pred_id == DSL_PRED_IMPLIES && !push_op(kOpNot)) return false;  // or(negate(a), b)
+      if (!emit(in.pool[p.arg1], level + 1, sp)) return false;
+      if (!push_op(p.pred_id == DSL_PRED_AND ? kOpAnd : kOpOr)) return false;
+      (*sp)--;
+      if (p.negate && !push_op(kOpNot)) return false;
+      return true;
+    }
+    if (!known(p.pred_id)) return why = "predicate not supported by this protocol's device predicates", false;
+    if (d.n_ops >= kMaxProgOps) return why = "predicate programs too long", false;
+    d.ops[d.n_ops++] = DevPred{p.pred_id, p.negate, (int32_t)p.arg0, (int32_t)p.arg1, 0u, 0u};
+    if (++*sp > kMaxProgStack) return why = "predicate too wide", false;
+    return true;
+  };
+  auto compile = [&](const dsl_predicate* src, int n, DevProg* dst) {
     for (int i = 0; i < n; i++) {
-      if (!known(src[i].pred_id)) return false;
-      dst[i] = DevPred{src[i].pred_id, src[i].negate, src[i].arg0, src[i].arg1};
+      const int start = d.n_ops;
+      int sp = 0;
+      if (!emit(src[i], 0, &sp)) return false;
+      dst[i] = DevProg{(int16_t)start, (int16_t)(d.n_ops - start)};
     }
     return true;
   };
-  if (!copy(in.invariants, d.n_inv, d.inv) || !copy(in.goals, d.n_goal, d.goal) ||
-      !copy(in.prunes, d.n_prune, d.prune)) {
-    set_error("predicate not supported by this protocol's device predicates");
-    return DSL_ERR_UNKNOWN_PREDICATE;
+  if (!compile(in.invariants, d.n_inv, d.inv) || !compile(in.goals, d.n_goal, d.goal) ||
+      !compile(in.prunes, d.n_prune, d.prune)) {
+    set_error(why);
+    return why.rfind("predicate not supported", 0) == 0 ? DSL_ERR_UNKNOWN_PREDICATE : DSL_ERR_ARG;
   }
   *out = d;
   return DSL_OK;

@@ -467,14 +467,9 @@ void describe_event(const uint32_t* w, int k, const typename P::Params& prm, con
   }
 }
 
-// checkState order over a node view (Search.java:162-231).
-// incremental: the view is a successor of an EXPANDED, non-initial parent, which therefore had
-// every invariant true, every goal false or throwing (ignored) and every prune false (a state
-// that violated, matched or was pruned is never expanded; only the initial state is expanded
-// when pruned, Search.java:475). A predicate that reads neither the changed node nor the
-// network has the parent's value, so it is skipped with that outcome. tests/hostcheck checks
-// the incremental verdict against the full one on every generated successor.
-// A predicate reading the changed node is also unchanged when the words it reads are: the
+// Incremental predicate evaluation (judge_view below): a leaf that reads neither the changed node
+// nor the network keeps the parent's value. A leaf reading the changed node is also unchanged
+// when the words it reads are: the
 // protocol's pred_same(pr, old, new) says so (e.g. Multi-Paxos LOGS_CONSISTENT reads only the
 // servers' log words); without one, the node's words must all be equal.
 template <int N>
@@ -494,50 +489,88 @@ struct PredSame<P, std::void_t<decltype(&P::pred_same)>> {
 };
 
 template <class P>
-DSL_HD bool pred_unchanged(const DevPred& pr, const NodeView& v, bool incremental) {
-  if (!incremental || v.changed < 0 || (pr.reads >> 31)) return false;
+DSL_HD bool leaf_unchanged(const DevPred& pr, const NodeView& v) {
+  if (pr.reads >> 31) return false;
   if (!((pr.reads >> v.changed) & 1u)) return true;
   return PredSame<P>::same(pr, v.base + v.changed * v.nw, v.over);
 }
+// A program is unchanged when every leaf is.
+template <class P>
+DSL_HD bool prog_unchanged(const DevSettings& set, DevProg g, const NodeView& v, bool incremental) {
+  if (!incremental || v.changed < 0) return false;
+  for (int i = 0; i < g.len; i++) {
+    const DevPred& op = set.ops[g.start + i];
+    if (op.id > 0 && !leaf_unchanged<P>(op, v)) return false;
+  }
+  return true;
+}
 
+// StatePredicate.test of a program (false / true / threw): postfix over a stack of 2-bit values
+// kept in one word (no indexed private array). Combinators follow StatePredicate.java:397-431: a
+// throwing left operand throws; and(a, b) is a when a is false, else b; or(a, b) is a when a is
+// true, else b; negate keeps a throw.
+template <class P>
+DSL_HD int eval_prog(const DevSettings& set, DevProg g, const NodeView& v, const typename P::Params& prm) {
+  uint32_t st = 0;
+  for (int i = 0; i < g.len; i++) {
+    const DevPred& op = set.ops[g.start + i];
+    int x;
+    if (op.id == kOpAnd || op.id == kOpOr) {
+      const int b = (int)(st & 3u);
+      st >>= 2;
+      const int a = (int)(st & 3u);
+      st >>= 2;
+      x = a == PV_THREW ? PV_THREW : op.id == kOpAnd ? (a == PV_FALSE ? PV_FALSE : b) : (a == PV_TRUE ? PV_TRUE : b);
+    } else if (op.id == kOpNot) {
+      const int a = (int)(st & 3u);
+      st >>= 2;
+      x = a == PV_THREW ? PV_THREW : !a;
+    } else {
+      x = P::eval(op, v, prm);
+      if (x != PV_THREW && op.negate) x = !x;
+    }
+    st = (st << 2) | (uint32_t)x;
+  }
+  return (int)(st & 3u);
+}
+
+// checkState order over a node view (Search.java:162-231).
+// incremental: the view is a successor of an EXPANDED, non-initial parent, which therefore had
+// every invariant true, every goal false or throwing (ignored) and every prune false (a state
+// that violated, matched or was pruned is never expanded; only the initial state is expanded
+// when pruned, Search.java:475). A predicate whose leaves read neither the changed node's
+// relevant words nor the network has the parent's value, so it is skipped with that outcome.
+// tests/hostcheck checks the incremental verdict against the full one on every successor.
 template <class P>
 DSL_HD Verdict judge_view(const NodeView& v, const typename P::Params& prm, const DevSettings& set, int depth,
                           int* pred_index, bool incremental = false) {
   for (int i = 0; i < set.n_inv; i++) {
-    if (pred_unchanged<P>(set.inv[i], v, incremental)) continue;
-    int x = P::eval(set.inv[i], v, prm);
-    if (x != PV_THREW && set.inv[i].negate) x = !x;
-    if (x != PV_TRUE) {
+    if (prog_unchanged<P>(set, set.inv[i], v, incremental)) continue;
+    if (eval_prog<P>(set, set.inv[i], v, prm) != PV_TRUE) {
       *pred_index = i;
       return V_TERM_INVARIANT;
     }
   }
   for (int i = 0; i < set.n_goal; i++) {
-    if (pred_unchanged<P>(set.goal[i], v, incremental)) continue;
-    int x = P::eval(set.goal[i], v, prm);
-    if (x == PV_THREW) continue;
-    if (set.goal[i].negate) x = !x;
-    if (x == PV_TRUE) {
+    if (prog_unchanged<P>(set, set.goal[i], v, incremental)) continue;
+    if (eval_prog<P>(set, set.goal[i], v, prm) == PV_TRUE) {  // throwing goals are ignored
       *pred_index = i;
       return V_TERM_GOAL;
     }
   }
   for (int i = 0; i < set.n_prune; i++) {
-    if (pred_unchanged<P>(set.prune[i], v, incremental)) continue;
-    int x = P::eval(set.prune[i], v, prm);
-    if (x != PV_THREW && set.prune[i].negate) x = !x;
-    if (x != PV_FALSE) return V_PRUNED;
+    if (prog_unchanged<P>(set, set.prune[i], v, incremental)) continue;
+    if (eval_prog<P>(set, set.prune[i], v, prm) != PV_FALSE) return V_PRUNED;  // true or throwing
   }
   if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
   return V_VALID;
 }
 
-// Fills DevPred::reads from the protocol's read sets (host, after resolve_settings).
+// Fills DevPred::reads of every leaf from the protocol's read sets (host, after resolve_settings).
 template <class P>
 void set_pred_reads(DevSettings& d, const typename P::Params& prm) {
-  for (int i = 0; i < d.n_inv; i++) d.inv[i].reads = P::pred_reads(d.inv[i], prm);
-  for (int i = 0; i < d.n_goal; i++) d.goal[i].reads = P::pred_reads(d.goal[i], prm);
-  for (int i = 0; i < d.n_prune; i++) d.prune[i].reads = P::pred_reads(d.prune[i], prm);
+  for (int i = 0; i < d.n_ops; i++)
+    if (d.ops[i].id > 0) d.ops[i].reads = P::pred_reads(d.ops[i], prm);
 }
 
 }  // namespace dsl

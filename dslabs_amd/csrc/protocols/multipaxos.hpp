@@ -8,18 +8,21 @@
 // exposes what PaxosTest's predicates read (status / command / lastNonEmpty, PaxosTest.java:113-346).
 //
 // Nodes: servers 0..n-1 ("server1.."), clients n..n+c-1 ("client1.."). Ballot = (round, leader),
-// compared as (round << 2) | leader. Commands: id 1 + 2*client + (seq-1) (0 = no-op); a command
-// appends value id vals[client][seq-1]. A KV result is the executed append sequence, 12 bits =
-// len:3 | value ids 2 bits each. Application state (the key's value, the AMO last-seq table) is a
-// function of the log's executed prefix (slots < slotOut), so it is recomputed, not stored.
+// compared as (round << 2) | leader. Commands: id 1 + 3*client + (seq-1) (0 = no-op); command
+// (c, q) is ops[c][q-1] in {Put, Append, Get} on the single key "foo" with value token
+// vals[c][q-1] (KVStoreWorkload put / append / get, KVStoreWorkload.java:40-66). The key's value is
+// a sequence of <= 4 value tokens, 11 bits = len:3 | tokens 2 bits each. A KV result (12 bits) is
+// PutOk (7), KeyNotFound (6), or AppendResult / GetResult of a value (its len is 1..4; which of
+// the two is fixed by the command). Application state (the key's value, the AMO last-seq table) is
+// a function of the log's executed prefix (slots < slotOut), so it is recomputed, not stored.
 //
 // Node words (6):
 //   server: w0 = round:4 | leader:2 @4 | active:1 @6 | electing:1 @7 | heard:1 @8 | missed:2 @9 |
 //                p1bVotes:3 @11 | slotOut:3 @14 | slotIn:3 @17
 //           w1-w2 = log[1..4], 16 bits each: status:2 | ballot:6 @2 | cmd:3 @8
 //           w3 = p2bVotes[1..4], 3 bits each;  w4-w5 = p1bLog[1..4] (merged phase-1 log)
-//   client: w0 = seq:2 | pending:1 @2 | result:12 @3 | nres:2 @15 | ntim:2 @17 | timers[2] @19, @21
-//           w1 = results[0..1], 12 bits each
+//   client: w0 = seq:2 | pending:1 @2 | result:12 @3 | nres:2 @15 | ntim:2 @17 | timers[3] @19, 21, 23
+//           w1 = results[0..1], 12 bits each; w2 = results[2]
 // Records (64 bit): type:3 @61 | from:3 @58 | to:3 @55 | payload
 //   0 Request  cmd:3                    4 P2a       round:4 leader:2 slot:3 @6 cmd:3 @9
 //   1 Reply    seq:2 result:12 @2       5 P2b       round:4 leader:2 slot:3 @6
@@ -34,7 +37,8 @@
 namespace dsl {
 
 struct MultiPaxos {
-  static constexpr int kMaxServers = 3, kMaxClients = 2, kMaxCmds = 2, kSlots = 4, kMaxRound = 15;
+  static constexpr int kMaxServers = 3, kMaxClients = 2, kMaxCmds = 3, kSlots = 4, kMaxRound = 15;
+  static constexpr int kMaxTokens = 4;  // value tokens of the key's value
   // kMaxSends: the most records one handler sends is 12 (P1b completing phase 1: a P2a to both
   // other servers for each of the 4 slots, plus up to 4 replies from execute); a larger send
   // list would be a hard STEP_OVERFLOW error, never a truncation.
@@ -51,9 +55,12 @@ struct MultiPaxos {
   struct Params {
     int32_t servers, clients;
     int32_t ncmds[kMaxClients];
-    int32_t vals[kMaxClients][kMaxCmds];      // value id 1..3 of each command
-    int32_t expected[kMaxClients][kMaxCmds];  // expected result encoding, -1 = workload has no results
+    int32_t ops[kMaxClients][kMaxCmds];       // OP_PUT / OP_APPEND / OP_GET
+    int32_t vals[kMaxClients][kMaxCmds];      // value token 1..3 (0 for a Get)
+    int32_t expected[kMaxClients][kMaxCmds];  // expected result code, -1 = the workload checks none
   };
+  enum { OP_PUT = 1, OP_APPEND = 2, OP_GET = 3 };
+  static constexpr uint32_t kPutOk = 7, kKeyNotFound = 6;  // result codes beside values (len 1..4)
   enum { M_REQUEST = 0, M_REPLY, M_P1A, M_P1B, M_P2A, M_P2B, M_DECISION, M_HEARTBEAT, T_TICK = 8, T_CLIENT = 9 };
   enum { EMPTY = 0, ACCEPTED = 1, CHOSEN = 2 };
 
@@ -106,54 +113,75 @@ struct MultiPaxos {
 
   // Workload parameters by client / command index. Selects, not array indexing: a run-time index
   // into the kernel-argument struct makes the compiler copy it to scratch memory.
-  static DSL_HD int val(const Params& p, int c, int k) {
-    return c ? (k ? p.vals[1][1] : p.vals[1][0]) : (k ? p.vals[0][1] : p.vals[0][0]);
+  static DSL_HD int sel6(int c, int k, int a0, int a1, int a2, int b0, int b1, int b2) {
+    const int x = k == 2 ? a2 : k == 1 ? a1 : a0, y = k == 2 ? b2 : k == 1 ? b1 : b0;
+    return c ? y : x;
   }
-  static DSL_HD int expect(const Params& p, int c, int k) {
-    return c ? (k ? p.expected[1][1] : p.expected[1][0]) : (k ? p.expected[0][1] : p.expected[0][0]);
-  }
+#define DSL_MP_SEL(f) sel6(c, k, p.f[0][0], p.f[0][1], p.f[0][2], p.f[1][0], p.f[1][1], p.f[1][2])
+  static DSL_HD int val(const Params& p, int c, int k) { return DSL_MP_SEL(vals); }
+  static DSL_HD int op_of(const Params& p, int c, int k) { return DSL_MP_SEL(ops); }
+  static DSL_HD int expect(const Params& p, int c, int k) { return DSL_MP_SEL(expected); }
+#undef DSL_MP_SEL
   static DSL_HD int ncmd(const Params& p, int c) { return c ? p.ncmds[1] : p.ncmds[0]; }
 
   // ---- application: the executed prefix ----------------------------------------------------------
-  static DSL_HD int cmd_client(int cmd) { return (cmd - 1) >> 1; }
-  static DSL_HD int cmd_seq(int cmd) { return ((cmd - 1) & 1) + 1; }
+  static DSL_HD int cmd_id(int c, int q) { return 1 + 3 * c + (q - 1); }
+  static DSL_HD int cmd_client(int cmd) { return cmd >= 4 ? 1 : 0; }  // cmd in 1..6
+  static DSL_HD int cmd_seq(int cmd) { return cmd - 3 * cmd_client(cmd); }
   static DSL_HD uint32_t res_push(uint32_t r, int v) {
     int len = r & 7;
     return (uint32_t)(len + 1) | (r & ~7u) | ((uint32_t)v << (3 + 2 * len));
   }
-  // The executed prefix: the key's value (append sequence) after slots [1, upto) and each client's
-  // last executed sequence number. Fixed trip counts over the kSlots slots: the loops unroll and
-  // every log access has a constant bit offset (no select chains over the node words).
+  // KVStore.execute of command (c, q) on the key's value `kv`: the new value in *kv, the result
+  // code returned (KVStore.java:59-78 as lab1 specifies it: Put -> PutOk, Append -> the new value,
+  // Get -> the value or KeyNotFound).
+  static DSL_HD uint32_t kv_apply(const Params& p, int c, int q, uint32_t* kv) {
+    const int op = op_of(p, c, q - 1), v = val(p, c, q - 1);
+    if (op == OP_PUT) {
+      *kv = 1u | ((uint32_t)v << 3);
+      return kPutOk;
+    }
+    if (op == OP_APPEND) {
+      *kv = res_push(*kv, v);
+      return *kv;
+    }
+    return (*kv & 7) ? *kv : kKeyNotFound;
+  }
+  // Bit offset of a client's result k (never straddling a word).
+  static DSL_HD int res_bit(int k) { return k < 2 ? 32 + 12 * k : 64; }
+  // The executed prefix: the key's value after slots [1, upto) and each client's last executed
+  // sequence number. Fixed trip counts over the kSlots slots: the loops unroll and every log
+  // access has a constant bit offset (no select chains over the node words).
   static DSL_HD uint32_t executed(const uint32_t* w, const Params& p, int upto, int* last_seq) {
-    uint32_t seqv = 0;
+    uint32_t kv = 0;
     int ls0 = 0, ls1 = 0;
 #pragma unroll
     for (int slot = 1; slot <= kSlots; slot++) {
       const int cmd = e_cmd(entry(w, slot));
       const int c = cmd_client(cmd), q = cmd_seq(cmd);
       if (slot < upto && cmd && (c ? ls1 : ls0) < q) {
-        seqv = res_push(seqv, val(p, c, q - 1));
+        kv_apply(p, c, q, &kv);
         if (c) ls1 = q;
         else ls0 = q;
       }
     }
     last_seq[0] = ls0;
     last_seq[1] = ls1;
-    return seqv;
+    return kv;
   }
-  // The result a client got for command (c0, q0): the value right after it executed.
+  // The result of command (c0, q0) when it executed (the AMO cache's entry).
   static DSL_HD uint32_t result_of(const uint32_t* w, const Params& p, int upto, int c0, int q0) {
-    uint32_t seqv = 0, r = 0;
+    uint32_t kv = 0, r = 0;
     int ls0 = 0, ls1 = 0;
 #pragma unroll
     for (int slot = 1; slot <= kSlots; slot++) {
       const int cmd = e_cmd(entry(w, slot));
       const int c = cmd_client(cmd), q = cmd_seq(cmd);
       if (slot < upto && cmd && (c ? ls1 : ls0) < q) {
-        seqv = res_push(seqv, val(p, c, q - 1));
+        const uint32_t x = kv_apply(p, c, q, &kv);
         if (c) ls1 = q;
         else ls0 = q;
-        if (c == c0 && q == q0) r = seqv;
+        if (c == c0 && q == q0) r = x;
       }
     }
     return r;
@@ -163,7 +191,7 @@ struct MultiPaxos {
   static DSL_HD void execute(int s, uint32_t* w, const Params& p, O& out) {
     const int so0 = slot_out(w);
     const bool act = active(w);
-    uint32_t seqv = 0;
+    uint32_t kv = 0;
     int ls0 = 0, ls1 = 0, so = so0;
     bool run = true;  // every slot from slotOut to here is chosen
 #pragma unroll
@@ -175,10 +203,10 @@ struct MultiPaxos {
       const bool now = !before && run && e_status(e) == CHOSEN;
       run = run && (before || now);
       if ((before || now) && cmd && (c ? ls1 : ls0) < q) {
-        seqv = res_push(seqv, val(p, c, q - 1));
+        const uint32_t x = kv_apply(p, c, q, &kv);
         if (c) ls1 = q;
         else ls0 = q;
-        if (now && act) out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)seqv << 2)));
+        if (now && act) out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)x << 2)));
       }
       if (now) so = slot + 1;
     }
@@ -251,10 +279,10 @@ struct MultiPaxos {
     put(w, 0, 2, q);
     put(w, 2, 1, 1);
     put(w, 3, 12, 0);
-    const int cmd = 1 + 2 * c + (q - 1);
+    const int cmd = cmd_id(c, q);
     for (int s = 0; s < p.servers; s++) out.send(msg(M_REQUEST, p.servers + c, s, (uint64_t)cmd));
     const int n = get(w, 17, 2);
-    if (n >= 2) {
+    if (n >= kMaxCmds) {
       out.overflow = true;
       return;
     }
@@ -266,7 +294,7 @@ struct MultiPaxos {
     int nres = get(w, 15, 2);
     const int res = get(w, 3, 12);
     if (nres < ncmd(p, c) && res != 0) {
-      put(w, 32 + 12 * nres, 12, res);
+      put(w, res_bit(nres), 12, res);
       nres++;
       put(w, 15, 2, nres);
       if (nres < ncmd(p, c)) client_send(c, w, p, nres + 1, out);
@@ -295,17 +323,19 @@ struct MultiPaxos {
       const int c = i - p.servers;
       const int t = get(w, 19, 2);
       if (get(w, 2, 1) && t == get(w, 0, 2)) {
-        const int cmd = 1 + 2 * c + (t - 1);
+        const int cmd = cmd_id(c, t);
         for (int s = 0; s < p.servers; s++) out.send(msg(M_REQUEST, i, s, (uint64_t)cmd));
         const int n = get(w, 17, 2);
-        if (n >= 2) return STEP_OVERFLOW;
+        if (n >= kMaxCmds) return STEP_OVERFLOW;
         put(w, 19 + 2 * n, 2, t);
         put(w, 17, 2, n + 1);
       }
       client_worker_continue(c, w, p, out);
       const int n = get(w, 17, 2);
+      // remove the head (the queue's entries move up one; the last slot empties)
       put(w, 19, 2, n > 1 ? get(w, 21, 2) : 0);
-      put(w, 21, 2, 0);
+      put(w, 21, 2, n > 2 ? get(w, 23, 2) : 0);
+      put(w, 23, 2, 0);
       put(w, 17, 2, n - 1);
       return STEP_OK;
     }
@@ -441,46 +471,63 @@ struct MultiPaxos {
     return (int)((w[bit >> 5] >> (bit & 31)) & ((1u << width) - 1u));
   }
   static DSL_HD uint32_t entryd(const uint32_t* w, int slot) { return (uint32_t)getd(w, 32 + 16 * (slot - 1), 16); }
-  static DSL_HD int value_of(const Params& p, int cmd) { return cmd ? val(p, cmd_client(cmd), cmd_seq(cmd) - 1) : 0; }
+  // PaxosServer.command(i) as a KV command code: op << 2 | value token (0 = null: an empty slot or a
+  // no-op). Commands compare as KV commands (Lombok equals of Put / Append / Get), not as AMO
+  // commands: PaxosTest's slotValid requires command(i) to return the unwrapped command.
+  static DSL_HD int kv_cmd(const Params& p, int cmd) {
+    return cmd ? (op_of(p, cmd_client(cmd), cmd_seq(cmd) - 1) << 2) | val(p, cmd_client(cmd), cmd_seq(cmd) - 1) : 0;
+  }
 
-  // PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (slotValid, PaxosTest.java:215-322); MARKERS_VALID holds by
-  // construction (firstNonCleared() == 1, lastNonEmpty() = last non-EMPTY slot). The servers' log
-  // words are read once (independent LDS reads), then everything is register arithmetic.
-  static DSL_HD int logs_consistent(const NodeView& v, const Params& p) {
-    uint32_t lw[kMaxServers][2];
+  // PaxosTest.slotValid(st, i) (PaxosTest.java:215-279) over the servers' log words lw; with no
+  // garbage collection firstNonCleared() == 1 and no slot is CLEARED, lastNonEmpty() is the last
+  // non-EMPTY slot, and command(i) is null exactly for EMPTY slots and no-ops.
+  static DSL_HD bool slot_valid(const uint32_t (&lw)[kMaxServers][2], const Params& p, int slot) {
+    if (slot < 1) return false;  // i < firstNonCleared but the status is not CLEARED
+    if (slot > kSlots) return true;  // EMPTY everywhere: never chosen
+    bool is_chosen = false, conflict = false;
+    int chosen = 0, count = 0;
+#pragma unroll
+    for (int s = 0; s < kMaxServers; s++) {
+      const uint32_t e = (sel2(lw[s], (slot - 1) >> 1) >> (16 * ((slot - 1) & 1))) & 0xffffu;
+      if (s < p.servers && e_status(e) == CHOSEN) {
+        const int x = kv_cmd(p, e_cmd(e));
+        conflict |= is_chosen && x != chosen;
+        chosen = x;
+        is_chosen = true;
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < kMaxServers; s++) {
+      const uint32_t e = (sel2(lw[s], (slot - 1) >> 1) >> (16 * ((slot - 1) & 1))) & 0xffffu;
+      if (s < p.servers && e_status(e) != EMPTY && (e_status(e) != ACCEPTED || kv_cmd(p, e_cmd(e)) == chosen)) count++;
+    }
+    return !is_chosen || (!conflict && 2 * count > p.servers);
+  }
+  static DSL_HD uint32_t sel2(const uint32_t (&a)[2], int i) { return i ? a[1] : a[0]; }
+  static DSL_HD void load_logs(const NodeView& v, const Params& p, uint32_t (&lw)[kMaxServers][2]) {
 #pragma unroll
     for (int s = 0; s < kMaxServers; s++) {
       const uint32_t* w = v.node(s < p.servers ? s : 0);
       lw[s][0] = s < p.servers ? w[1] : 0u;
       lw[s][1] = s < p.servers ? w[2] : 0u;
     }
+  }
+  // PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (:302-322): every slot up to the last non-empty one; and
+  // LOGS_CONSISTENT (:282-300): slots from the smallest firstNonCleared() -- 1 here -- on, so the
+  // two coincide. MARKERS_VALID (:128-193) holds by construction. The servers' log words are
+  // read once (independent LDS reads), then everything is register arithmetic; slots past the
+  // last non-empty one are EMPTY everywhere and valid.
+  static DSL_HD int logs_consistent(const NodeView& v, const Params& p) {
+    uint32_t lw[kMaxServers][2];
+    load_logs(v, p, lw);
     bool ok = true;
 #pragma unroll
-    for (int slot = 1; slot <= kSlots; slot++) {
-      bool is_chosen = false, conflict = false;
-      int chosen = 0, count = 0;
-#pragma unroll
-      for (int s = 0; s < kMaxServers; s++) {
-        const uint32_t e = (lw[s][(slot - 1) >> 1] >> (16 * ((slot - 1) & 1))) & 0xffffu;
-        if (e_status(e) == CHOSEN) {
-          const int x = value_of(p, e_cmd(e));
-          conflict |= is_chosen && x != chosen;
-          chosen = x;
-          is_chosen = true;
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < kMaxServers; s++) {
-        const uint32_t e = (lw[s][(slot - 1) >> 1] >> (16 * ((slot - 1) & 1))) & 0xffffu;
-        if (e_status(e) != EMPTY && (e_status(e) != ACCEPTED || value_of(p, e_cmd(e)) == chosen)) count++;
-      }
-      // slots past the last non-empty one are empty everywhere: never chosen, never checked
-      ok &= !is_chosen || (!conflict && 2 * count > p.servers);
-    }
+    for (int slot = 1; slot <= kSlots; slot++) ok &= slot_valid(lw, p, slot);
     return ok ? PV_TRUE : PV_FALSE;
   }
 
-  // KVStoreWorkload.APPENDS_LINEARIZABLE (KVStoreWorkload.java:282-340)
+  // KVStoreWorkload.APPENDS_LINEARIZABLE (KVStoreWorkload.java:282-340): clients in address order,
+  // their (command, result) pairs in order; a non-Append command throws.
   static DSL_HD int appends_linearizable(const NodeView& v, const Params& p) {
     uint32_t all[kMaxClients * kMaxCmds];
     int n = 0;
@@ -488,9 +535,10 @@ struct MultiPaxos {
       const uint32_t* w = v.node(p.servers + c);
       const int nres = getd(w, 15, 2);
       for (int k = 0; k < nres; k++) {
-        const uint32_t r = (uint32_t)getd(w, 32 + 12 * k, 12);
+        if (op_of(p, c, k) != OP_APPEND) return PV_THREW;  // "Client workers have non-Append Commands"
+        const uint32_t r = (uint32_t)getd(w, res_bit(k), 12);
         const int len = r & 7;
-        if (len == 0 || (int)((r >> (3 + 2 * (len - 1))) & 3) != val(p, c, k)) return PV_FALSE;  // endsWith
+        if (len == 0 || len > kMaxTokens || (int)((r >> (3 + 2 * (len - 1))) & 3) != val(p, c, k)) return PV_FALSE;
         all[n++] = r;
       }
     }
@@ -516,7 +564,7 @@ struct MultiPaxos {
           const uint32_t* w = v.node(p.servers + c);
           const int nres = getd(w, 15, 2);
           for (int k = 0; k < nres; k++)
-            if (expect(p, c, k) >= 0 && getd(w, 32 + 12 * k, 12) != expect(p, c, k)) return PV_FALSE;
+            if (expect(p, c, k) >= 0 && getd(w, res_bit(k), 12) != expect(p, c, k)) return PV_FALSE;
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
@@ -524,7 +572,7 @@ struct MultiPaxos {
           if (getd(v.node(p.servers + c), 15, 2) < ncmd(p, c)) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_DONE: {
-        const int c = (int)pr.arg0 - p.servers;
+        const int c = pr.arg0 - p.servers;
         if (c < 0 || c >= p.clients) return PV_THREW;
         return getd(v.node(p.servers + c), 15, 2) >= ncmd(p, c) ? PV_TRUE : PV_FALSE;
       }
@@ -533,12 +581,27 @@ struct MultiPaxos {
           if (getd(v.node(p.servers + c), 15, 2) > 0) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_HAS_RESULTS: {
-        const int c = (int)pr.arg0 - p.servers;
+        const int c = pr.arg0 - p.servers;
         if (c < 0 || c >= p.clients) return PV_THREW;
         return getd(v.node(p.servers + c), 15, 2) == pr.arg1 ? PV_TRUE : PV_FALSE;
       }
       case DSL_PRED_LOGS_CONSISTENT:
+      case DSL_PRED_LOGS_CONSISTENT_ACTIVE:
         return logs_consistent(v, p);
+      case DSL_PRED_SLOT_VALID: {
+        uint32_t lw[kMaxServers][2];
+        load_logs(v, p, lw);
+        return slot_valid(lw, p, pr.arg0) ? PV_TRUE : PV_FALSE;
+      }
+      case DSL_PRED_HAS_STATUS:
+      case DSL_PRED_HAS_COMMAND: {  // (PaxosServer) st.server(a): a non-server address throws
+        if (pr.arg0 < 0 || pr.arg0 >= p.servers) return PV_THREW;
+        const int slot = pr.id == DSL_PRED_HAS_STATUS ? pr.arg1 >> 4 : pr.arg1 >> 8;
+        const uint32_t e = slot >= 1 && slot <= kSlots ? entryd(v.node(pr.arg0), slot) : 0u;
+        if (pr.id == DSL_PRED_HAS_STATUS) return e_status(e) == (pr.arg1 & 15) ? PV_TRUE : PV_FALSE;
+        const int c = e_status(e) == EMPTY ? 0 : kv_cmd(p, e_cmd(e));
+        return c == (pr.arg1 & 0xff) ? PV_TRUE : PV_FALSE;
+      }
       case DSL_PRED_APPENDS_LINEARIZABLE:
         return appends_linearizable(v, p);
       default:
@@ -546,49 +609,61 @@ struct MultiPaxos {
     }
   }
 
+  static DSL_HD bool server_log_pred(int id) {
+    return id == DSL_PRED_LOGS_CONSISTENT || id == DSL_PRED_LOGS_CONSISTENT_ACTIVE || id == DSL_PRED_SLOT_VALID ||
+           id == DSL_PRED_HAS_STATUS || id == DSL_PRED_HAS_COMMAND;
+  }
   // Word-level read sets for the incremental check: a client predicate reads the client's
-  // result count (w0 bits 15-16) and results (w1); LOGS_CONSISTENT reads a server's log (w1-w2).
+  // result count (w0 bits 15-16) and results (w1-w2); a log predicate a server's log (w1-w2).
   static DSL_HD bool pred_same(const DevPred& pr, const uint32_t* a, const uint32_t* b) {
-    if (pr.id == DSL_PRED_LOGS_CONSISTENT) return ((a[1] ^ b[1]) | (a[2] ^ b[2])) == 0;
+    if (server_log_pred(pr.id)) return ((a[1] ^ b[1]) | (a[2] ^ b[2])) == 0;
     if ((pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) || pr.id == DSL_PRED_APPENDS_LINEARIZABLE)
-      return (((a[0] ^ b[0]) & (3u << 15)) | (a[1] ^ b[1])) == 0;
+      return (((a[0] ^ b[0]) & (3u << 15)) | (a[1] ^ b[1]) | (a[2] ^ b[2])) == 0;
     return same_words<kNodeWords>(a, b);
   }
-  // Read sets (judge_view's incremental check): client predicates read client nodes only,
-  // LOGS_CONSISTENT the servers only.
+  // Read sets (judge_view's incremental check): client predicates read client nodes only, log
+  // predicates the servers (hasStatus / hasCommand: their one server).
   static uint32_t pred_reads(const DevPred& pr, const Params& p) {
     const uint32_t servers = (1u << p.servers) - 1u, clients = ((1u << p.clients) - 1u) << p.servers;
     switch (pr.id) {
-      case DSL_PRED_LOGS_CONSISTENT: return servers;
+      case DSL_PRED_LOGS_CONSISTENT: case DSL_PRED_LOGS_CONSISTENT_ACTIVE: case DSL_PRED_SLOT_VALID: return servers;
+      case DSL_PRED_HAS_STATUS: case DSL_PRED_HAS_COMMAND:
+        return pr.arg0 >= 0 && pr.arg0 < p.servers ? 1u << pr.arg0 : kReadsAll;
       case DSL_PRED_RESULTS_OK: case DSL_PRED_CLIENTS_DONE: case DSL_PRED_CLIENT_DONE: case DSL_PRED_NONE_DECIDED:
       case DSL_PRED_CLIENT_HAS_RESULTS: case DSL_PRED_APPENDS_LINEARIZABLE: return clients;
       default: return kReadsAll;
     }
   }
   static bool known_predicate(int id) {
-    return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == DSL_PRED_LOGS_CONSISTENT ||
+    return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || server_log_pred(id) ||
            id == DSL_PRED_APPENDS_LINEARIZABLE;
   }
   static bool valid(const Params& p) {
     if (p.servers < 1 || p.servers > kMaxServers || p.clients < 1 || p.clients > kMaxClients) return false;
+    int tokens = 0;  // the key's value never exceeds kMaxTokens (every Put / Append adds at most one)
     for (int c = 0; c < p.clients; c++) {
       if (p.ncmds[c] < 1 || p.ncmds[c] > kMaxCmds) return false;
-      for (int k = 0; k < p.ncmds[c]; k++)
-        if (p.vals[c][k] < 1 || p.vals[c][k] > 3) return false;
+      for (int k = 0; k < p.ncmds[c]; k++) {
+        const int op = p.ops[c][k];
+        if (op != OP_PUT && op != OP_APPEND && op != OP_GET) return false;
+        if (op != OP_GET && (p.vals[c][k] < 1 || p.vals[c][k] > 3)) return false;
+        tokens += op != OP_GET;
+      }
     }
-    return true;
+    return tokens <= kMaxTokens;
   }
-  // params: servers, clients, then per client: ncmds, val[0], val[1], expected[0], expected[1]
+  // params: servers, clients, then per client: ncmds, ops[3], vals[3], expected[3]
   static Params from_desc(const dsl_protocol_desc& d) {
     Params p{};
     p.servers = (int32_t)d.params[0];
     p.clients = (int32_t)d.params[1];
     for (int c = 0; c < kMaxClients; c++) {
-      const int b = 2 + 5 * c;
+      const int b = 2 + (1 + 3 * kMaxCmds) * c;
       p.ncmds[c] = (int32_t)d.params[b];
       for (int k = 0; k < kMaxCmds; k++) {
-        p.vals[c][k] = (int32_t)d.params[b + 1 + k];
-        p.expected[c][k] = (int32_t)d.params[b + 3 + k];
+        p.ops[c][k] = (int32_t)d.params[b + 1 + k];
+        p.vals[c][k] = (int32_t)d.params[b + 1 + kMaxCmds + k];
+        p.expected[c][k] = (int32_t)d.params[b + 1 + 2 * kMaxCmds + k];
       }
     }
     return p;

@@ -42,7 +42,7 @@ struct TraceTool {
   // (PV_FALSE / PV_TRUE, or PV_THREW).
   struct Expected {
     bool exception;
-    const DevPred* pred;
+    DevProg pred;
     int outcome;
   };
 
@@ -74,11 +74,9 @@ struct TraceTool {
     return 0;
   }
 
-  int eval(const DevPred& pr, const State& s) const {
+  int eval(DevProg g, const State& s) const {
     const NodeView v{s.w, P::kNodeWords, -1, nullptr};
-    int x = P::eval(pr, v, prm);
-    if (x != PV_THREW && pr.negate) x = !x;
-    return x;
+    return eval_prog<P>(search, g, v, prm);
   }
 
   // checkState (Search.java:162-231) of one state: Verdict and the predicate index.
@@ -91,14 +89,14 @@ struct TraceTool {
 
   // The result the minimized trace must keep, for a terminal verdict v / predicate pi of `last`.
   Expected expected(int v, int pi, const State& last) const {
-    if (v == V_TERM_EXCEPTION) return Expected{true, nullptr, 0};
-    const DevPred* pr = v == V_TERM_INVARIANT ? &search.inv[pi] : &search.goal[pi];
-    return Expected{false, pr, eval(*pr, last)};
+    if (v == V_TERM_EXCEPTION) return Expected{true, DevProg{0, 0}, 0};
+    const DevProg g = v == V_TERM_INVARIANT ? search.inv[pi] : search.goal[pi];
+    return Expected{false, g, eval(g, last)};
   }
 
   bool matches(const Step& x, const Expected& e) const {
     if (e.exception) return x.exc;
-    return eval(*e.pred, x.s) == e.outcome;
+    return eval(e.pred, x.s) == e.outcome;
   }
 
   // The event matching e among the enabled events of s under st (-1: none).

@@ -122,61 +122,123 @@ class SIPaxos(Protocol):
 
 class MultiPaxos(Protocol):
     """lab3 Multi-Paxos (builder-authored): servers "server1..n", clients
-    "client1..c"; each client appends single-character values to key "foo"
-    (KVStoreWorkload.append, labs/lab1-clientserver/tst/dslabs/kvstore/KVStoreWorkload.java:52)."""
+    "client1..c"; each client runs a KVStoreWorkload of Put / Append / Get commands on the key
+    "foo" (KVStoreWorkload.java:40-66, :184-188). Values are token sequences (a workload's
+    tokens, <= 4 per value); result codes: 7 PutOk, 6 KeyNotFound, else a value."""
 
     proto_id = DSL_PROTO_MULTIPAXOS
-    VALUES = ["X", "Y", "Z"]
     PREDICATES = {"LOGS_CONSISTENT_ALL_SLOTS": (400, "Non-empty log slots consistent"),
+                  "LOGS_CONSISTENT": (401, "Active log slots consistent"),
                   "APPENDS_LINEARIZABLE": (300, "Sequence of appends to the same key is linearizable")}
-    WORKLOADS = {  # same names as the oracle's --workload
-        "append-xy": ([["X"], ["Y"]], [[], []]),
-        "append-xy-expect": ([["X"], ["Y"]], [["X"], ["XY"]]),
-        "append-x": ([["X"]], [["X"]]),
-        "append-xz": ([["X", "Z"], ["Y"]], [[], []]),
+    OPS = {"PUT": 1, "APPEND": 2, "GET": 3}
+    PUT_OK, KEY_NOT_FOUND = 7, 6
+    STATUS = {"EMPTY": 0, "ACCEPTED": 1, "CHOSEN": 2, "CLEARED": 3}  # PaxosLogSlotStatus
+    WORKLOADS = {  # same names as the oracle's --workload: (commands, expected results, value tokens)
+        "append-xy": ([["APPEND:foo:X"], ["APPEND:foo:Y"]], [[], []], ["X", "Y", "Z"]),
+        "append-xy-expect": ([["APPEND:foo:X"], ["APPEND:foo:Y"]], [["X"], ["XY"]], ["X", "Y", "Z"]),
+        "append-x": ([["APPEND:foo:X"]], [["X"]], ["X", "Y", "Z"]),
+        "append-xz": ([["APPEND:foo:X", "APPEND:foo:Z"], ["APPEND:foo:Y"]], [[], []], ["X", "Y", "Z"]),
+        # KVStoreWorkload.putAppendGetWorkload (PaxosTest.test27)
+        "put-append-get": ([["PUT:foo:bar", "APPEND:foo:baz", "GET:foo"]], [["Ok", "barbaz", "barbaz"]],
+                           ["bar", "baz"]),
     }
 
     def __init__(self, servers: int = 3, clients: int = 2, workload: str = "append-xy"):
-        vals, exp = self.WORKLOADS[workload]
+        cmds, exp, tokens = self.WORKLOADS[workload]
         self.workload = workload
         self.servers = servers
         self.clients = clients
-        self.values = vals[:clients]
+        self.tokens = tokens
+        self.cmds = [[self._parse_cmd(c) for c in cl] for cl in cmds[:clients]]
         self.expected = exp[:clients]
         self.addresses = [f"server{i}" for i in range(1, servers + 1)] + [f"client{i}" for i in range(1, clients + 1)]
 
     @staticmethod
-    def encode_result(s: str) -> int:
-        r = len(s)
-        for i, ch in enumerate(s):
-            r |= (MultiPaxos.VALUES.index(ch) + 1) << (3 + 2 * i)
+    def _parse_cmd(t: str):
+        parts = t.split(":")
+        return (parts[0], parts[2] if len(parts) > 2 else None)
+
+    def encode_value(self, s: str) -> int:
+        toks, i = [], 0
+        while i < len(s):
+            for k, tok in enumerate(self.tokens):
+                if s.startswith(tok, i):
+                    toks.append(k + 1)
+                    i += len(tok)
+                    break
+            else:
+                raise ValueError(f"value {s!r} is not a sequence of the workload's tokens")
+        r = len(toks)
+        for i, t in enumerate(toks):
+            r |= t << (3 + 2 * i)
         return r
 
-    @staticmethod
-    def decode_result(r: int) -> str:
-        return "".join(MultiPaxos.VALUES[((r >> (3 + 2 * i)) & 3) - 1] for i in range(r & 7))
+    def encode_result(self, op: str, s: str) -> int:
+        if op == "PUT":
+            return self.PUT_OK
+        if op == "GET" and s == "KeyNotFound":
+            return self.KEY_NOT_FOUND
+        return self.encode_value(s)
+
+    def decode_result(self, r: int) -> str:
+        if r == self.PUT_OK:
+            return "Ok"
+        if r == self.KEY_NOT_FOUND:
+            return "KeyNotFound"
+        return "".join(self.tokens[((r >> (3 + 2 * i)) & 3) - 1] for i in range(r & 7))
 
     def params(self):
         ps = [self.servers, self.clients]
         for c in range(2):
-            vals = self.values[c] if c < self.clients else []
+            cl = self.cmds[c] if c < self.clients else []
             exp = self.expected[c] if c < self.clients else []
-            v = [self.VALUES.index(x) + 1 for x in vals] + [0] * (2 - len(vals))
-            e = [self.encode_result(x) for x in exp] + [-1] * (2 - len(exp))
-            ps += [len(vals)] + v + e
+            ops = [self.OPS[op] for op, _ in cl] + [0] * (3 - len(cl))
+            vals = [0 if v is None else self.tokens.index(v) + 1 for _, v in cl] + [0] * (3 - len(cl))
+            e = [self.encode_result(cl[k][0], x) for k, x in enumerate(exp)] + [-1] * (3 - len(exp))
+            ps += [len(cl)] + ops + vals + e
         return ps
 
+    def kv_code(self, cmd: str) -> int:
+        """A KV command as hasCommand's code: a workload command ("APPEND:foo:X", "PUT:foo:bar",
+        "GET:foo"), the oracle's form ("X", "=bar", "?"), or None = null."""
+        if cmd is None:
+            return 0
+        if ":" not in cmd:
+            cmd = "GET:foo" if cmd == "?" else f"PUT:foo:{cmd[1:]}" if cmd.startswith("=") else f"APPEND:foo:{cmd}"
+        op, v = self._parse_cmd(cmd)
+        return (self.OPS[op] << 2) | (0 if v is None else self.tokens.index(v) + 1)
+
     def predicate(self, name):
+        """LOGS_CONSISTENT_ALL_SLOTS, LOGS_CONSISTENT, APPENDS_LINEARIZABLE; slotValid:i;
+        hasStatus:serverK:i:STATUS; hasCommand:serverK:i:CMD (CMD a workload command, or null)
+        (PaxosTest.java:113-346)."""
         from .search import StatePredicate
-        pid, full = self.PREDICATES[name]
-        return StatePredicate(full, pid)
+        if name in self.PREDICATES:
+            pid, full = self.PREDICATES[name]
+            return StatePredicate(full, pid)
+        parts = name.split(":")
+        if parts[0] == "slotValid":
+            return StatePredicate(f"Logs consistent for slot {parts[1]}", 402, int(parts[1]))
+        if parts[0] == "hasStatus":
+            a, i, st = parts[1], int(parts[2]), parts[3]
+            return StatePredicate(f"{a} has status {st} in slot {i}", 403, a, (i << 4) | self.STATUS[st],
+                                  address_args=(0,))
+        if parts[0] == "hasCommand":
+            a, i = parts[1], int(parts[2])
+            c = ":".join(parts[3:])
+            code = self.kv_code(None if c == "null" else c)
+            return StatePredicate(f"{a} has command {c} in slot {i}", 404, a, (i << 8) | code, address_args=(0,))
+        raise KeyError(name)
 
     # ---- rendering in the oracle's toString form ------------------------------------------------
     def _cmd(self, cmd: int) -> str:
         if cmd == 0:
             return "noop"
-        c, q = (cmd - 1) >> 1, ((cmd - 1) & 1) + 1
-        return f"{self.servers + c}#{q}:{self.values[c][q - 1]}"
+        c = 1 if cmd >= 4 else 0
+        q = cmd - 3 * c
+        op, v = self.cmds[c][q - 1]
+        body = {"PUT": f"={v}", "GET": "?"}.get(op, v)
+        return f"{self.servers + c}#{q}:{body}"
 
     @staticmethod
     def _ballot(cb: int) -> str:

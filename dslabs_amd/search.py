@@ -39,21 +39,30 @@ PRED_NONE_DECIDED = 4
 PRED_CLIENT_HAS_RESULTS = 5
 
 
+# combinators (dsl_predicate_id DSL_PRED_AND / _OR / _IMPLIES)
+PRED_AND = 900
+PRED_OR = 901
+PRED_IMPLIES = 902
+
+
 class StatePredicate:
     """A named state predicate evaluated on the device (StatePredicate.java).
 
     ``address_args`` names the positional args that are node addresses; they are resolved
     to node indices against the search state's address table when the search starts.
+    Combinators follow StatePredicate.and / or / implies (StatePredicate.java:397-431); ``and``
+    and ``or`` are Python keywords, so they are spelled ``and_`` / ``or_`` here.
     """
 
     def __init__(self, name: str, pred_id: int, arg0=0, arg1=0, negated: bool = False,
-                 address_args: Sequence[int] = ()):
+                 address_args: Sequence[int] = (), operands: Sequence["StatePredicate"] = ()):
         self.name = name
         self.pred_id = pred_id
         self.arg0 = arg0
         self.arg1 = arg1
         self.negated = negated
         self.address_args = tuple(address_args)
+        self.operands = tuple(operands)
 
     def negate(self) -> "StatePredicate":
         # StatePredicate.negate(): "¬(name)" or strip an existing "¬(...)".
@@ -61,9 +70,26 @@ class StatePredicate:
             name = self.name[2:-1]
         else:
             name = f"¬({self.name})"
-        return StatePredicate(name, self.pred_id, self.arg0, self.arg1, not self.negated, self.address_args)
+        return StatePredicate(name, self.pred_id, self.arg0, self.arg1, not self.negated, self.address_args,
+                              self.operands)
 
-    def _encode(self, state: "SearchState") -> _lib.dsl_predicate:
+    def and_(self, other: "StatePredicate") -> "StatePredicate":
+        return StatePredicate(f"({self.name}) ∧ ({other.name})", PRED_AND, operands=(self, other))
+
+    def or_(self, other: "StatePredicate") -> "StatePredicate":
+        return StatePredicate(f"({self.name}) ∨ ({other.name})", PRED_OR, operands=(self, other))
+
+    def implies(self, other: "StatePredicate") -> "StatePredicate":
+        return StatePredicate(f"({self.name}) → ({other.name})", PRED_IMPLIES, operands=(self, other))
+
+    def _encode(self, state: "SearchState", pool: list) -> _lib.dsl_predicate:
+        """The C ABI form; a combinator's operands are appended to ``pool`` (dsl_settings.pool)."""
+        if self.operands:
+            idx = []
+            for op in self.operands:
+                pool.append(op._encode(state, pool))
+                idx.append(len(pool) - 1)
+            return _lib.dsl_predicate(self.pred_id, 1 if self.negated else 0, idx[0], idx[1])
         args = [self.arg0, self.arg1]
         for i in self.address_args:
             args[i] = state.protocol.address_index(args[i])
@@ -242,13 +268,19 @@ class SearchSettings:
             s.receiver_active[proto.address_index(a)] = 1 if v else 0
         for a, v in self._timers_active.items():
             s.timers_active[proto.address_index(a)] = 1 if v else 0
+        pool = []
         for name, lst, arr in (("n_invariants", self._invariants, s.invariants),
                                ("n_goals", self._goals, s.goals), ("n_prunes", self._prunes, s.prunes)):
             if len(lst) > _lib.DSL_MAX_PREDICATES:
                 raise ValueError("too many predicates")
             setattr(s, name, len(lst))
             for i, p in enumerate(lst):
-                arr[i] = p._encode(state)
+                arr[i] = p._encode(state, pool)
+        if len(pool) > _lib.DSL_MAX_POOL:
+            raise ValueError("too many combinator operands")
+        s.n_pool = len(pool)
+        for i, p in enumerate(pool):
+            s.pool[i] = p
         s.table_log2_slots = self.table_log2_slots
         s.max_frontier_states = self.max_frontier_states
         return s

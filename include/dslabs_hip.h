@@ -37,6 +37,7 @@ extern "C" {
 #define DSL_ABI_VERSION 1
 #define DSL_MAX_NODES 32
 #define DSL_MAX_PREDICATES 16
+#define DSL_MAX_POOL 32          /* operands of combinator predicates (dsl_settings.pool) */
 #define DSL_MAX_PARAMS 64
 #define DSL_MAX_EVENT_FIELDS 8
 
@@ -94,11 +95,24 @@ typedef enum {
   DSL_PRED_SYNTH_NOT_ALL_MAX = 200, /* synthetic: not every node word at its maximum */
   DSL_PRED_SYNTH_COUNTER_LT = 201,  /* synthetic: node word arg0 < arg1 */
   DSL_PRED_APPENDS_LINEARIZABLE = 300, /* KVStoreWorkload.APPENDS_LINEARIZABLE */
-  DSL_PRED_LOGS_CONSISTENT = 400,   /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS */
+  DSL_PRED_LOGS_CONSISTENT = 400,   /* PaxosTest LOGS_CONSISTENT_ALL_SLOTS (PaxosTest.java:302-322) */
+  DSL_PRED_LOGS_CONSISTENT_ACTIVE = 401, /* PaxosTest LOGS_CONSISTENT (:282-300) */
+  DSL_PRED_SLOT_VALID = 402,        /* PaxosTest slotValid(i) (:276-279): arg0 = slot */
+  DSL_PRED_HAS_STATUS = 403,        /* PaxosTest hasStatus(a, i, s) (:113-117): arg0 = server node,
+                                       arg1 = slot << 4 | PaxosLogSlotStatus ordinal */
+  DSL_PRED_HAS_COMMAND = 404,       /* PaxosTest hasCommand(a, i, c) (:119-123): arg0 = server node,
+                                       arg1 = slot << 8 | KV command code (op << 2 | value; 0 = null) */
   DSL_PRED_PB_HAS_VIEW_REPLY = 500, /* PrimaryBackupTest.hasViewReply(n): arg0 = n */
   DSL_PRED_MINI_FOO = 700,          /* SearchAndTraceMinimizerTest foo: !a.foo */
   DSL_PRED_MINI_FOO_EXCEPTION = 701,    /* fooException: throws when a.foo, else true */
-  DSL_PRED_MINI_ALWAYS_EXCEPTION = 702  /* alwaysException: always throws */
+  DSL_PRED_MINI_ALWAYS_EXCEPTION = 702, /* alwaysException: always throws */
+  /* Combinators (T/StatePredicate.java:397-431): arg0 / arg1 index the operands in
+   * dsl_settings.pool (an operand may itself be a combinator of lower pool entries). With the
+   * reference's short-circuit semantics: a throwing left operand throws; and(a, b) is a when a
+   * is false, else b; or(a, b) is a when a is true, else b; implies(a, b) = or(negate(a), b). */
+  DSL_PRED_AND = 900,
+  DSL_PRED_OR = 901,
+  DSL_PRED_IMPLIES = 902
 } dsl_predicate_id;
 
 typedef struct {
@@ -124,9 +138,10 @@ typedef struct {
   dsl_predicate prunes[DSL_MAX_PREDICATES];
   /* engine capacity knobs (0 = automatic) */
   int32_t table_log2_slots; /* visited table = 2^k 8-byte slots (per shard) */
-  int32_t reserved0;
+  int32_t n_pool;           /* entries of pool[] */
   uint64_t max_frontier_states;
   uint64_t memory_budget_bytes;
+  dsl_predicate pool[DSL_MAX_POOL]; /* operands of DSL_PRED_AND / _OR / _IMPLIES predicates */
 } dsl_settings;
 
 typedef struct {

@@ -120,7 +120,22 @@ static Scenario build(const Args& a) {
       auto p = common(n);
       if (p) return *p;
       if (n == "LOGS_CONSISTENT_ALL_SLOTS") return multipaxos::logsConsistent(cfg);
+      if (n == "LOGS_CONSISTENT") return multipaxos::logsConsistent(cfg, true);
       if (n == "APPENDS_LINEARIZABLE") return multipaxos::appendsLinearizable(cfg);
+      auto parts = split(n, ':');
+      if (parts[0] == "slotValid" && parts.size() == 2) return multipaxos::slotValidPred(cfg, std::stoi(parts[1]));
+      if (parts[0] == "hasStatus" && parts.size() == 4) {  // hasStatus:serverK:slot:STATUS
+        static const std::map<std::string, multipaxos::Status> st = {
+            {"EMPTY", multipaxos::EMPTY}, {"ACCEPTED", multipaxos::ACCEPTED}, {"CHOSEN", multipaxos::CHOSEN}};
+        if (parts[3] == "CLEARED")  // never cleared (no garbage collection): always false
+          return Predicate{n, [](const State&) { PredResult r; r.value = false; return r; }};
+        return multipaxos::hasStatus(cfg, std::stoi(parts[1].substr(6)) - 1, std::stoi(parts[2]), st.at(parts[3]));
+      }
+      if (parts[0] == "hasCommand" && parts.size() >= 4) {  // hasCommand:serverK:slot:CMD (Cmd string form)
+        const std::string c = n.substr(n.find(':', n.find(':', 11) + 1) + 1);
+        return multipaxos::hasCommand(cfg, std::stoi(parts[1].substr(6)) - 1, std::stoi(parts[2]),
+                                      c == "null" ? multipaxos::Cmd{} : multipaxos::Cmd::parse("0#0:" + c));
+      }
       throw std::runtime_error("unknown predicate " + n);
     };
   } else if (a.proto == "amokv") {
@@ -178,12 +193,31 @@ static Scenario build(const Args& a) {
   return sc;
 }
 
+// A predicate argument: NAME, !P (negate), and(P,Q), or(P,Q), implies(P,Q), nested.
+static Predicate parsePred(const std::string& raw, Scenario& sc) {
+  if (!raw.empty() && raw[0] == '!') return parsePred(raw.substr(1), sc).negate();
+  for (const char* op : {"and(", "or(", "implies("}) {
+    const std::string o(op);
+    if (raw.rfind(o, 0) == 0 && raw.back() == ')') {
+      const std::string in = raw.substr(o.size(), raw.size() - o.size() - 1);
+      int depth = 0;
+      for (size_t k = 0; k < in.size(); k++) {
+        if (in[k] == '(') depth++;
+        else if (in[k] == ')') depth--;
+        else if (in[k] == ',' && depth == 0) {
+          Predicate x = parsePred(in.substr(0, k), sc), y = parsePred(in.substr(k + 1), sc);
+          return o == "and(" ? x.and_(y) : o == "or(" ? x.or_(y) : x.implies(y);
+        }
+      }
+      throw std::runtime_error("bad predicate " + raw);
+    }
+  }
+  return sc.pred(raw);
+}
+
 static Settings settingsFrom(const Args& a, Scenario& sc) {
   Settings st;
-  auto mk = [&](const std::string& raw) {
-    if (!raw.empty() && raw[0] == '!') return sc.pred(raw.substr(1)).negate();
-    return sc.pred(raw);
-  };
+  auto mk = [&](const std::string& raw) { return parsePred(raw, sc); };
   for (auto& n : a.all("inv")) st.invariants.push_back(mk(n));
   for (auto& n : a.all("goal")) st.goals.push_back(mk(n));
   for (auto& n : a.all("prune")) st.prunes.push_back(mk(n));

@@ -373,6 +373,45 @@ struct Predicate {
     };
     return p;
   }
+  // StatePredicate.and / or / implies (StatePredicate.java:397-431): the operands' functions are
+  // applied directly, so an exception in an evaluated operand propagates (the right operand is
+  // evaluated only when the left one does not decide).
+  Predicate and_(const Predicate& o) const {
+    Predicate p;
+    p.name = "(" + name + ") ∧ (" + o.name + ")";
+    auto f = fn, g = o.fn;
+    p.fn = [f, g](const State& s) {
+      PredResult r1 = f(s);
+      if (!r1.value) return r1;
+      PredResult r2 = g(s);
+      if (!r2.value) return r2;
+      PredResult r;
+      r.detail = "(" + r1.detail + ") and (" + r2.detail + ")";
+      return r;
+    };
+    return p;
+  }
+  Predicate or_(const Predicate& o) const {
+    Predicate p;
+    p.name = "(" + name + ") ∨ (" + o.name + ")";
+    auto f = fn, g = o.fn;
+    p.fn = [f, g](const State& s) {
+      PredResult r1 = f(s);
+      if (r1.value) return r1;
+      PredResult r2 = g(s);
+      if (r2.value) return r2;
+      PredResult r;
+      r.value = false;
+      r.detail = "(" + r1.detail + ") or (" + r2.detail + ")";
+      return r;
+    };
+    return p;
+  }
+  Predicate implies(const Predicate& o) const {
+    Predicate p = negate().or_(o);
+    p.name = "(" + name + ") → (" + o.name + ")";
+    return p;
+  }
 };
 
 struct Settings {

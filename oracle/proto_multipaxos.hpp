@@ -44,34 +44,57 @@ constexpr int kMaxSlots = 4;
 constexpr int kMaxRound = 15;
 constexpr int kTick = 100, kClientRetry = 100;
 
+// Workloads are KVStoreWorkload command / result templates on the key "foo"
+// (labs/lab1-clientserver/tst/dslabs/kvstore/KVStoreWorkload.java:40-66, :76-133).
 struct Config {
   int servers = 3, clients = 2;
-  std::vector<std::vector<std::string>> values;    // per client: appended values, in order
+  std::vector<std::vector<std::string>> cmds;      // per client: "APPEND:foo:X" / "PUT:foo:bar" / "GET:foo"
   std::vector<std::vector<std::string>> expected;  // per client: expected results (may be empty)
   static Config fromArgs(int servers, int clients, const std::string& workload, bool) {
     Config c;
     c.servers = servers;
     c.clients = clients;
     if (workload == "append-xy") {  // BASELINE C5: concurrent appends, results checked by linearizability
-      c.values = {{"X"}, {"Y"}};
+      c.cmds = {{"APPEND:foo:X"}, {"APPEND:foo:Y"}};
       c.expected = {{}, {}};
     } else if (workload == "append-xy-expect") {  // PaxosTest.test22: client1 -> X, client2 -> XY
-      c.values = {{"X"}, {"Y"}};
+      c.cmds = {{"APPEND:foo:X"}, {"APPEND:foo:Y"}};
       c.expected = {{"X"}, {"XY"}};
     } else if (workload == "append-x") {  // single client
-      c.values = {{"X"}};
+      c.cmds = {{"APPEND:foo:X"}};
       c.expected = {{"X"}};
     } else if (workload == "append-xz") {  // two commands from client1, one from client2
-      c.values = {{"X", "Z"}, {"Y"}};
+      c.cmds = {{"APPEND:foo:X", "APPEND:foo:Z"}, {"APPEND:foo:Y"}};
       c.expected = {{}, {}};
+    } else if (workload == "put-append-get") {  // KVStoreWorkload.putAppendGetWorkload (PaxosTest.test27)
+      c.cmds = {{"PUT:foo:bar", "APPEND:foo:baz", "GET:foo"}};
+      c.expected = {{"Ok", "barbaz", "barbaz"}};
     } else {
       throw std::runtime_error("unknown workload " + workload);
     }
-    c.values.resize(clients);
+    c.cmds.resize(clients);
     c.expected.resize(clients);
     return c;
   }
 };
+
+// KVStoreWorkload.parse for the templates above (the same forms as lab1's, proto_amokv.hpp).
+inline std::pair<Rec, Rec> parseKv(const std::string& c, const std::string& r) {
+  Rec cmd, res;
+  if (c.rfind("GET:", 0) == 0) {
+    cmd = Rec{"Get", {c.substr(4)}};
+    if (!r.empty()) res = r == "KeyNotFound" ? Rec{"KeyNotFound", {}} : Rec{"GetResult", {r}};
+  } else if (c.rfind("PUT:", 0) == 0) {
+    const size_t k = c.find(':', 4);
+    cmd = Rec{"Put", {c.substr(4, k - 4), c.substr(k + 1)}};
+    if (r == "Ok") res = Rec{"PutOk", {}};
+  } else {
+    const size_t k = c.find(':', 7);
+    cmd = Rec{"Append", {c.substr(7, k - 7), c.substr(k + 1)}};
+    if (!r.empty()) res = Rec{"AppendResult", {r}};
+  }
+  return {cmd, res};
+}
 
 struct Ballot {
   int round = 0, leader = 0;
@@ -86,14 +109,22 @@ struct Ballot {
   }
 };
 
-// An AMO command: (client address, seq, appended value). "" client = no-op.
+// An AMO command: (client address, seq, KV command on "foo"). client < 0 = no-op. String form:
+// "c#s:X" for Append(foo, X), "c#s:=X" for Put(foo, X), "c#s:?" for Get(foo).
 struct Cmd {
   int client = -1, seq = 0;
+  char op = 'A';  // 'A'ppend, 'P'ut, 'G'et
   std::string value;
   bool noop() const { return client < 0; }
-  bool operator==(const Cmd& o) const { return client == o.client && seq == o.seq && value == o.value; }
+  bool operator==(const Cmd& o) const {
+    return client == o.client && seq == o.seq && op == o.op && value == o.value;
+  }
+  // PaxosServer.command(i): the KV command (Lombok equals: type and fields), null for a no-op
+  bool sameKv(const Cmd& o) const { return noop() == o.noop() && (noop() || (op == o.op && value == o.value)); }
   std::string str() const {
-    return noop() ? "noop" : std::to_string(client) + "#" + std::to_string(seq) + ":" + value;
+    if (noop()) return "noop";
+    const std::string pre = std::to_string(client) + "#" + std::to_string(seq) + ":";
+    return op == 'P' ? pre + "=" + value : op == 'G' ? pre + "?" : pre + value;
   }
   static Cmd parse(const std::string& s) {
     Cmd c;
@@ -101,7 +132,15 @@ struct Cmd {
     size_t h = s.find('#'), k = s.find(':');
     c.client = std::stoi(s.substr(0, h));
     c.seq = std::stoi(s.substr(h + 1, k - h - 1));
-    c.value = s.substr(k + 1);
+    std::string v = s.substr(k + 1);
+    if (!v.empty() && v[0] == '=') {
+      c.op = 'P';
+      c.value = v.substr(1);
+    } else if (v == "?") {
+      c.op = 'G';
+    } else {
+      c.value = v;
+    }
     return c;
   }
 };
@@ -159,6 +198,7 @@ struct PaxosServer : Node {
   // application (derived from the executed prefix, kept explicitly like an AMOApplication)
   std::map<int, std::pair<int, std::string>> amo;  // client -> (last seq, result)
   std::string foo;
+  bool fooSet = false;  // the key exists (a Put or Append executed)
 
   std::shared_ptr<Node> clone() const override { return std::make_shared<PaxosServer>(*this); }
   void key(std::string& out) const override {
@@ -170,7 +210,7 @@ struct PaxosServer : Node {
       for (int v : p2bVotes[i]) out += std::to_string(v);
       out += ",";
     }
-    out += "|" + std::to_string(slotOut) + "," + std::to_string(slotIn) + "|" + foo + "}";
+    out += "|" + std::to_string(slotOut) + "," + std::to_string(slotIn) + "|" + (fooSet ? foo : "-") + "}";
   }
   std::string str() const override { return "PaxosServer(" + ballot.str() + ")"; }
 
@@ -193,15 +233,31 @@ struct PaxosServer : Node {
     }
   }
 
+  // KVStore.execute on "foo" (KVStore.java:59-78 as lab1 specifies it); the result as the reply
+  // carries it: "Ok" (PutOk), "KeyNotFound", or the value (AppendResult / GetResult).
+  std::string kvExecute(const Cmd& c) {
+    if (c.op == 'P') {
+      foo = c.value;
+      fooSet = true;
+      return "Ok";
+    }
+    if (c.op == 'A') {
+      foo += c.value;
+      fooSet = true;
+      return foo;
+    }
+    return fooSet ? foo : "KeyNotFound";
+  }
+
   void execute(Ctx& ctx) {
     while (slotOut <= kMaxSlots && log[slotOut].status == CHOSEN) {
       const Cmd& c = log[slotOut].cmd;
       if (!c.noop()) {
         auto it = amo.find(c.client);
         if (it == amo.end() || it->second.first < c.seq) {
-          foo += c.value;  // KVStore.append returns the new value
-          amo[c.client] = {c.seq, foo};
-          if (active) ctx.send(Rec{"PaxosReply", {std::to_string(c.seq), foo}}, c.client);
+          const std::string res = kvExecute(c);
+          amo[c.client] = {c.seq, res};
+          if (active) ctx.send(Rec{"PaxosReply", {std::to_string(c.seq), res}}, c.client);
         }
       }
       slotOut++;
@@ -367,6 +423,7 @@ struct PaxosClient : Client {
   int me = 0;
   int seq = 0;
   std::optional<Cmd> pending;
+  char pendingOp = 'A';  // the op of the last command sent (transient: implied by seq and the workload)
   std::optional<std::string> result;
 
   std::shared_ptr<Node> clone() const override { return std::make_shared<PaxosClient>(*this); }
@@ -377,13 +434,19 @@ struct PaxosClient : Client {
   std::string str() const override { return "PaxosClient(seq=" + std::to_string(seq) + ")"; }
   void sendCommand(const Rec& cmd, Ctx& ctx) override {
     seq++;
-    pending = Cmd{me, seq, cmd.f[1]};
+    Cmd c{me, seq, cmd.type == "Put" ? 'P' : cmd.type == "Get" ? 'G' : 'A', cmd.type == "Get" ? "" : cmd.f[1]};
+    pending = c;
+    pendingOp = c.op;
     result.reset();
     ctx.broadcast(Rec{"PaxosRequest", {pending->str()}}, servers);
     ctx.set(Rec{"ClientTimer", {std::to_string(seq)}}, kClientRetry);
   }
   bool hasResult() const override { return result.has_value(); }
-  Rec getResult() const override { return Rec{"AppendResult", {*result}}; }
+  Rec getResult() const override {  // typed by the command it answers
+    if (pendingOp == 'P') return Rec{"PutOk", {}};
+    if (pendingOp == 'G') return *result == "KeyNotFound" ? Rec{"KeyNotFound", {}} : Rec{"GetResult", {*result}};
+    return Rec{"AppendResult", {*result}};
+  }
   void handleMessage(const Rec& m, int, int, Ctx&) override {
     if (m.type != "PaxosReply") throw HandlerException("no handler");
     if (pending && std::stoi(m.f[0]) == seq) {
@@ -421,12 +484,10 @@ inline std::shared_ptr<State> initial(const Config& cfg, Names& names) {
     auto cw = std::make_shared<ClientWorker>();
     cw->client = pc;
     cw->addrName = names.addr.back();
-    for (auto& v : cfg.values[c]) cw->workload.cmds.push_back("APPEND:foo:" + v);
+    cw->workload.cmds = cfg.cmds[c];
     cw->workload.results = cfg.expected[c];
     cw->workload.numTimes = 1;
-    cw->workload.parser = [](const std::string& cmd, const std::string& res) {
-      return std::make_pair(Rec{"Append", {"foo", cmd.substr(11)}}, Rec{"AppendResult", {res}});
-    };
+    cw->workload.parser = parseKv;
     nodes.push_back(cw);
     kinds.push_back(Kind::ClientWorker);
   }
@@ -435,47 +496,93 @@ inline std::shared_ptr<State> initial(const Config& cfg, Names& names) {
 
 inline const PaxosServer* server(const State& s, int i) { return dynamic_cast<const PaxosServer*>(s.nodes[i].get()); }
 
-// PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (PaxosTest.java:290-322, slotValid :215-279) with
-// MARKERS_VALID (:128-193); firstNonCleared() == 1 since the log is never garbage-collected.
-inline Predicate logsConsistent(const Config& cfg) {
+// PaxosTest.slotValid(st, i) (PaxosTest.java:215-279). No garbage collection: firstNonCleared()
+// == 1, no slot is CLEARED, and command(i) is the KV command (null for EMPTY slots and no-ops).
+inline bool slotValid(const State& s, int N, int i, std::string* why) {
+  std::optional<Cmd> chosen;
+  bool isChosen = false;
+  for (int k = 0; k < N; k++) {
+    const PaxosServer* p = server(s, k);
+    const int nc = 1, ne = p->lastNonEmpty();
+    const Status st = p->status(i);
+    if (i < nc) {  // status(i) is not CLEARED (nothing ever is)
+      *why = "slot " + std::to_string(i) + " below the first non-cleared slot is not cleared";
+      return false;
+    }
+    if (i > ne && st != EMPTY) {
+      *why = "slot past the last non-empty one is not empty";
+      return false;
+    }
+    if (st == CHOSEN) {
+      const Cmd& c = p->log[i].cmd;
+      if (isChosen && !chosen->sameKv(c)) {
+        *why = "Two different commands chosen for slot " + std::to_string(i);
+        return false;
+      }
+      chosen = c;
+      isChosen = true;
+    }
+  }
+  if (!isChosen) return true;
+  int count = 0;
+  for (int k = 0; k < N; k++) {
+    const PaxosServer* p = server(s, k);
+    const Status st = p->status(i);
+    if (st != EMPTY && (st != ACCEPTED || p->log[i].cmd.sameKv(*chosen))) count++;
+  }
+  if (2 * count <= N) {
+    *why = "chosen for slot " + std::to_string(i) + " without a majority accepting";
+    return false;
+  }
+  return true;
+}
+
+// PaxosTest.LOGS_CONSISTENT_ALL_SLOTS (:302-322) and LOGS_CONSISTENT (:282-300; from the smallest
+// firstNonCleared(), i.e. 1, so the two coincide), each with MARKERS_VALID (:128-193), which holds
+// by construction here (firstNonCleared() == 1, lastNonEmpty() the last non-EMPTY slot).
+inline Predicate logsConsistent(const Config& cfg, bool active = false) {
   int N = cfg.servers;
-  return {"Non-empty log slots consistent", [N](const State& s) {
+  return {active ? "Active log slots consistent" : "Non-empty log slots consistent", [N](const State& s) {
             PredResult r;
             int maxNe = 0;
             for (int i = 0; i < N; i++) maxNe = std::max(maxNe, server(s, i)->lastNonEmpty());
-            for (int slot = 1; slot <= maxNe; slot++) {
-              std::optional<Cmd> chosen;
-              bool isChosen = false;
-              for (int i = 0; i < N; i++) {
-                const PaxosServer* p = server(s, i);
-                if (p->status(slot) == CHOSEN) {
-                  const Cmd& c = p->log[slot].cmd;
-                  // command(i) returns the KV command (null for a no-op); compare that
-                  if (isChosen && !(chosen->noop() && c.noop()) &&
-                      (chosen->noop() != c.noop() || chosen->value != c.value)) {
-                    r.value = false;
-                    r.detail = "Two different commands chosen for slot " + std::to_string(slot);
-                    return r;
-                  }
-                  chosen = c;
-                  isChosen = true;
-                }
-              }
-              if (!isChosen) continue;
-              int count = 0;
-              for (int i = 0; i < N; i++) {
-                const PaxosServer* p = server(s, i);
-                Status st = p->status(slot);
-                bool same = st != EMPTY && (p->log[slot].cmd.noop() == chosen->noop()) &&
-                            (chosen->noop() || p->log[slot].cmd.value == chosen->value);
-                if (st != EMPTY && (st != ACCEPTED || same)) count++;
-              }
-              if (2 * count <= N) {
+            for (int slot = 1; slot <= maxNe; slot++)
+              if (!slotValid(s, N, slot, &r.detail)) {
                 r.value = false;
-                r.detail = "chosen for slot " + std::to_string(slot) + " without a majority accepting";
                 return r;
               }
-            }
+            return r;
+          }};
+}
+inline Predicate slotValidPred(const Config& cfg, int i) {
+  int N = cfg.servers;
+  return {"Logs consistent for slot " + std::to_string(i), [N, i](const State& s) {
+            PredResult r;
+            r.value = slotValid(s, N, i, &r.detail);
+            return r;
+          }};
+}
+// PaxosTest.hasStatus(a, i, s) (:113-117): ((PaxosServer) st.server(a)).status(i) == s.
+inline Predicate hasStatus(const Config& cfg, int a, int i, Status want) {
+  int N = cfg.servers;
+  return {"has status", [N, a, i, want](const State& s) {
+            if (a < 0 || a >= N) throw HandlerException("not a PaxosServer");
+            PredResult r;
+            r.value = server(s, a)->status(i) == want;
+            return r;
+          }};
+}
+// PaxosTest.hasCommand(a, i, c) (:119-123): Objects.equals(command(i), c); c as a Cmd ("noop" =
+// null; only its KV command is compared).
+inline Predicate hasCommand(const Config& cfg, int a, int i, const Cmd& want) {
+  int N = cfg.servers;
+  return {"has command", [N, a, i, want](const State& s) {
+            if (a < 0 || a >= N) throw HandlerException("not a PaxosServer");
+            const PaxosServer* p = server(s, a);
+            Cmd have;  // null unless the slot holds a (non-no-op) command
+            if (p->status(i) != EMPTY) have = p->log[i].cmd;
+            PredResult r;
+            r.value = have.sameKv(want);
             return r;
           }};
 }
@@ -489,8 +596,14 @@ inline Predicate appendsLinearizable(const Config& cfg) {
               const ClientWorker* cw = s.cw(a);
               int ci = a - cfg.servers;
               for (size_t k = 0; k < cw->results.size(); k++) {
+                const std::string& tmpl = cfg.cmds[ci][k];
+                if (tmpl.rfind("APPEND:", 0) != 0) throw std::runtime_error("Client workers have non-Append Commands");
+                const std::string val = tmpl.substr(tmpl.find(':', 7) + 1);
+                if (cw->results[k].type != "AppendResult") {
+                  r.value = false;
+                  return r;
+                }
                 const std::string& res = cw->results[k].f[0];
-                const std::string& val = cfg.values[ci][k];
                 if (res.size() < val.size() || res.compare(res.size() - val.size(), val.size(), val) != 0) {
                   r.value = false;
                   return r;

@@ -33,8 +33,20 @@ def protocol(args):
 
 
 def predicate(proto, name):
-    neg = name.startswith("!")
-    name = name.lstrip("!")
+    """An oracle predicate argument: NAME, !P, and(P,Q), or(P,Q), implies(P,Q) (nested)."""
+    if name.startswith("!"):
+        return predicate(proto, name[1:]).negate()
+    for op in ("and(", "or(", "implies("):
+        if name.startswith(op) and name.endswith(")"):
+            inner, depth = name[len(op):-1], 0
+            for k, ch in enumerate(inner):
+                depth += ch == "("
+                depth -= ch == ")"
+                if ch == "," and depth == 0:
+                    a, b = predicate(proto, inner[:k]), predicate(proto, inner[k + 1:])
+                    return a.and_(b) if op == "and(" else a.or_(b) if op == "or(" else a.implies(b)
+            raise ValueError(name)
+    neg = False
     std = {"RESULTS_OK": RESULTS_OK, "CLIENTS_DONE": CLIENTS_DONE, "NONE_DECIDED": NONE_DECIDED}
     if name in std:
         p = std[name]

@@ -90,6 +90,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   int v = judge_view<P>(v0, prm, set, 0, &pi);
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
+  long long nterm[3] = {0, 0, 0};
   long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0, dup_sends = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
@@ -117,6 +118,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         if ((int)per.size() <= d) per.resize(d + 1, 0);
         per[d]++;
         if (tdepth < 0) tdepth = d;
+        if (d == tdepth) nterm[0]++;
         best = std::min(best, (int)V_TERM_EXCEPTION);
         continue;
       }
@@ -148,6 +150,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       }
       if (v >= V_TERM_EXCEPTION) {
         if (tdepth < 0) tdepth = d;
+        if (d == tdepth) nterm[v - V_TERM_EXCEPTION]++;
         if (first_term_parent == -2) first_term_parent = n.id, first_term_event = k;
         best = std::min(best, v);
         continue;
@@ -167,7 +170,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];
   }
-  printf("],\"states\":%llu,\"successors\":%lld,\"noop_successors\":%lld", total, succ, noop);
+  printf("],\"terminals_at_depth\":[%lld,%lld,%lld],\"states\":%llu,\"successors\":%lld,\"noop_successors\":%lld", nterm[0], nterm[1], nterm[2], total, succ, noop);
   if (first_term_parent >= 0) {
     std::vector<int> evs{first_term_event};
     for (long long id = first_term_parent; id > 0; id = parent[id].first) evs.push_back(parent[id].second);
@@ -278,7 +281,7 @@ int main(int argc, char** argv) {
   for (int a = 0; a < DSL_MAX_NODES; a++) set.deliver[a] = 0xffffffffu;
   set.timer_mask = 0xffffffffu;
   set.all_deliver = 1;
-  DevPred* lists[3] = {set.inv, set.goal, set.prune};
+  DevProg* lists[3] = {set.inv, set.goal, set.prune};
   int* counts[3] = {&set.n_inv, &set.n_goal, &set.n_prune};
   int which = 0;
   for (; i < argc - 1; i++) {
@@ -286,16 +289,28 @@ int main(int argc, char** argv) {
       which++;
       continue;
     }
-    // predicate token: [-]id[:arg0[:arg1]] (leading '-' = negated)
-    int id = 0;
-    long long a0 = 0, a1 = 0;
-    sscanf(argv[i], "%d:%lld:%lld", &id, &a0, &a1);
-    DevPred p{};
-    p.negate = id < 0;
-    p.id = id < 0 ? -id : id;
-    p.arg0 = a0;
-    p.arg1 = a1;
-    lists[which][(*counts[which])++] = p;
+    // predicate token: a leaf [-]id[:arg0[:arg1]] (leading '-' = negated), or a postfix program of
+    // leaves and the combinators "and" / "or" / "not" joined by commas
+    const int start = set.n_ops;
+    for (const char* tok = argv[i]; *tok;) {
+      const char* end = strchr(tok, ',');
+      std::string t(tok, end ? (size_t)(end - tok) : strlen(tok));
+      DevPred p{};
+      if (t == "and") p.id = kOpAnd;
+      else if (t == "or") p.id = kOpOr;
+      else if (t == "not") p.id = kOpNot;
+      else {
+        int id = 0, a0 = 0, a1 = 0;
+        sscanf(t.c_str(), "%d:%d:%d", &id, &a0, &a1);
+        p.negate = id < 0;
+        p.id = id < 0 ? -id : id;
+        p.arg0 = a0;
+        p.arg1 = a1;
+      }
+      set.ops[set.n_ops++] = p;
+      tok = end ? end + 1 : tok + t.size();
+    }
+    lists[which][(*counts[which])++] = DevProg{(int16_t)start, (int16_t)(set.n_ops - start)};
   }
   set.max_depth = atoi(argv[argc - 1]);
   switch (d.protocol) {

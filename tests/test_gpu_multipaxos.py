@@ -88,3 +88,46 @@ def test_test22_two_phase_search():
     assert r2.initial_depth == first.depth()
     assert rep["ok"] and rep["goals"][0]["value"], rep
     assert rep["depth"] == r2.goalMatchingState().depth()
+
+
+# PaxosTest.test27 (PaxosTest.java:1214-1228): singleton Paxos, putAppendGetWorkload; the goal
+# CLIENTS_DONE is reached at depth exactly 6, then the space with CLIENTS_DONE pruned is exhausted.
+# lab3 predicates (PaxosTest.java:113-346) and StatePredicate combinators (:397-431).
+LIVE = {
+    "test27_goal": ["--proto", "multipaxos", "--servers", "1", "--clients", "1", "--workload", "put-append-get",
+                    "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE", "--max-depth", "6"],
+    "test27_exhaustive": ["--proto", "multipaxos", "--servers", "1", "--clients", "1", "--workload",
+                          "put-append-get", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"],
+    "goal_has_status": ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
+                        "LOGS_CONSISTENT", "--goal", "hasStatus:server2:1:CHOSEN", "--max-depth", "10"],
+    "inv_implies": ["--proto", "multipaxos", "--workload", "append-xy", "--inv",
+                    "implies(hasStatus:server1:1:CHOSEN,hasCommand:server1:1:X)", "--inv", "slotValid:1",
+                    "--max-depth", "10"],
+    "goal_and_or": ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "LOGS_CONSISTENT_ALL_SLOTS",
+                    "--goal", "and(hasStatus:server1:2:CHOSEN,or(hasStatus:server2:2:ACCEPTED,"
+                    "!hasStatus:server3:2:EMPTY))", "--max-depth", "9"],
+    "c5_lab3_invariants": ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
+                           "LOGS_CONSISTENT", "--inv", "and(slotValid:1,slotValid:2)", "--inv",
+                           "APPENDS_LINEARIZABLE", "--max-depth", "10"],
+}
+
+
+@pytest.mark.parametrize("name", sorted(LIVE))
+def test_multipaxos_lab3_predicates_and_test27(name):
+    args = LIVE[name]
+    want = oracle_util.run("bfs", args + ["--finish-level"], timeout=300)
+    proto = argmap.protocol(args)
+    r = Search.bfs(proto.initial_state(), argmap.settings(args, proto))
+    assert r.endCondition().name == want["end"]
+    assert r.per_depth == want["per_depth"]
+    st = r.invariantViolatingState() or r.goalMatchingState()
+    if name == "test27_goal":
+        assert r.endCondition() == EndCondition.GOAL_FOUND and st.depth() == 6
+    if st is not None:
+        rep = oracle_util.replay(args, st.trace())
+        assert rep["ok"], rep["error"]
+        assert rep["depth"] == st.depth()
+        if r.endCondition() == EndCondition.INVARIANT_VIOLATED:
+            assert not all(i["value"] for i in rep["invariants"])
+        else:
+            assert rep["goals"][0]["value"]

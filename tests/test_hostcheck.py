@@ -9,8 +9,19 @@ import subprocess
 import pytest
 
 import oracle_util
+from dslabs_amd.protocols import MultiPaxos
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def mp(servers, clients, workload):
+    """protocheck's protocol arguments for Multi-Paxos: the id, then the engine's parameters."""
+    return [5] + MultiPaxos(servers, clients, workload).params()
+
+
+_MP3 = ["--inv", "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE"]
+_PAG = mp(1, 1, "put-append-get")
+_X = MultiPaxos(3, 2, "append-xy").kv_code("APPEND:foo:X")
 SRC = os.path.join(ROOT, "tests", "hostcheck", "protocheck.cpp")
 BIN = os.path.join(ROOT, "tests", "hostcheck", "_build", "protocheck")
 
@@ -57,16 +68,37 @@ CASES = {
     "sip_2p5a_d6": ([2, 2, 5, 0, "--", 101, 100, "/", "/", 6],
                     ["--proto", "sipaxos", "--proposers", "2", "--acceptors", "5", "--values", "a,b", "--inv",
                      "Integrity", "--inv", "Agreement", "--max-depth", "6"]),
-    "mp_c5_d10": ([5, 3, 2, 1, 1, 0, -1, -1, 1, 2, 0, -1, -1, "--", 1, 400, 300, "/", "/", 10],
-                  ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
-                   "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--max-depth", "10"]),
-    "mp_xz_d8": ([5, 3, 2, 2, 1, 3, -1, -1, 1, 2, 0, -1, -1, "--", 1, 400, 300, "/", "/", 8],
-                 ["--proto", "multipaxos", "--workload", "append-xz", "--inv", "RESULTS_OK", "--inv",
-                  "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--max-depth", "8"]),
-    "mp_2s1c_d11": ([5, 2, 1, 1, 1, 0, 9, -1, 0, 0, 0, -1, -1, "--", 1, 400, 300, "/", "/", 2, 11],
-                    ["--proto", "multipaxos", "--servers", "2", "--clients", "1", "--workload", "append-x", "--inv",
-                     "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--inv", "APPENDS_LINEARIZABLE", "--prune",
-                     "CLIENTS_DONE", "--max-depth", "11"]),
+    "mp_c5_d10": (mp(3, 2, "append-xy") + ["--", 1, 400, 300, "/", "/", 10],
+                  ["--proto", "multipaxos", "--workload", "append-xy"] + _MP3 + ["--max-depth", "10"]),
+    "mp_xz_d8": (mp(3, 2, "append-xz") + ["--", 1, 400, 300, "/", "/", 8],
+                 ["--proto", "multipaxos", "--workload", "append-xz"] + _MP3 + ["--max-depth", "8"]),
+    "mp_2s1c_d11": (mp(2, 1, "append-x") + ["--", 1, 400, 300, "/", "/", 2, 11],
+                    ["--proto", "multipaxos", "--servers", "2", "--clients", "1", "--workload", "append-x"] + _MP3 +
+                    ["--prune", "CLIENTS_DONE", "--max-depth", "11"]),
+    # PaxosTest.test27 (PaxosTest.java:1214-1228): singleton Paxos, putAppendGetWorkload, goal
+    # CLIENTS_DONE at depth exactly 6; then exhaustive with CLIENTS_DONE pruned
+    "mp_test27_goal": (_PAG + ["--", 1, "/", 2, "/", 6],
+                       ["--proto", "multipaxos", "--servers", "1", "--clients", "1", "--workload", "put-append-get",
+                        "--inv", "RESULTS_OK", "--goal", "CLIENTS_DONE", "--max-depth", "6", "--finish-level"]),
+    "mp_test27_exhaustive": (_PAG + ["--", 1, "/", "/", 2, -1],
+                             ["--proto", "multipaxos", "--servers", "1", "--clients", "1", "--workload",
+                              "put-append-get", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE"]),
+    # lab3 predicates (PaxosTest.java:113-346) and StatePredicate combinators (:397-431)
+    "mp_goal_has_status": (mp(3, 2, "append-xy") + ["--", 1, 401, "/", f"403:1:{(1 << 4) | 2}", "/", 10],
+                           ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "RESULTS_OK", "--inv",
+                            "LOGS_CONSISTENT", "--goal", "hasStatus:server2:1:CHOSEN", "--max-depth", "10",
+                            "--finish-level"]),
+    "mp_inv_implies": (mp(3, 2, "append-xy") + ["--", f"403:0:{(1 << 4) | 2},not,404:0:{(1 << 8) | _X},or", "402:1",
+                                                "/", "/", 10],
+                       ["--proto", "multipaxos", "--workload", "append-xy", "--inv",
+                        "implies(hasStatus:server1:1:CHOSEN,hasCommand:server1:1:X)", "--inv", "slotValid:1",
+                        "--max-depth", "10", "--finish-level"]),
+    "mp_goal_and_or": (mp(3, 2, "append-xy") + ["--", 400, "/",
+                                                f"403:0:{(2 << 4) | 2},403:1:{(2 << 4) | 1},-403:2:{(2 << 4) | 0},or,and",
+                                                "/", 9],
+                       ["--proto", "multipaxos", "--workload", "append-xy", "--inv", "LOGS_CONSISTENT_ALL_SLOTS",
+                        "--goal", "and(hasStatus:server1:2:CHOSEN,or(hasStatus:server2:2:ACCEPTED,"
+                        "!hasStatus:server3:2:EMPTY))", "--max-depth", "9", "--finish-level"]),
     # synthetic C3: nodes K P seed -- invariant NOT_ALL_MAX (200)
     "synth_c3_d6": ([3, 5, 64, 7, 0x5EEDD51AB5, "--", 200, "/", "/", 6],
                     ["--proto", "synthetic", "--inv", "NOT_ALL_MAX", "--max-depth", "6"]),
