@@ -183,6 +183,7 @@ struct BfsEngine : EngineBase {
   uint64_t queue_flimit(uint64_t span) const {
     return W > 1 ? std::min<uint64_t>(span / 4, rep_threshold() - 1) : span / 4;
   }
+  double q_ms_per_level = 0;       // the last queue's device time per level
   unsigned char* qctr = nullptr;   // kQueue + 1 counter sets
   unsigned char* hq = nullptr;     // pinned copy of the kQueue sets
   std::vector<hipEvent_t> qev;     // brackets the whole queue (no event packets between its levels)
@@ -375,7 +376,10 @@ struct BfsEngine : EngineBase {
   }
 
   // Enqueues up to kQueue levels of shard 0 (see the members above); returns how many ran.
-  int enqueue_queue(int depth, const Table& tbl_proto, double growth, int* ran) {
+  // elapsed_ms: the search's time so far; with a time limit, the queue holds no more levels than
+  // the remaining budget covers at the last queue's measured time per level (SearchSettings
+  // maxTimeSecs is checked between levels, so a queue never runs far past it).
+  int enqueue_queue(int depth, const Table& tbl_proto, double growth, double elapsed_ms, int* ran) {
     Shard& S = sh[0];
     if (!qctr) {
       DSL_HIP(hipMalloc(&qctr, (size_t)(kQueue + 1) * kCtrSet));
@@ -394,7 +398,9 @@ struct BfsEngine : EngineBase {
     }
     q_segcap = span / nseg;
     // levels: up to kQueue, none past max_depth (its level's successors are all pruned)
-    const int nq = hset.max_depth >= 0 ? std::max(1, std::min(kQueue, hset.max_depth - depth)) : kQueue;
+    int nq = hset.max_depth >= 0 ? std::max(1, std::min(kQueue, hset.max_depth - depth)) : kQueue;
+    if (hset.max_time_ms > 0 && q_ms_per_level > 0)
+      nq = std::max(1, std::min(nq, (int)((hset.max_time_ms - elapsed_ms) / q_ms_per_level)));
     const uint64_t flimit = queue_flimit(span), wlimit = 8 * span;
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
@@ -481,6 +487,8 @@ struct BfsEngine : EngineBase {
         break;
       }
     }
+    float qms = 0;
+    if (hipEventElapsedTime(&qms, qev[0], qev[1]) == hipSuccess) q_ms_per_level = (double)qms / *ran;
     return DSL_OK;
   }
 
@@ -709,7 +717,8 @@ struct BfsEngine : EngineBase {
               nd >= 2 && per_depth[nd - 2] ? std::max(1.0, (double)per_depth[nd - 1] / per_depth[nd - 2]) : 3.0;
           int ran = 0;
           const auto tq0 = std::chrono::steady_clock::now();
-          DSL_TRY(enqueue_queue(depth, tbl_proto, growth, &ran));
+          DSL_TRY(enqueue_queue(depth, tbl_proto, growth,
+                                std::chrono::duration<double, std::milli>(tq0 - t_start).count(), &ran));
           if (trace_levels)
             fprintf(stderr, "[queue] enqueue+run %.4f ms (loop entry %.4f ms after start)\n",
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tq0).count(),

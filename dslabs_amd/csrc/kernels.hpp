@@ -900,7 +900,7 @@ namespace dsl {
 struct DfsArgs {
   const uint32_t* init;
   int32_t init_depth;
-  int32_t tcap;              // events a probe may record (longer probes are restarted)
+  int32_t tcap;              // events a probe may record (a probe at depth tcap is restarted)
   uint32_t* rows;            // 2 rows per probe (current / successor)
   uint32_t* trace;           // tcap events per probe
   int32_t* pdepth;           // steps taken by the probe; -1 = start a new probe
@@ -938,6 +938,10 @@ __global__ void __launch_bounds__(kBlock) k_dfs(DfsArgs a, typename P::Params pr
         c_probes++;
         c_states++;
       }
+      if (dep >= a.tcap) {  // a successor would be too deep to record: restart before stepping
+        dep = -1;
+        continue;
+      }
       const uint32_t* w = base + cur * NW;
       uint32_t* nxt = base + (cur ^ 1) * NW;
       const int ne = count_events<P>(w, prm, set);
@@ -961,7 +965,7 @@ __global__ void __launch_bounds__(kBlock) k_dfs(DfsArgs a, typename P::Params pr
           v = judge_view<P>(view, prm, set, a.init_depth + dep + 1, &pi);
         }
         if (v >= V_TERM_EXCEPTION) {
-          if (dep < a.tcap) a.trace[lane * a.tcap + dep] = (uint32_t)k;
+          a.trace[lane * a.tcap + dep] = (uint32_t)k;
           if (atomicCAS(a.found, 0, (int)(lane + 1)) == 0) {
             a.term[0] = v;
             a.term[1] = pi;
@@ -971,10 +975,6 @@ __global__ void __launch_bounds__(kBlock) k_dfs(DfsArgs a, typename P::Params pr
           break;
         }
         if (v == V_PRUNED) continue;
-        if (dep >= a.tcap) {  // too long to record: restart
-          ended = true;
-          break;
-        }
         a.trace[lane * a.tcap + dep] = (uint32_t)k;
         dep++;
         cur ^= 1;

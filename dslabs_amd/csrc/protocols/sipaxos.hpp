@@ -3,7 +3,8 @@
 // Re-expresses framework/tst/dslabs/framework/testing/visualization/examples/paxosmadesimple/
 // SingleInstancePaxos.java:177-293 (Proposer.onPropose / handlePrepareAck / handleAcceptAck,
 // Acceptor.handlePrepare / handleAccept), :296-323 (messages, Propose timer = 100 ms) and the
-// buggy acceptor of IncorrectSingleInstancePaxos.java:29-64 (accepts regardless of promise).
+// BadProposer of IncorrectSingleInstancePaxos.java:42-64 (decides once acceptAcks * 2 >=
+// acceptors - 1, i.e. without a majority).
 //
 // Nodes: proposers 0..P-1 ("proposer1.."), acceptors P..P+A-1 ("acceptor1..").
 // Proposal values are interned: value id v in 1..P = the initial proposal of proposer v.
@@ -131,7 +132,7 @@ struct SIPaxos {
       }
       case T_ACCEPT: {  // Acceptor.handleAccept
         const int hp = get(w, 0, 8);
-        if (!p.incorrect && hp != 0 && hp > r_n(m)) return STEP_OK;
+        if (hp != 0 && hp > r_n(m)) return STEP_OK;
         out.send(rec(T_ACCEPT_ACK, i, from, r_n(m), 0, 0));
         const int han = get(w, 8, 8);
         if (han == 0 || han < r_n(m)) {
@@ -140,11 +141,12 @@ struct SIPaxos {
         }
         return STEP_OK;
       }
-      default: {  // Proposer.handleAcceptAck
+      default: {  // Proposer.handleAcceptAck (BadProposer: acks * 2 >= acceptors - 1)
         if (pnum(w) != r_n(m)) return STEP_OK;
         const int acks = accept_acks(w) | (1 << (from - p.proposers));
         put(w, 6, 5, acks);
-        if (__builtin_popcount(acks) * 2 > p.acceptors) put(w, 4, 2, value(w));
+        const int acks2 = __builtin_popcount(acks) * 2;
+        if (p.incorrect ? acks2 >= p.acceptors - 1 : acks2 > p.acceptors) put(w, 4, 2, value(w));
         return STEP_OK;
       }
     }

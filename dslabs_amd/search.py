@@ -253,7 +253,7 @@ class SearchSettings:
         proto = state.protocol
         s = _lib.dsl_settings()
         s.max_depth = self._max_depth
-        s.max_time_ms = self._max_time_secs * 1000 if self._max_time_secs > 0 else -1
+        s.max_time_ms = max(1, int(round(self._max_time_secs * 1000))) if self._max_time_secs > 0 else -1
         s.network_active = 1 if self._network_active else 0
         s.deliver_timers = 1 if self._deliver_timers else 0
         ctypes.memset(ctypes.addressof(s.link_active), 0xFF, ctypes.sizeof(s.link_active))
@@ -431,14 +431,14 @@ class Engine:
         return self._results(state, settings, res_p)
 
     def dfs(self, state: SearchState, settings: Optional[SearchSettings] = None, probes: int = 65536,
-            seed: int = 0, max_probes: int = 0, minimize: bool = True) -> SearchResults:
+            seed: int = 0, max_probes: int = 0, minimize: bool = True, max_trace: int = 0) -> SearchResults:
         """Search.dfs / RandomDFS (Search.java:397-402, :507-583) on the device: `probes` random
         walks at once until a terminal state, settings.maxTimeSecs, or `max_probes` probes. The
         terminal's trace is minimized as RandomDFS does (TraceMinimizer) unless minimize=False."""
         if settings is None:
             settings = SearchSettings()
         self._prepare(state, settings)
-        c = _lib.dsl_dfs_config(probes, seed & ((1 << 64) - 1), max_probes, 0, 0, 0 if minimize else 1, 0)
+        c = _lib.dsl_dfs_config(probes, seed & ((1 << 64) - 1), max_probes, 0, max_trace, 0 if minimize else 1, 0)
         res_p = ctypes.POINTER(_lib.dsl_result)()
         check(self.lib.dsl_run_dfs(self.handle, ctypes.byref(c), ctypes.byref(res_p)), "dsl_run_dfs")
         return self._results(state, settings, res_p)

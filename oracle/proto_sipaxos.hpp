@@ -4,7 +4,8 @@
 //   SingleInstancePaxos.java:50-127 (initial state: proposers "proposer1..", acceptors
 //   "acceptor1.."; invariants Integrity/Agreement, goal Termination), :177-293 (Proposer /
 //   Acceptor handlers), :296-323 (messages, Propose timer).
-//   IncorrectSingleInstancePaxos.java:29-64 (buggy acceptor: accepts regardless of promise).
+//   IncorrectSingleInstancePaxos.java:29-64 (BadProposer.handleAcceptAck, :54-63: decides once
+//   acceptAcks.size() * 2 >= acceptors.length - 1, i.e. without a majority).
 // Lombok equality: Proposer includes hasProposed, numProposers, acceptors, proposalValue,
 // proposalNumber, prepareFinished, prepareAcks (map), acceptAcks (set), decision.
 #pragma once
@@ -24,6 +25,7 @@ struct Proposer : Node {
   std::map<int, Rec> prepareAcks;  // sender -> PrepareAck
   std::set<int> acceptAcks;
   std::optional<std::string> decision;
+  bool incorrect = false;  // IncorrectSingleInstancePaxos BadProposer
 
   std::shared_ptr<Node> clone() const override { return std::make_shared<Proposer>(*this); }
   void key(std::string& out) const override {
@@ -77,7 +79,8 @@ struct Proposer : Node {
       int n = std::stoi(m.f[0]);
       if (proposalNumber != n) return;
       acceptAcks.insert(from);
-      if (acceptAcks.size() * 2 > acceptors.size()) decision = proposalValue;
+      const size_t acks2 = acceptAcks.size() * 2;
+      if (incorrect ? acks2 + 1 >= acceptors.size() : acks2 > acceptors.size()) decision = proposalValue;
     } else {
       throw HandlerException("no handler");
     }
@@ -85,7 +88,6 @@ struct Proposer : Node {
 };
 
 struct Acceptor : Node {
-  bool incorrect = false;  // IncorrectSingleInstancePaxos acceptor
   std::optional<int> highestPrepared;
   std::optional<std::pair<int, std::string>> highestAccepted;
 
@@ -106,7 +108,7 @@ struct Acceptor : Node {
       if (highestAccepted) ack.f = {std::to_string(n), std::to_string(highestAccepted->first), highestAccepted->second};
       ctx.send(ack, from);
     } else if (m.type == "Accept") {
-      if (!incorrect && highestPrepared && *highestPrepared > n) return;
+      if (highestPrepared && *highestPrepared > n) return;
       ctx.send(Rec{"AcceptAck", {std::to_string(n)}}, from);
       if (!highestAccepted || highestAccepted->first < n) highestAccepted = std::make_pair(n, m.f[1]);
     } else {
@@ -129,13 +131,13 @@ inline std::shared_ptr<State> initial(int P, int A, const std::vector<std::strin
     n->numProposers = P;
     n->proposalNumber = p + 1;
     n->proposalValue = values[p];
+    n->incorrect = incorrect;
     nodes.push_back(n);
     kinds.push_back(Kind::Server);
   }
   for (int a = 0; a < A; a++) {
     names.addr.push_back("acceptor" + std::to_string(a + 1));
     auto n = std::make_shared<Acceptor>();
-    n->incorrect = incorrect;
     nodes.push_back(n);
     kinds.push_back(Kind::Server);
   }

@@ -77,7 +77,7 @@ LAB0 = {
 def gen(cases, fname):
     out = {}
     for name, c in cases.items():
-        r = oracle_util.run("bfs", c["args"], timeout=600)
+        r = oracle_util.run("bfs", c["args"], timeout=c.get("timeout", 600))
         if r.get("terminals"):
             t = r["terminals"]
             r["terminal_depth"] = t[0]["depth"]
@@ -102,6 +102,8 @@ def gen_lab0_sip():
         "sipaxos_2p3a_d6": dict(
             args=["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
                   "Integrity", "--inv", "Agreement", "--max-depth", "6"], pinned={}),
+        # IncorrectSingleInstancePaxos (BadProposer, :53-63): no Agreement violation through depth 11
+        # (the first one is at depth 14, found on the GPU; tests/test_gpu_sipaxos.py replays it here)
         "sipaxos_incorrect_2p3a": dict(
             args=["--proto", "sipaxos", "--proposers", "2", "--acceptors", "3", "--values", "a,b", "--inv",
                   "Integrity", "--inv", "Agreement", "--incorrect", "--max-depth", "11", "--finish-level"],
@@ -137,12 +139,16 @@ MULTIPAXOS = {
     "mp_expect_violation": dict(args=MP + ["--workload", "append-xy-expect", "--inv", "RESULTS_OK", "--inv",
                                            "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "CLIENTS_DONE", "--finish-level"],
                                 pinned={}),
-    # PaxosTest.test27-style singleton group: CLIENTS_DONE after 2 steps per command
+    # PaxosTest.test27 (:1214-1228): singleton group, putAppendGetWorkload, CLIENTS_DONE at depth 6
+    "mp_test27": dict(args=MP + ["--servers", "1", "--clients", "1", "--workload", "put-append-get", "--inv",
+                                 "RESULTS_OK", "--goal", "CLIENTS_DONE", "--finish-level"],
+                      pinned={"terminal_depth": 6, "end": "GOAL_FOUND",
+                              "source": "labs/lab3-paxos/tst/dslabs/paxos/PaxosTest.java:1214-1228 "
+                                        "(assertGoalFound, goal depth 6)"}),
+    # singleton group, one command: CLIENTS_DONE after 2 steps
     "mp_singleton": dict(args=MP + ["--servers", "1", "--clients", "1", "--workload", "append-x"] + INV3 +
                          ["--goal", "CLIENTS_DONE", "--finish-level"],
-                         pinned={"terminal_depth": 2,
-                                 "source": "PaxosTest.java:1214-1228 (singleton reaches CLIENTS_DONE at 2 steps per "
-                                           "command; its 3-command workload at depth 6)"}),
+                         pinned={}),
     "mp_2s1c_prune": dict(args=MP + ["--servers", "2", "--clients", "1", "--workload", "append-x"] + INV3 +
                           ["--prune", "CLIENTS_DONE", "--max-depth", "11"], pinned={}),
     "mp_xz_d8": dict(args=MP + ["--workload", "append-xz"] + INV3 + ["--max-depth", "8"], pinned={}),

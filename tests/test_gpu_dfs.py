@@ -78,3 +78,28 @@ def test_dfs_without_terminal_runs_out_of_budget():
         e.close()
     assert r.endCondition() == EndCondition.TIME_EXHAUSTED
     assert r.states >= 20000  # every probe counts its initial state, plus each successor
+
+
+@pytest.mark.parametrize("name,fixture,max_trace", [
+    ("lab0_mutant_nocheck", LAB0, 5),
+    ("synth_counter_violation", SYN, None),
+])
+def test_dfs_unbounded_depth_small_trace_capacity(name, fixture, max_trace):
+    """No maxDepth: probes run until they reach max_trace events and are then restarted before
+    stepping, so a reported terminal is always within the recorded trace; the trace replays on
+    the oracle to a state with the reported predicate value (depth = trace length)."""
+    case = fixture[name]
+    cap = max_trace or case["terminal_depth"] + 2
+    proto = argmap.protocol(case["args"])
+    s = argmap.settings(case["args"], proto)
+    s.maxTimeSecs(60)
+    e = Engine(proto)
+    try:
+        r = e.dfs(proto.initial_state(), s, probes=16384, seed=11, max_trace=cap, minimize=False)
+    finally:
+        e.close()
+    assert r.endCondition() == EndCondition.INVARIANT_VIOLATED, r.endCondition()
+    st = r.invariantViolatingState()
+    assert case["terminal_depth"] <= st.depth() <= cap
+    assert len(st.trace()) == st.depth()
+    _replay_ok(case["args"], st, EndCondition.INVARIANT_VIOLATED)

@@ -50,3 +50,30 @@ def test_queue_modes_match_golden(fname, name, mode, monkeypatch):
                 assert rep["depth"] == st.depth()
     finally:
         e.close()
+
+
+@pytest.mark.parametrize("secs", [0.005, 0.02])
+def test_time_limit_ends_queued_search(secs):
+    """SearchSettings.maxTimeSecs (Search.java:313-318): an unbounded C5 search ends
+    TIME_EXHAUSTED soon after the limit, also when queued levels are running (a queue holds no
+    more levels than the remaining time covers at the last queue's time per level); the levels it
+    completed match the golden vector."""
+    case = _gold("multipaxos", "mp_c5_d12")
+    args = [a for a in case["args"]]
+    k = args.index("--max-depth")
+    del args[k:k + 2]
+    proto = argmap.protocol(args)
+    s = argmap.settings(args, proto, table_log2=27)
+    s.maxTimeSecs(secs)
+    e = Engine(proto)
+    try:
+        for run in range(2):  # the first run also allocates the table; the second has a queue time
+            r = e.bfs(proto.initial_state(), s)
+            assert r.endCondition().name == "TIME_EXHAUSTED"
+            assert r.elapsed_s < secs + 0.25
+            n = min(len(r.per_depth), len(case["per_depth"]))
+            assert r.per_depth[:n] == case["per_depth"][:n]
+            if run:
+                assert n >= 6, r.per_depth
+    finally:
+        e.close()
