@@ -38,7 +38,7 @@ WORKLOADS = {
     # proposers, 3 acceptors, invariants Integrity + Agreement, exhaustive to maxDepth.
     # BASELINE config C3: the table-driven synthetic protocol, 5 nodes, 64-byte
     # packed state, ~20-25 successors per state, maxDepth 10 (~8e8 unique states).
-    "synthetic": dict(depth=10, cpu_depth=6, table_log2=31,
+    "synthetic": dict(depth=10, cpu_depth=6, cpu_mt_depth=8, table_log2=31,
                       desc="table-driven synthetic protocol (5 nodes, K=64, pokes at v%7==0, seed 0x5EEDD51AB5), "
                            "invariant NOT_ALL_MAX, BFS to maxDepth"),
     # BASELINE config C2: lab1 AMO KV, ClientServerPart2Test.test10 workload
@@ -105,17 +105,34 @@ def build_search(name: str, depth: int):
     raise SystemExit(f"unknown workload {name}")
 
 
-def cpu_baseline(oracle_args, depth: int) -> dict:
-    """The CPU oracle (a scalar C++ restatement of the reference BFS, oracle/) on the GPU box's
-    host, one thread, on a bounded sample of the same workload (smaller maxDepth)."""
-    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    exe = os.path.join(ROOT, "oracle", "_build", "dslabs_oracle")
-    out = subprocess.run([exe, "bfs"] + oracle_args + ["--max-depth", str(depth)], check=True,
-                         capture_output=True, text=True, timeout=300)
-    r = json.loads(out.stdout)
-    return {"value": r["states"] / r["elapsed_s"], "unit": "states/s", "cores": 1, "kind": "port",
-            "sample": f"same workload, maxDepth {depth} ({r['states']} states, {r['elapsed_s']:.2f} s, "
-                      f"oracle/dslabs_oracle single-threaded)"}
+def cpu_baseline(proto, settings, depth: int, gpu_per_depth, oracle_args, oracle_depth: int) -> dict:
+    """SURVEY.md §8(d)'s CPU baseline: the multithreaded level-synchronous BFS of
+    tools/cpu_bfs.cpp (the reference's BFS worker scheme, Search.java:241-348, over the same packed
+    transition functions, a lock-free visited set and a barrier per level) on this host's cores,
+    on the SAME workload and maxDepth as the GPU line; run twice, the second run reported (the
+    first grows its buffers, as the GPU's warmup step does). `oracle_sample` is the scalar
+    string-keyed oracle (oracle/, the reference's object model restated) on a smaller maxDepth: a
+    reference-semantics sample, not the baseline."""
+    sys.path.insert(0, ROOT)
+    from tools import cpu_baseline as cb
+    s = settings.clone()
+    s.maxDepth(depth)
+    r = cb.run(proto, s, repeat=2)
+    out = {"value": round(r["states_per_s"], 1), "unit": "states/s", "cores": r["threads"],
+           "kind": "cpu_ref multithreaded",
+           "sample": f"same workload, maxDepth {depth} ({r['states']} states, {r['elapsed_s']:.3f} s, "
+                     f"{r['threads']} threads, tools/cpu_bfs.cpp)",
+           "per_depth_equal_gpu": r["per_depth"] == gpu_per_depth[:len(r["per_depth"])]}
+    if oracle_depth > 0:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+        exe = os.path.join(ROOT, "oracle", "_build", "dslabs_oracle")
+        o = subprocess.run([exe, "bfs"] + oracle_args + ["--max-depth", str(oracle_depth)], check=True,
+                           capture_output=True, text=True, timeout=300)
+        ro = json.loads(o.stdout)
+        out["oracle_sample"] = {"value": round(ro["states"] / ro["elapsed_s"], 1), "cores": 1,
+                                "sample": f"oracle/dslabs_oracle (scalar, string-keyed object model), maxDepth "
+                                          f"{oracle_depth}, {ro['states']} states, {ro['elapsed_s']:.2f} s"}
+    return out
 
 
 def pmc_traffic(workload: str, depth: int, launches: int, staged_bytes: int = 0):
@@ -244,7 +261,8 @@ def main():
             "roofline": roofline(stats, args.workload, depth),
         }
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(oracle_args, wl["cpu_depth"])
+            line["cpu_baseline"] = cpu_baseline(proto, settings, min(depth, wl.get("cpu_mt_depth", depth)) if depth >= 0
+                                                else depth, res.per_depth, oracle_args, wl["cpu_depth"])
         print(json.dumps(line), flush=True)
     eng.close()
     if dist is not None:

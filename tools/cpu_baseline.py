@@ -1,0 +1,70 @@
+"""Driver of the multithreaded CPU baseline (tools/cpu_bfs.cpp): builds it, writes the search as
+a (dsl_protocol_desc, dsl_settings) blob through the same encoding the engine receives, and runs
+it on the host's cores. Used by bench.py's cpu_baseline leg and tests/test_cpu_bfs.py only."""
+from __future__ import annotations
+
+import ctypes
+import json
+import os
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tools", "cpu_bfs.cpp")
+EXE = os.path.join(ROOT, "tools", "_build", "cpu_bfs")
+DEPS = [SRC, os.path.join(ROOT, "dslabs_amd", "csrc"), os.path.join(ROOT, "include")]
+
+
+def _newest() -> float:
+    t = 0.0
+    for d in DEPS:
+        if os.path.isfile(d):
+            t = max(t, os.path.getmtime(d))
+            continue
+        for dp, _, fs in os.walk(d):
+            for f in fs:
+                t = max(t, os.path.getmtime(os.path.join(dp, f)))
+    return t
+
+
+def build(force: bool = False) -> str:
+    if not force and os.path.exists(EXE) and os.path.getmtime(EXE) >= _newest():
+        return EXE
+    if not os.path.exists(SRC):  # a tree shipped without sources: use the prebuilt binary
+        return EXE
+    os.makedirs(os.path.dirname(EXE), exist_ok=True)
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    subprocess.run([hipcc, "-O3", "-std=c++17", "-pthread", "-Wno-unused-result", "-o", EXE + ".tmp", SRC],
+                   check=True, cwd=ROOT)
+    os.replace(EXE + ".tmp", EXE)
+    return EXE
+
+
+def default_threads() -> int:
+    """The host cores this process may use, at most 16 (a GPU box's CPU share per GPU)."""
+    if os.environ.get("DSL_CPU_THREADS"):
+        return max(1, int(os.environ["DSL_CPU_THREADS"]))
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def run(proto, settings, threads: int | None = None, table_log2: int | None = None, repeat: int = 1,
+        timeout: float = 600) -> dict:
+    exe = build()
+    state = proto.initial_state()
+    blob = bytes(proto.desc()) + bytes(settings._encode(state))
+    assert len(blob) == ctypes.sizeof(type(proto.desc())) + ctypes.sizeof(type(settings._encode(state)))
+    threads = threads or default_threads()
+    log2 = table_log2 or settings.table_log2_slots
+    with tempfile.NamedTemporaryFile("wb", suffix=".blob", delete=False) as f:
+        f.write(blob)
+        path = f.name
+    try:
+        out = subprocess.run([exe, path, str(threads), str(log2), str(repeat)], check=True, capture_output=True, text=True,
+                             timeout=timeout)
+    finally:
+        os.unlink(path)
+    return json.loads(out.stdout)
