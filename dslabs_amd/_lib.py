@@ -30,7 +30,8 @@ STATUS_NAMES = {
 
 # Exported symbols declared in include/dslabs_hip.h (checked by tests/test_capi.py).
 EXPORTED = [
-    "dsl_abi_version", "dsl_device_count", "dsl_state_bytes", "dsl_comm_unique_id", "dsl_create",
+    "dsl_abi_version", "dsl_device_count", "dsl_state_bytes", "dsl_init_state", "dsl_drop_pending_messages",
+    "dsl_undrop_messages", "dsl_comm_unique_id", "dsl_create",
     "dsl_set_settings", "dsl_set_initial", "dsl_get_initial", "dsl_run", "dsl_progress",
     "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
     "dsl_run_dfs", "dsl_replay", "dsl_human_readable_trace",
@@ -123,6 +124,11 @@ def load() -> ctypes.CDLL:
     lib.dsl_abi_version.restype = ctypes.c_int
     lib.dsl_device_count.restype = ctypes.c_int
     lib.dsl_state_bytes.argtypes = [P(dsl_protocol_desc)]
+    lib.dsl_init_state.argtypes = [P(dsl_protocol_desc), P(ctypes.c_uint8), ctypes.c_size_t]
+    lib.dsl_drop_pending_messages.argtypes = [P(dsl_protocol_desc), P(ctypes.c_uint8), ctypes.c_size_t,
+                                              P(ctypes.c_uint64), ctypes.c_int32, P(ctypes.c_int32)]
+    lib.dsl_undrop_messages.argtypes = [P(dsl_protocol_desc), P(ctypes.c_uint8), ctypes.c_size_t,
+                                        P(ctypes.c_uint64), ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]
     lib.dsl_comm_unique_id.argtypes = [P(ctypes.c_uint8)]
     lib.dsl_create.argtypes = [P(dsl_protocol_desc), P(dsl_engine_config), P(ctypes.c_void_p)]
     lib.dsl_set_settings.argtypes = [ctypes.c_void_p, P(dsl_settings)]

@@ -1,6 +1,7 @@
 // engine.hip -- libdslabs_hip.so: C ABI (include/dslabs_hip.h) over the templated engine.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <functional>
 #include <string>
 
@@ -210,6 +211,56 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
   }
 }
 
+// dsl_drop_pending_messages / dsl_undrop_messages over one protocol's packed network.
+template <class P>
+static int drop_pending(uint8_t* packed, size_t len, uint64_t* dropped, int32_t cap, int32_t* n) {
+  using S = typename P::State;
+  if (len != sizeof(S) || *n < 0 || *n > cap) return DSL_ERR_ARG;
+  S st;
+  std::memcpy(&st, packed, sizeof(S));
+  std::vector<uint64_t> d(dropped, dropped + *n);
+  for (int i = 0; i < Net<P>::size(st.w); i++) d.push_back((uint64_t)Net<P>::at(st.w, i));
+  std::sort(d.begin(), d.end());
+  d.erase(std::unique(d.begin(), d.end()), d.end());
+  if ((int64_t)d.size() > cap) return DSL_ERR_ARG;
+  for (int i = 0; i < Net<P>::size(st.w); i++) Net<P>::put(st.w, i, 0);
+  st.w[Layout<P>::kNetCount] = 0;
+  std::memcpy(packed, &st, sizeof(S));
+  std::copy(d.begin(), d.end(), dropped);
+  *n = (int32_t)d.size();
+  return DSL_OK;
+}
+template <class P>
+static int init_packed(const dsl_protocol_desc& d, uint8_t* packed, size_t len) {
+  using S = typename P::State;
+  const typename P::Params prm = P::from_desc(d);
+  if (len != sizeof(S) || !P::valid(prm)) return DSL_ERR_ARG;
+  S st;
+  if (!init_state<P>(st.w, prm)) {
+    set_error("initial state exceeds the protocol's network capacity");
+    return DSL_ERR_STATE_OVERFLOW;
+  }
+  std::memcpy(packed, &st, sizeof(S));
+  return DSL_OK;
+}
+template <class P>
+static int undrop(uint8_t* packed, size_t len, const uint64_t* dropped, int32_t n, int32_t from, int32_t to) {
+  using S = typename P::State;
+  if (len != sizeof(S) || n < 0) return DSL_ERR_ARG;
+  S st;
+  std::memcpy(&st, packed, sizeof(S));
+  for (int i = 0; i < n; i++) {
+    const auto r = (typename P::Rec)dropped[i];
+    if ((from >= 0 && P::rec_from(r) != from) || (to >= 0 && P::rec_to(r) != to)) continue;
+    if (Net<P>::insert(st.w, r) < 0) {
+      set_error("undropped network exceeds the protocol's network capacity");
+      return DSL_ERR_STATE_OVERFLOW;
+    }
+  }
+  std::memcpy(packed, &st, sizeof(S));
+  return DSL_OK;
+}
+
 }  // namespace dsl
 
 struct dsl_engine {
@@ -240,6 +291,35 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_MINITEST: return (int)sizeof(dsl::MiniTest::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
+}
+
+#define DSL_PROTO_DISPATCH(call)                                        \
+  switch (proto->protocol) {                                            \
+    case DSL_PROTO_PINGPONG: { using P = dsl::PingPong; return call; }     \
+    case DSL_PROTO_SIPAXOS: { using P = dsl::SIPaxos; return call; }       \
+    case DSL_PROTO_MULTIPAXOS: { using P = dsl::MultiPaxos; return call; } \
+    case DSL_PROTO_SYNTHETIC: { using P = dsl::Synthetic; return call; }   \
+    case DSL_PROTO_AMOKV: { using P = dsl::AmoKV; return call; }           \
+    case DSL_PROTO_PB: { using P = dsl::PB; return call; }                 \
+    case DSL_PROTO_MINITEST: { using P = dsl::MiniTest; return call; }     \
+    default: return DSL_ERR_UNKNOWN_PROTOCOL;                           \
+  }
+
+int dsl_init_state(const dsl_protocol_desc* proto, uint8_t* packed, size_t len) {
+  if (!proto || !packed) return DSL_ERR_ARG;
+  DSL_PROTO_DISPATCH((dsl::init_packed<P>(*proto, packed, len)))
+}
+
+int dsl_drop_pending_messages(const dsl_protocol_desc* proto, uint8_t* packed, size_t len, uint64_t* dropped,
+                              int32_t cap, int32_t* n_dropped) {
+  if (!proto || !packed || !n_dropped || (cap > 0 && !dropped)) return DSL_ERR_ARG;
+  DSL_PROTO_DISPATCH((dsl::drop_pending<P>(packed, len, dropped, cap, n_dropped)))
+}
+
+int dsl_undrop_messages(const dsl_protocol_desc* proto, uint8_t* packed, size_t len, const uint64_t* dropped,
+                        int32_t n_dropped, int32_t from, int32_t to) {
+  if (!proto || !packed || (n_dropped > 0 && !dropped)) return DSL_ERR_ARG;
+  DSL_PROTO_DISPATCH((dsl::undrop<P>(packed, len, dropped, n_dropped, from, to)))
 }
 
 int dsl_comm_unique_id(uint8_t out[128]) {

@@ -294,13 +294,68 @@ class SearchState:
     (``trace()``), the analogue of the reference's ``previous`` chain.
     """
 
+    DROPPED_CAP = 4096
+
     def __init__(self, protocol, packed: Optional[bytes] = None, depth: int = 0,
-                 events: Optional[List[str]] = None, raw_events=None):
+                 events: Optional[List[str]] = None, raw_events=None, dropped=None):
         self.protocol = protocol
         self.packed = packed
         self._depth = depth
         self._events = events or []
         self._raw_events = raw_events or []
+        # SearchState.droppedNetwork (SearchState.java:77): records set aside by
+        # dropPendingMessages; successors found by a search from this state inherit the set
+        self._dropped = list(dropped or [])
+
+    # ---- dropped network (SearchState.java:538-561) ----------------------------------------------
+    def _packed_now(self) -> bytes:
+        if self.packed is not None:
+            return self.packed
+        lib = _lib.load()
+        desc = self.protocol.desc()
+        n = lib.dsl_state_bytes(ctypes.byref(desc))
+        check(n if n < 0 else 0, "dsl_state_bytes")
+        buf = (ctypes.c_uint8 * n)()
+        check(lib.dsl_init_state(ctypes.byref(desc), buf, n), "dsl_init_state")
+        return bytes(buf)
+
+    def dropPendingMessages(self) -> None:
+        """Every pending message moves to the dropped set: no longer an event, still part of the
+        state's message union (SearchState.dropPendingMessages, :538-541). Mutates this state."""
+        lib = _lib.load()
+        packed = self._packed_now()
+        buf = (ctypes.c_uint8 * len(packed)).from_buffer_copy(packed)
+        arr = (ctypes.c_uint64 * self.DROPPED_CAP)(*self._dropped)
+        n = ctypes.c_int32(len(self._dropped))
+        check(lib.dsl_drop_pending_messages(ctypes.byref(self.protocol.desc()), buf, len(packed), arr,
+                                            self.DROPPED_CAP, ctypes.byref(n)), "dsl_drop_pending_messages")
+        self.packed = bytes(buf)
+        self._dropped = list(arr[:n.value])
+
+    def _undrop(self, frm: int, to: int) -> None:
+        lib = _lib.load()
+        packed = self._packed_now()
+        buf = (ctypes.c_uint8 * len(packed)).from_buffer_copy(packed)
+        arr = (ctypes.c_uint64 * max(1, len(self._dropped)))(*self._dropped)
+        check(lib.dsl_undrop_messages(ctypes.byref(self.protocol.desc()), buf, len(packed), arr,
+                                      len(self._dropped), frm, to), "dsl_undrop_messages")
+        self.packed = bytes(buf)
+
+    def undropMessages(self) -> None:
+        """SearchState.undropMessages (:543-545): every dropped message is pending again."""
+        self._undrop(-1, -1)
+
+    def undropMessagesFrom(self, address: str) -> None:
+        """SearchState.undropMessagesFrom (:547-553)."""
+        self._undrop(self.protocol.address_index(address), -1)
+
+    def undropMessagesTo(self, address: str) -> None:
+        """SearchState.undropMessagesTo (:555-561)."""
+        self._undrop(-1, self.protocol.address_index(address))
+
+    def droppedMessages(self) -> List[int]:
+        """The dropped set as packed records (sorted)."""
+        return list(self._dropped)
 
     def depth(self) -> int:
         return self._depth
@@ -477,7 +532,7 @@ class Engine:
             raw = [r.trace[i] for i in range(r.trace_len)]
             packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
             return SearchState(self.protocol, packed, r.terminal_depth, [self.protocol.render_event(e) for e in raw],
-                               [_lib.dsl_event.from_buffer_copy(e) for e in raw])
+                               [_lib.dsl_event.from_buffer_copy(e) for e in raw], state._dropped)
         finally:
             self.lib.dsl_result_free(res_p)
 
@@ -495,7 +550,7 @@ class Engine:
                 packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
                 base_events = state.trace() if state.packed is not None else []
                 terminal = SearchState(self.protocol, packed, r.terminal_depth, base_events + events,
-                                       [_lib.dsl_event.from_buffer_copy(e) for e in raw])
+                                       [_lib.dsl_event.from_buffer_copy(e) for e in raw], state._dropped)
                 if end == EndCondition.INVARIANT_VIOLATED:
                     pred = PredicateResult(settings.invariants()[r.predicate_index], False)
                 elif end == EndCondition.GOAL_FOUND:

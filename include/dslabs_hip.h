@@ -189,6 +189,23 @@ typedef struct dsl_engine dsl_engine;
 int dsl_abi_version(void);
 int dsl_device_count(void);
 int dsl_state_bytes(const dsl_protocol_desc* proto);
+/* The protocol's initial packed state (every node added and init()-ed, SearchState.addServer /
+ * addClientWorker order), computed on the host: no engine or device needed. */
+int dsl_init_state(const dsl_protocol_desc* proto, uint8_t* packed, size_t len);
+/* SearchState.dropPendingMessages (T/search/SearchState.java:538-541) on a packed state: every
+ * message of its network moves into the caller's dropped set (`dropped`: one record per uint64,
+ * kept sorted and duplicate-free; *n_dropped is read and updated; DSL_ERR_ARG past `cap`). Events
+ * only come from the remaining (undropped) network. The dropped set never changes during a search
+ * that starts from such a state, so search-equivalence (SearchEquivalenceWrappedSearchState,
+ * :575-619: equal union of both sets and equal undropped sets) is equality of the packed states
+ * and the engine needs nothing more: the caller keeps the set with the state and its successors. */
+int dsl_drop_pending_messages(const dsl_protocol_desc* proto, uint8_t* packed, size_t len, uint64_t* dropped,
+                              int32_t cap, int32_t* n_dropped);
+/* undropMessages / undropMessagesFrom / undropMessagesTo (:543-561): the dropped messages sent by
+ * address index `from` and addressed to `to` (-1 = any) are added back to the packed state's
+ * network; the dropped set itself is unchanged, as in the reference. */
+int dsl_undrop_messages(const dsl_protocol_desc* proto, uint8_t* packed, size_t len, const uint64_t* dropped,
+                        int32_t n_dropped, int32_t from, int32_t to);
 int dsl_comm_unique_id(uint8_t out[128]);
 int dsl_create(const dsl_protocol_desc* proto, const dsl_engine_config* cfg, dsl_engine** out);
 int dsl_set_settings(dsl_engine* e, const dsl_settings* s);

@@ -257,15 +257,39 @@ static void printTerminal(const Terminal& t, const Names& names, bool printState
 }
 
 // --start-trace FILE: replay the events (one per line, unfiltered) from the initial state and
-// start the search there (bfs(goalStateOfAnEarlierSearch), e.g. PaxosTest.java:898-910).
+// start the search there (bfs(goalStateOfAnEarlierSearch), e.g. PaxosTest.java:898-910); lines
+// starting with '#' apply dropPendingMessages / undropMessages* to the state reached so far
+// (PaxosTest.java:1065, :1092, :1132).
 static std::shared_ptr<const State> replayStart(const Args& a, Scenario& sc) {
   std::shared_ptr<const State> s = sc.init;
   if (!a.has("start-trace")) return s;
   Settings all;  // events are matched without delivery filters
   std::ifstream in(a.get("start-trace"));
   std::string line;
+  auto addrOf = [&](const std::string& n) {
+    for (size_t i = 0; i < sc.names.addr.size(); i++)
+      if (sc.names.addr[i] == n) return (int)i;
+    throw std::runtime_error("unknown address " + n);
+  };
   while (std::getline(in, line)) {
     if (line.empty()) continue;
+    // state operations between searches (SearchState.java:538-561): "#DROP" = dropPendingMessages,
+    // "#UNDROP" / "#UNDROP_FROM a" / "#UNDROP_TO a" = undropMessages / ...From / ...To
+    if (line[0] == '#') {
+      auto ns = std::make_shared<State>(*s);
+      if (line == "#DROP") {
+        ns->dropped.insert(ns->network.begin(), ns->network.end());
+        ns->network.clear();
+      } else {
+        const bool from = line.rfind("#UNDROP_FROM ", 0) == 0, to = line.rfind("#UNDROP_TO ", 0) == 0;
+        if (!from && !to && line != "#UNDROP") throw std::runtime_error("unknown start-trace directive " + line);
+        const int x = (from || to) ? addrOf(line.substr(line.find(' ') + 1)) : -1;
+        for (auto& m : ns->dropped)
+          if ((!from || m.from == x) && (!to || m.to == x)) ns->network.insert(m);
+      }
+      s = ns;
+      continue;
+    }
     bool found = false;
     for (auto& ev : events(*s, all))
       if (eventStr(ev, sc.names) == line) {
@@ -417,8 +441,30 @@ static int runReplay(const Args& a) {
   int step = 0;
   bool ok = true;
   std::string err;
+  auto addrOf = [&](const std::string& n) {
+    for (size_t i = 0; i < sc.names.addr.size(); i++)
+      if (sc.names.addr[i] == n) return (int)i;
+    throw std::runtime_error("unknown address " + n);
+  };
   while (std::getline(in, line)) {
     if (line.empty()) continue;
+    // state operations between searches (SearchState.java:538-561): "#DROP" = dropPendingMessages,
+    // "#UNDROP" / "#UNDROP_FROM a" / "#UNDROP_TO a" = undropMessages / ...From / ...To
+    if (line[0] == '#') {
+      auto ns = std::make_shared<State>(*s);
+      if (line == "#DROP") {
+        ns->dropped.insert(ns->network.begin(), ns->network.end());
+        ns->network.clear();
+      } else {
+        const bool from = line.rfind("#UNDROP_FROM ", 0) == 0, to = line.rfind("#UNDROP_TO ", 0) == 0;
+        if (!from && !to && line != "#UNDROP") throw std::runtime_error("unknown start-trace directive " + line);
+        const int x = (from || to) ? addrOf(line.substr(line.find(' ') + 1)) : -1;
+        for (auto& m : ns->dropped)
+          if ((!from || m.from == x) && (!to || m.to == x)) ns->network.insert(m);
+      }
+      s = ns;
+      continue;
+    }
     bool found = false;
     for (auto& ev : events(*s, st)) {
       if (eventStr(ev, sc.names) == line) {

@@ -76,3 +76,25 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
         assert ctypes.sizeof(cls) == int(got[st]), st
         for f in fields:
             assert getattr(cls, f).offset == int(got[f"{st}.{f}"]), (st, f)
+
+
+def test_drop_and_undrop_pending_messages_without_device(lib):
+    """SearchState.dropPendingMessages / undropMessages* (SearchState.java:538-561) on packed
+    states (host functions of the library): dropping empties the network into the dropped set,
+    undropping everything restores the state exactly, undropMessagesFrom restores a subset."""
+    from dslabs_amd.protocols import MultiPaxos, PingPong
+    for proto in (PingPong(2, 3), MultiPaxos(3, 2, "append-xy")):
+        st = proto.initial_state()
+        init = st._packed_now()
+        st.dropPendingMessages()
+        assert st.droppedMessages() == sorted(set(st.droppedMessages()))
+        st.undropMessages()
+        assert st.packed == init  # sends of init() are the whole network; all come back
+        st.dropPendingMessages()
+        n_all = len(st.droppedMessages())
+        st.undropMessagesFrom(proto.addresses[0])
+        st2 = proto.initial_state()
+        st2.dropPendingMessages()
+        assert len(st2.droppedMessages()) == n_all
+        st2.dropPendingMessages()  # dropping twice keeps the set
+        assert len(st2.droppedMessages()) == n_all

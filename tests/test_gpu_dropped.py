@@ -1,0 +1,72 @@
+"""Searches from states with dropped messages (SearchState.dropPendingMessages / undropMessagesFrom,
+SearchState.java:538-561; search-equivalence over the undropped network, :575-619), as PaxosTest's
+test23 / test24 narrow their searches (PaxosTest.java:1065, :1092, :1132). Each phase starts from
+the GPU's own terminal state; the oracle rebuilds the same start state from the trace with the
+drop / undrop operations in between ('#' lines of --start-trace) and must give the same per-depth
+counts and end condition; the GPU's terminal trace replays on the oracle."""
+import os
+import tempfile
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import EndCondition, Search
+
+pytestmark = pytest.mark.gpu
+
+MP = ["--proto", "multipaxos", "--workload", "append-xy-expect"]
+PHASE1 = MP + ["--inv", "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "!NONE_DECIDED", "--partition",
+               "server1,server2,client1"]
+PHASE2 = MP + ["--inv", "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS", "--goal", "CLIENTS_DONE"]
+PHASE3 = MP + ["--inv", "RESULTS_OK", "--inv", "LOGS_CONSISTENT_ALL_SLOTS"]
+
+
+def _oracle(args, start_lines):
+    with tempfile.NamedTemporaryFile("w", suffix=".trace", delete=False) as f:
+        f.write("\n".join(start_lines) + "\n")
+    try:
+        return oracle_util.run("bfs", args + ["--start-trace", f.name, "--finish-level"], timeout=300), f.name
+    except Exception:
+        os.unlink(f.name)
+        raise
+
+
+def _check(r, args, start, start_lines):
+    want, path = _oracle(args, start_lines)
+    try:
+        assert r.endCondition().name == want["end"]
+        assert r.per_depth == want["per_depth"][start.depth():]
+        st = r.invariantViolatingState() or r.goalMatchingState()
+        if st is not None:
+            rep = oracle_util.replay(args + ["--start-trace", path], st.trace()[start.depth():])
+            assert rep["ok"], rep
+            assert rep["depth"] == st.depth()
+        return st
+    finally:
+        os.unlink(path)
+
+
+@pytest.mark.parametrize("undrop", ["#UNDROP_FROM server2", "#UNDROP_TO server1", "#UNDROP"])
+def test_dropped_network_phases(undrop):
+    proto = argmap.protocol(PHASE1)
+    r1 = Search.bfs(proto.initial_state(), argmap.settings(PHASE1, proto))
+    assert r1.endCondition() == EndCondition.GOAL_FOUND
+    s1 = r1.goalMatchingState()
+    s1.dropPendingMessages()
+    assert s1.droppedMessages()
+    lines1 = s1.trace() + ["#DROP"]
+    r2 = Search.bfs(s1, argmap.settings(PHASE2, proto))
+    s2 = _check(r2, PHASE2, s1, lines1)
+    assert s2 is not None and s2.droppedMessages() == s1.droppedMessages()  # successors inherit the set
+    op, _, who = undrop.partition(" ")
+    if op == "#UNDROP_FROM":
+        s2.undropMessagesFrom(who)
+    elif op == "#UNDROP_TO":
+        s2.undropMessagesTo(who)
+    else:
+        s2.undropMessages()
+    lines2 = lines1 + s2.trace()[s1.depth():] + [undrop]
+    args3 = PHASE3 + ["--max-depth", str(s2.depth() + 5)]
+    r3 = Search.bfs(s2, argmap.settings(args3, proto))
+    _check(r3, args3, s2, lines2)

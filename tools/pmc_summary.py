@@ -63,6 +63,21 @@ def main(d):
         # and half of the 16-B/lane streaming staging reads; WRITE_SIZE is exact)
         out["fetch_bytes_per_step"] = fetch
         out["write_bytes_per_step"] = write
+        # visited-set atomics (north_star: atomic throughput of the probe/insert): every atomic
+        # request at the L2 per search, over the search's k_level time (launches in one search x
+        # the traced average launch)
+        if "TCC_ATOMIC_sum" in tot:
+            out["atomics_per_step"] = tot["TCC_ATOMIC_sum"]
+            out["atomics_to_dram_per_step"] = tot.get("TCC_EA0_WRREQ_ATOMIC_DRAM_sum")
+            if out.get("avg_launch_ms"):
+                out["atomics_per_s"] = tot["TCC_ATOMIC_sum"] / (out["avg_launch_ms"] * n / 1e3)
+        if tot.get("TCC_EA0_RDREQ_sum"):
+            # memory-side reads that went to DRAM (the rest were served by the Infinity Cache)
+            out["dram_read_frac"] = tot.get("TCC_EA0_RDREQ_DRAM_sum", 0) / tot["TCC_EA0_RDREQ_sum"]
+            if tot.get("TCC_EA0_WRREQ_sum"):
+                out["dram_write_frac"] = tot.get("TCC_EA0_WRREQ_DRAM_sum", 0) / tot["TCC_EA0_WRREQ_sum"]
+        if tot.get("TCC_HIT_sum") is not None and tot.get("TCC_MISS_sum") is not None:
+            out["l2_hit_rate"] = tot["TCC_HIT_sum"] / max(1.0, tot["TCC_HIT_sum"] + tot["TCC_MISS_sum"])
         if "SQ_WAVE_CYCLES" in tot and tot.get("SQ_WAVE_CYCLES"):
             out["wait_frac"] = tot.get("SQ_WAIT_ANY", 0) / tot["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in tot else None
     json.dump(out, sys.stdout, indent=1)
