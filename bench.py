@@ -135,6 +135,12 @@ def cpu_baseline(proto, settings, depth: int, gpu_per_depth, oracle_args, oracle
     return out
 
 
+def pmc_profile(workload: str, depth: int):
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{workload}_d{depth}.json")))
+    return json.load(open(fs[-1])) if fs else None
+
+
 def pmc_traffic(workload: str, depth: int, launches: int, staged_bytes: int = 0):
     """HBM bytes per k_level launch from the committed rocprofv3 PMC summary of the same
     workload (tools/gpu_prof.sh + tools/pmc_summary.py, separate --pmc passes over one search),
@@ -177,6 +183,15 @@ def roofline(stats: dict, workload: str, depth: int) -> dict:
            "alg_bytes_per_launch": int(alg / launches)}
     if src:
         out["traffic_source"] = src
+    # visited-set atomics (north_star): one 64-bit CAS per inserted state (live, HIP events), the
+    # probes (bucket lookups) behind them, the table's size, and the PMC count of every atomic at
+    # the L2 (TCC_ATOMIC, the committed profile of the same workload) per search
+    out["atomics_per_s"] = round(stats["new_states"] / t, 1) if t > 0 else 0.0
+    out["probes_per_s"] = round(stats["probes"] / t, 1) if t > 0 else 0.0
+    out["table_bytes"] = int(stats["table_slots"] * 8)
+    prof = pmc_profile(workload, depth)
+    if prof and prof.get("atomics_per_step") is not None:
+        out["pmc_atomics_per_search"] = int(prof["atomics_per_step"])
     return out
 
 

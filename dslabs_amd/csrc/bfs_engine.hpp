@@ -7,9 +7,11 @@
 //     (RCCL: grouped ncclSend/ncclRecv = all-to-all over the xGMI links, allreduce, broadcast);
 //   * virtual shards: W shards on ONE device, exchanges are device-to-device copies (tests).
 // Multi-shard level: k_level<ROUTE> (local successors inserted in-kernel, remote ones as 24-byte
-// FpRecs) -> exchange #1 -> k_probe_remote at the owner -> NEW items back (#2) -> k_materialize
-// at the source (judge; terminal candidates stay with the parent's shard) -> VALID states to the
-// owner (#3) -> k_append_received. Only new states cross the links at full size.
+// FpRecs) -> round A: FpRecs to their owners -> k_probe_remote (one answer byte per record) ->
+// round B: the answers back, in the order received -> k_materialize at the source (judge, append
+// to the source's own next frontier). Only the visited set is partitioned: a new state stays
+// where it was generated, so no state crosses the links, and one count exchange serves both
+// rounds (round B's counts are round A's, reversed).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -83,7 +85,6 @@ struct EngineBase {
 template <class P>
 struct BfsEngine : EngineBase {
   static constexpr int NW = Layout<P>::kWords;
-  using SRec = StateRec<P>;
 
   struct Shard {
     int gid = 0;
@@ -109,14 +110,10 @@ struct BfsEngine : EngineBase {
     uint64_t out_fp_cap = 0;
     FpRec* in_fp = nullptr;
     uint64_t in_fp_cap = 0;
-    uint64_t* out_items = nullptr;
-    uint64_t out_items_cap = 0;
-    uint64_t* in_items = nullptr;
-    uint64_t in_items_cap = 0;
-    SRec* out_st = nullptr;
-    uint64_t out_st_cap = 0;
-    SRec* in_st = nullptr;
-    uint64_t in_st_cap = 0;
+    uint8_t* rep_out = nullptr;  // answers to the received FpRecs (owner side)
+    uint64_t rep_out_cap = 0;
+    uint8_t* rep_in = nullptr;   // answers to this shard's FpRecs, W regions of cap_fp (source side)
+    uint64_t rep_in_cap = 0;
     uint64_t* spill = nullptr;
     uint64_t spill_cap = 0;
     uint64_t F = 0;
@@ -132,8 +129,7 @@ struct BfsEngine : EngineBase {
     uint64_t segcap = 0;
     int nseg = 1;
     std::vector<uint64_t> level_size;  // rows of each level's frontier (history entries)
-    uint64_t cap_fp = 0, cap_v = 0, cap_s = 0;
-    uint64_t n_in_fp = 0, n_in_items = 0, n_in_st = 0;
+    uint64_t cap_fp = 0;
     LevelCounters lc{};
   };
 
@@ -213,7 +209,7 @@ struct BfsEngine : EngineBase {
   ~BfsEngine() override {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,     s.seed,
-                      s.out_fp,    s.in_fp,    s.out_items, s.in_items, s.out_st, s.in_st, s.spill, s.ctrbuf,
+                      s.out_fp,    s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
                       s.find_ctr};
       for (void* q : ptrs) (void)hipFree(q);
       for (auto* q : s.hpar) (void)hipFree(q);
@@ -305,56 +301,17 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
-  template <class T>
-  int exchange(T* Shard::*out, uint64_t Shard::*cap, T* Shard::*in, uint64_t Shard::*in_cap, uint64_t Shard::*n_in,
-               const std::vector<std::vector<uint64_t>>& cnt, std::vector<std::vector<uint64_t>>& src_off) {
+  // One all-to-all round: local shard l sends sb[l][d] bytes at send[l] + so[l][d] to shard d and
+  // receives rb[l][s] bytes from shard s at recv[l] + ro[l][s] (RCCL grouped send/recv across
+  // ranks; device-to-device copies between the virtual shards of one device).
+  using Mat = std::vector<std::vector<uint64_t>>;
+  int xfer(const std::vector<const uint8_t*>& send, const Mat& so, const Mat& sb, const std::vector<uint8_t*>& recv,
+           const Mat& ro, const Mat& rb) {
+    if (comm) return comm->alltoallv(send[0], so[0].data(), sb[0].data(), recv[0], ro[0].data(), rb[0].data(), stream);
     const int L = (int)sh.size();
-    std::vector<uint64_t> matrix((size_t)W * W, 0);  // [src][dst]
-    if (comm) {
-      DSL_TRY(comm->allgather_u64(cnt[0].data(), W, matrix.data(), stream));
-    } else {
-      for (int s = 0; s < L; s++)
-        for (int d = 0; d < W; d++) matrix[(size_t)s * W + d] = cnt[s][d];
-    }
-    src_off.assign(L, std::vector<uint64_t>(W + 1, 0));
-    for (int l = 0; l < L; l++) {
-      Shard& S = sh[l];
-      for (int s = 0; s < W; s++) src_off[l][s + 1] = src_off[l][s] + matrix[(size_t)s * W + S.gid];
-      S.*n_in = src_off[l][W];
-      DSL_TRY(grow(&(S.*in), &(S.*in_cap), std::max<uint64_t>(S.*n_in, 1), false, 0));
-    }
-    if (comm) {
-      Shard& S = sh[0];
-      std::vector<uint64_t> so(W), sb(W), ro(W), rb(W);
-      for (int d = 0; d < W; d++) {
-        so[d] = (uint64_t)d * (S.*cap) * sizeof(T);
-        sb[d] = cnt[0][d] * sizeof(T);
-        ro[d] = src_off[0][d] * sizeof(T);
-        rb[d] = matrix[(size_t)d * W + S.gid] * sizeof(T);
-      }
-      DSL_TRY(comm->alltoallv((const uint8_t*)(S.*out), so.data(), sb.data(), (uint8_t*)(S.*in), ro.data(), rb.data(),
-                              stream));
-    } else {
-      for (int s = 0; s < L; s++)
-        for (int d = 0; d < W; d++) {
-          const uint64_t n = cnt[s][d];
-          if (!n) continue;
-          DSL_HIP(hipMemcpyAsync((sh[d].*in) + src_off[d][s], (sh[s].*out) + (uint64_t)d * (sh[s].*cap),
-                                 n * sizeof(T), hipMemcpyDeviceToDevice, stream));
-        }
-    }
-    return DSL_OK;
-  }
-
-  int read_route_counts(std::vector<std::vector<uint64_t>>& cnt) {
-    const int L = (int)sh.size();
-    cnt.assign(L, std::vector<uint64_t>(W, 0));
-    std::vector<RouteCounters> rcs(L);
-    for (int l = 0; l < L; l++) DSL_HIP(hipMemcpyAsync(&rcs[l], sh[l].rc, sizeof(RouteCounters), hipMemcpyDeviceToHost, stream));
-    DSL_HIP(hipStreamSynchronize(stream));
-    for (int l = 0; l < L; l++)
-      for (int d = 0; d < W; d++) cnt[l][d] = rcs[l].out[d];
-    for (int l = 0; l < L; l++) DSL_HIP(hipMemsetAsync(sh[l].rc, 0, sizeof(RouteCounters), stream));
+    for (int s = 0; s < L; s++)
+      for (int d = 0; d < L; d++)
+        if (sb[s][d]) DSL_HIP(hipMemcpyAsync(recv[d] + ro[d][s], send[s] + so[s][d], sb[s][d], hipMemcpyDeviceToDevice, stream));
     return DSL_OK;
   }
 
@@ -365,7 +322,7 @@ struct BfsEngine : EngineBase {
   static constexpr uint64_t kLevelGrid = 256ull * 16;
   // Frontier size below which a multi-shard search runs the level replicated (see run()):
   // dsl_engine_config.replicate_below, -1 = default, 0 = never.
-  uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 19) : (uint64_t)cfg.replicate_below; }
+  uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 16) : (uint64_t)cfg.replicate_below; }
   int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / per);
@@ -584,7 +541,7 @@ struct BfsEngine : EngineBase {
       }
       DSL_HIP(hipMemsetAsync(S.table, 0, buckets * 64, stream));
       if (!S.ctrbuf) DSL_HIP(hipMalloc(&S.ctrbuf, 2 * kCtrSet));
-      if (!S.hctr) DSL_HIP(hipHostMalloc(&S.hctr, kCtrSet));
+      if (!S.hctr) DSL_HIP(hipHostMalloc(&S.hctr, kCtrSet + sizeof(RouteCounters)));
       DSL_HIP(hipMemsetAsync(S.ctrbuf, 0, 2 * kCtrSet, stream));
       S.cset = 0;
       S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf);
@@ -816,6 +773,7 @@ struct BfsEngine : EngineBase {
         }  // !queued (launch)
         // spilled VALID states: grow the next frontier and materialize them after the local rows
         std::vector<std::vector<unsigned long long>> segc(L, std::vector<unsigned long long>(kSegs * kSegStride));
+        Mat rcnt(L, std::vector<uint64_t>(W, 0));  // routed records per destination shard
         if (queued) {  // this level's counters came back with the queue
           const unsigned char* set = hq + (size_t)q_pos * kCtrSet;
           std::memcpy(&sh[0].lc, set, sizeof(LevelCounters));
@@ -825,12 +783,21 @@ struct BfsEngine : EngineBase {
           Shard& S = sh[l];
           DSL_HIP(hipMemcpyAsync(S.hctr, S.ctrbuf + S.cset * kCtrSet, kCtrSegOff + 8 * S.nseg * kSegStride,
                                  hipMemcpyDeviceToHost, stream));
+          if (route) {  // the level's route counts come with the same synchronization
+            DSL_HIP(hipMemcpyAsync(S.hctr + kCtrSet, S.rc, sizeof(RouteCounters), hipMemcpyDeviceToHost, stream));
+            DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
+          }
         }
         DSL_HIP(hipStreamSynchronize(stream));
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
           std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
           std::memcpy(segc[l].data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
+          if (route) {
+            RouteCounters rcs;
+            std::memcpy(&rcs, S.hctr + kCtrSet, sizeof(rcs));
+            rcnt[l].assign(rcs.out, rcs.out + W);
+          }
         }
         }
         // next frontier: the filled part of each segment, then the spill range (then received)
@@ -864,76 +831,105 @@ struct BfsEngine : EngineBase {
           span[l] = need;
         }
 
+        std::vector<uint64_t> mat_keep(L, 0), mat_total(L, 0);
+        const auto tx0 = std::chrono::steady_clock::now();
         if (route) {
-          std::vector<std::vector<uint64_t>> cnt, src_off;
-          DSL_TRY(read_route_counts(cnt));
+          stats.sharded_levels++;
+          Mat matrix(W, std::vector<uint64_t>(W, 0));  // [source][owner] records
+          if (comm) {
+            std::vector<uint64_t> flat((size_t)W * W);
+            DSL_TRY(comm->allgather_u64(rcnt[0].data(), W, flat.data(), stream));
+            for (int x = 0; x < W; x++)
+              for (int d = 0; d < W; d++) matrix[x][d] = flat[(size_t)x * W + d];
+          } else {
+            for (int l = 0; l < L; l++) matrix[sh[l].gid] = rcnt[l];
+          }
           for (int l = 0; l < L; l++)
-            for (int d = 0; d < W; d++) exchanged += cnt[l][d];
-          // fingerprints to owners; owners probe; NEW items back to their sources
-          DSL_TRY(exchange(&Shard::out_fp, &Shard::cap_fp, &Shard::in_fp, &Shard::in_fp_cap, &Shard::n_in_fp, cnt,
-                           src_off));
+            for (int d = 0; d < W; d++) exchanged += rcnt[l][d];
+          // round A: fingerprints to their owners
+          Mat so(L, std::vector<uint64_t>(W)), sb = so, ro = so, rb = so, src_off(L, std::vector<uint64_t>(W + 1, 0));
+          std::vector<const uint8_t*> snd(L);
+          std::vector<uint8_t*> rcv(L);
           for (int l = 0; l < L; l++) {
             Shard& S = sh[l];
-            S.cap_v = std::max<uint64_t>(S.n_in_fp, 1);
-            DSL_TRY(grow(&S.out_items, &S.out_items_cap, S.cap_v * W, false, 0));
-            if (!S.n_in_fp) continue;
+            const int g = S.gid;
+            for (int x = 0; x < W; x++) src_off[l][x + 1] = src_off[l][x] + matrix[x][g];
+            const uint64_t nin = src_off[l][W];
+            DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>(nin, 1), false, 0));
+            DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(nin, 1), false, 0));
+            for (int d = 0; d < W; d++) {
+              so[l][d] = (uint64_t)d * S.cap_fp * sizeof(FpRec);
+              sb[l][d] = rcnt[l][d] * sizeof(FpRec);
+              ro[l][d] = src_off[l][d] * sizeof(FpRec);
+              rb[l][d] = matrix[d][g] * sizeof(FpRec);
+            }
+            snd[l] = reinterpret_cast<const uint8_t*>(S.out_fp);
+            rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
+          }
+          DSL_TRY(xfer(snd, so, sb, rcv, ro, rb));
+          for (int l = 0; l < L; l++) {
+            Shard& S = sh[l];
+            const uint64_t nin = src_off[l][W];
+            if (!nin) continue;
             ProbeArgs pa;
             pa.in = S.in_fp;
-            pa.n = S.n_in_fp;
-            for (int s = 0; s <= W; s++) pa.src_off[s] = src_off[l][s];
-            pa.W = W;
+            pa.n = nin;
             pa.table = tbl_proto;
             pa.table.slots = S.table;
-            pa.out_items = S.out_items;
-            pa.cap_v = S.cap_v;
-            pa.rc = S.rc;
+            pa.reply = S.rep_out;
             pa.ctr = S.ctr;
-            const int blocks = (int)std::min<uint64_t>((S.n_in_fp + kBlock - 1) / kBlock, 256ull * 32);
+            const int blocks = (int)std::min<uint64_t>((nin + kBlock - 1) / kBlock, 256ull * 32);
             hipLaunchKernelGGL(k_probe_remote, dim3(blocks), dim3(kBlock), 0, stream, pa);
           }
-          DSL_TRY(read_route_counts(cnt));
-          DSL_TRY(exchange(&Shard::out_items, &Shard::cap_v, &Shard::in_items, &Shard::in_items_cap,
-                           &Shard::n_in_items, cnt, src_off));
+          // round B: one answer byte per record back to its source, in the order the source sent
           for (int l = 0; l < L; l++) {
             Shard& S = sh[l];
-            S.cap_s = std::max<uint64_t>(S.n_in_items, 1);
-            DSL_TRY(grow(&S.out_st, &S.out_st_cap, S.cap_s * W, false, 0));
-            if (!S.n_in_items) continue;
-            MaterializeArgs<P> ma;
-            ma.items = S.in_items;
-            ma.n = S.n_in_items;
-            ma.cur = S.cur;
-            ma.cur_fp = S.cur_fp;
-            ma.W = W;
-            ma.me = S.gid;
-            ma.depth = depth + 1;
-            ma.incremental = depth > init_depth ? 1 : 0;
-            ma.out = S.out_st;
-            ma.cap_s = S.cap_s;
-            ma.rc = S.rc;
-            ma.ctr = S.ctr;
-            ma.terms = S.terms;
-            ma.term_cap = term_cap;
-            const int blocks = (int)std::min<uint64_t>((S.n_in_items + kBlock - 1) / kBlock, 256ull * 32);
-            hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
+            const int g = S.gid;
+            DSL_TRY(grow(&S.rep_in, &S.rep_in_cap, std::max<uint64_t>(S.cap_fp * W, 1), false, 0));
+            for (int x = 0; x < W; x++) {
+              so[l][x] = src_off[l][x];
+              sb[l][x] = matrix[x][g];
+              ro[l][x] = (uint64_t)x * S.cap_fp;
+              rb[l][x] = rcnt[l][x];
+            }
+            snd[l] = S.rep_out;
+            rcv[l] = S.rep_in;
           }
-          DSL_TRY(read_route_counts(cnt));
-          DSL_TRY(exchange(&Shard::out_st, &Shard::cap_s, &Shard::in_st, &Shard::in_st_cap, &Shard::n_in_st, cnt,
-                           src_off));
+          DSL_TRY(xfer(snd, so, sb, rcv, ro, rb));
+          // the new ones are materialized, judged and appended where they were generated
           for (int l = 0; l < L; l++) {
             Shard& S = sh[l];
-            if (!S.n_in_st) continue;
-            const uint64_t keep = span[l], need = keep + S.n_in_st;
+            uint64_t total = 0;
+            for (int d = 0; d < W; d++) total += rcnt[l][d];
+            if (!total) continue;
+            const uint64_t keep = span[l], need = keep + total;
             DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
             DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
             const size_t lv = S.level_size.size();
             DSL_TRY(hist_grow(S, lv, need, keep));
-            const int blocks = (int)std::min<uint64_t>((S.n_in_st + kBlock - 1) / kBlock, 256ull * 32);
-            hipLaunchKernelGGL(k_append_received<P>, dim3(blocks), dim3(kBlock), 0, stream, S.in_st, S.n_in_st,
-                               S.next + keep * NW, S.next_fp + keep, S.hpar[lv] + keep,
-                               S.hev[lv] + keep, S.n_in_st, S.ctr);
-            nbase[l].push_back(keep);
-            ncnt[l].push_back(S.n_in_st);
+            MaterializeArgs<P> ma{};
+            ma.sent = S.out_fp;
+            ma.reply = S.rep_in;
+            ma.cap = S.cap_fp;
+            for (int d = 0; d < kMaxShards; d++) ma.off[d + 1] = ma.off[d] + (d < W ? rcnt[l][d] : 0);
+            ma.cur = S.cur;
+            ma.cur_fp = S.cur_fp;
+            ma.me = S.gid;
+            ma.depth = depth + 1;
+            ma.incremental = depth > init_depth ? 1 : 0;
+            ma.next = S.next;
+            ma.next_fp = S.next_fp;
+            ma.next_parent = S.hpar[lv];
+            ma.next_event = S.hev[lv];
+            ma.next_base = keep;
+            ma.next_cap = total;
+            ma.ctr = S.ctr;
+            ma.terms = S.terms;
+            ma.term_cap = term_cap;
+            const int blocks = (int)std::min<uint64_t>((total + kBlock - 1) / kBlock, 256ull * 32);
+            hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
+            mat_keep[l] = keep;
+            mat_total[l] = total;
             span[l] = need;
           }
         }
@@ -944,6 +940,14 @@ struct BfsEngine : EngineBase {
           }
           DSL_HIP(hipStreamSynchronize(stream));
           for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
+        }
+        if (route)  // both rounds, the owners' probes and the materialization, up to the counters
+          stats.exchange_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx0).count();
+        for (int l = 0; l < L; l++) {  // the rows k_materialize appended
+          const uint64_t c = std::min<uint64_t>(sh[l].lc.next_size, mat_total[l]);
+          if (!c) continue;
+          nbase[l].push_back(mat_keep[l]);
+          ncnt[l].push_back(c);
         }
         if (!queued || q_pos == 0) {  // a queue is timed as a whole (its dispatches counted there)
           float kms = 0;

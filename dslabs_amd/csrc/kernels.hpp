@@ -729,67 +729,48 @@ __global__ void k_seed(const uint32_t* init, const Fp* fp, typename P::Params pr
 }
 
 // ---- multi-shard phases (see bfs_engine.hpp) -------------------------------------------------
+// A sharded level keeps every new state at the shard that generated it; only the visited set is
+// partitioned. Remote successors go to their owner as 24-byte FpRecs (round A), the owner probes
+// and answers one byte per record, in the order received (round B: its counts are round A's,
+// reversed, so no second count exchange), and the source materializes, judges and appends the
+// successors its owners found new.
 struct ProbeArgs {
   const FpRec* in;
   uint64_t n;
-  uint64_t src_off[kMaxShards + 1];  // records from source s are in [src_off[s], src_off[s+1])
-  int32_t W;
   Table table;
-  uint64_t* out_items;  // W regions of cap_v items (one per source)
-  uint64_t cap_v;
-  RouteCounters* rc;
+  uint8_t* reply;  // 1 = inserted (new), per received record
   LevelCounters* ctr;
 };
 
 __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
-  __shared__ BlockResv<> s_resv;
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_new = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    bool is_new = false;
-    int src = 0;
-    uint64_t item = 0;
-    if (i < a.n) {
-      const FpRec r = a.in[i];
-      while (src + 1 < a.W && a.src_off[src + 1] <= i) src++;
-      const int ins = table_insert(a.table, Fp{r.hi, r.lo});
-      if (ins == INS_NEW) {
-        is_new = true;
-        item = r.item;
-        c_new++;
-      } else if (ins == INS_FULL) {
-        atomicAdd(&a.ctr->err_table, 1ull);
-      }
-    }
-    const unsigned long long idx = block_reserve(s_resv, a.rc->out, is_new, src, a.W);
-    if (is_new) a.out_items[(uint64_t)src * a.cap_v + idx] = item;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const FpRec r = a.in[i];
+    const int ins = table_insert(a.table, Fp{r.hi, r.lo});
+    if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
+    c_new += ins == INS_NEW;
+    a.reply[i] = ins == INS_NEW ? 1 : 0;
   }
   block_flush(s_red, &a.ctr->new_states, c_new);
 }
 
-// A routed VALID new state: row, fingerprint, parent pointer, event.
-template <class P>
-struct StateRec {
-  uint32_t w[Layout<P>::kWords];
-  Fp fp;
-  uint64_t parent;
-  uint32_t event;
-  uint32_t pad;
-};
-
 template <class P>
 struct MaterializeArgs {
-  const uint64_t* items;  // items of this shard found new at their owner
-  uint64_t n;
+  const FpRec* sent;                 // W regions of cap records (this shard's round-A send buffer)
+  const uint8_t* reply;              // W regions of cap bytes (the owners' answers)
+  uint64_t cap;
+  uint64_t off[kMaxShards + 1];      // flattened index: records to shard d are [off[d], off[d+1])
   const uint32_t* cur;
   const Fp* cur_fp;
-  int32_t W, me, depth, incremental;
-  StateRec<P>* out;  // W regions of cap_s records
-  uint64_t cap_s;
-  RouteCounters* rc;
-  LevelCounters* ctr;
+  int32_t me, depth, incremental;
+  uint32_t* next;                    // rows [next_base, next_base + next_cap) of the next frontier
+  Fp* next_fp;
+  uint64_t* next_parent;
+  uint32_t* next_event;
+  uint64_t next_base, next_cap;
+  LevelCounters* ctr;                // next_size counts the appended rows
   TerminalRec* terms;
   uint32_t term_cap;
 };
@@ -797,93 +778,62 @@ struct MaterializeArgs {
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
-  __shared__ BlockResv<> s_resv;
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < a.n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
-    bool ship = false;
-    int dest = 0, tv = 0, tpi = -1;
-    uint64_t parent = 0, tkey = ~0ull;
-    int k = 0;
-    Delta<P> d;
-    Fp f{0, 0};
-    if (i < a.n) {
-      parent = a.items[i] >> 20;
-      k = (int)(a.items[i] & 0xfffff);
-      const uint32_t* w = a.cur + parent * NW;
-      delta_step<P>(w, k, d, prm, set);  // deterministic: the same successor as in k_level
-      f = delta_fingerprint<P>(w, a.cur_fp[parent], d);
-      dest = owner_of(f, a.W);
-      int pi = -1;
-      uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
-#pragma unroll
-      for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
-      const NodeView view{w, P::kNodeWords, d.node, my_nw};
-      const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
-      if (v == V_VALID) {
-        ship = true;
-      } else if (v >= V_TERM_EXCEPTION) {
-        tv = v;
-        tpi = pi;
-        tkey = term_key(v, f.hi);
-      }
-    }
-    fold_terminals(tkey != ~0ull, tkey, tv, tpi, (uint32_t)k, parent, a.ctr, a.terms, a.term_cap);
-    const unsigned long long idx = block_reserve(s_resv, a.rc->out, ship, dest, a.W);
-    StateRec<P>* r = a.out + (uint64_t)dest * a.cap_s + idx;
-    if (ship) {
-      const uint32_t* w = a.cur + parent * NW;
-      if (Net<P>::size(w) + d.out.n > P::kNetCap) {
-        atomicAdd(&a.ctr->err_overflow, 1ull);
-        ship = false;
-      }
-      r->fp = f;
-      r->parent = ((uint64_t)a.me << 48) | parent;
-      r->event = (uint32_t)k;
-      r->pad = (uint32_t)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
-    }
-    wave_emit<P>(ship, a.cur, parent, d, r->w);
-  }
-}
-
-template <class P>
-__global__ void __launch_bounds__(kBlock) k_append_received(const StateRec<P>* in, uint64_t n, uint32_t* next, Fp* next_fp,
-                                                            uint64_t* next_parent, uint32_t* next_event,
-                                                            uint64_t next_cap, LevelCounters* ctr) {
-  // rows [0, next_cap) of the received range; ctr->next_size counts them (k_level does not)
-  constexpr int NW = Layout<P>::kWords;
-  __shared__ BlockResv<> s_resv;
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_next_work = 0;
+  const uint64_t n = a.off[kMaxShards];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
-    const bool ok = i < n;
-    const unsigned long long idx = block_reserve(s_resv, &ctr->next_size, ok, 0, 1);
-    bool copy = false;
-    if (ok) {
-      if (idx < next_cap) {
-        copy = true;
-        next_fp[idx] = in[i].fp;
-        next_parent[idx] = in[i].parent;
-        next_event[idx] = in[i].event;
-        c_next_work += in[i].pad;  // enabled events of the state (next level's work)
-      } else {
-        atomicAdd(&ctr->err_frontier, 1ull);
+    bool ship = false;
+    int tv = 0, tpi = -1, k = 0;
+    uint64_t parent = 0, tkey = ~0ull;
+    Delta<P> d;
+    d.node = 0;
+    d.out.n = 0;
+    Fp f{0, 0};
+    if (i < n) {
+      int dst = 0;
+      while (dst + 1 < kMaxShards && a.off[dst + 1] <= i) dst++;
+      const uint64_t slot = (uint64_t)dst * a.cap + (i - a.off[dst]);
+      if (a.reply[slot]) {
+        const FpRec r = a.sent[slot];
+        parent = r.item >> 20;
+        k = (int)(r.item & 0xfffff);
+        const uint32_t* w = a.cur + parent * NW;
+        delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
+        f = Fp{r.hi, r.lo};
+        int pi = -1;
+        uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
+#pragma unroll
+        for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+        const NodeView view{w, P::kNodeWords, d.node, my_nw};
+        const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
+        if (v == V_VALID) {
+          if (Net<P>::size(w) + d.out.n <= P::kNetCap) ship = true;
+          else atomicAdd(&a.ctr->err_overflow, 1ull);
+        } else if (v >= V_TERM_EXCEPTION) {
+          tv = v;
+          tpi = pi;
+          tkey = term_key(v, f.hi);
+        }
       }
     }
-    // rows copied by the whole wave, one row at a time (coalesced)
-    unsigned long long mask = __ballot(copy);
-    while (mask) {
-      const int src = __ffsll((long long)mask) - 1;
-      mask &= mask - 1;
-      const uint32_t* from = in[base + threadIdx.x - __lane_id() + src].w;
-      uint32_t* to = next + __shfl(idx, src) * NW;
-      for (int o = __lane_id(); o < NW; o += 64) to[o] = from[o];
+    fold_terminals(tkey != ~0ull, tkey, tv, tpi, (uint32_t)k, parent, a.ctr, a.terms, a.term_cap);
+    const unsigned long long li = wave_reserve(&a.ctr->next_size, ship);
+    const bool fits = ship && li < a.next_cap;
+    if (ship && !fits) atomicAdd(&a.ctr->err_frontier, 1ull);
+    const uint64_t idx = a.next_base + li;
+    if (fits) {
+      const uint32_t* w = a.cur + parent * NW;
+      a.next_fp[idx] = f;
+      a.next_parent[idx] = ((uint64_t)a.me << 48) | parent;
+      a.next_event[idx] = (uint32_t)k;
+      c_next_work += (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
+    wave_emit<P>(fits, a.cur, parent, d, a.next + idx * NW);
   }
-  block_flush(s_red, &ctr->next_work, c_next_work);
+  block_flush(s_red, &a.ctr->next_work, c_next_work);
 }
 
 }  // namespace dsl

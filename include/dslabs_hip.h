@@ -150,7 +150,7 @@ typedef struct {
   int32_t virtual_shards;   /* >1: emulate that many hash shards on this one device (tests) */
   uint8_t comm_id[128];     /* RCCL ncclUniqueId when world_size > 1 */
   int64_t replicate_below;  /* multi-shard: a level whose frontier is smaller runs replicated on every
-                               shard (no exchange); -1 = default (524288), 0 = always hash-sharded */
+                               shard (no exchange); -1 = default (65536), 0 = always hash-sharded */
 } dsl_engine_config;
 
 /* A decoded event (MessageEnvelope / TimerEnvelope, T/MessageEnvelope.java, T/TimerEnvelope.java). */

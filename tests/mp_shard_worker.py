@@ -2,7 +2,7 @@
 
 env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT; argv: <mode> <out.json>
 mode 'collectives' runs the dsl_host_comm callbacks directly (CPU only);
-mode 'lab0' / 'sipaxos' / 'mutant' runs a sharded search on cuda:0 through the engine."""
+mode 'lab0' / 'sipaxos' / 'mutant' / 'mp_c5' runs a sharded search on cuda:0 through the engine."""
 import ctypes
 import json
 import os
@@ -52,8 +52,12 @@ def main():
         res["alltoallv"] = recv[:int(rb.sum())].tolist()
     else:
         from dslabs_amd import CLIENTS_DONE, RESULTS_OK, Engine, SearchSettings
-        from dslabs_amd.protocols import PingPong, SIPaxos
-        if mode == "lab0":
+        from dslabs_amd.protocols import MultiPaxos, PingPong, SIPaxos
+        if mode == "mp_c5":  # BASELINE C5 at maxDepth 12 (levels above replicate_below are sharded)
+            proto = MultiPaxos(3, 2, "append-xy")
+            s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
+            s.addInvariant(proto.predicate("APPENDS_LINEARIZABLE")).maxDepth(12)
+        elif mode == "lab0":
             proto = PingPong(2, 10)
             s = SearchSettings().addInvariant(RESULTS_OK).addPrune(CLIENTS_DONE)
         elif mode == "mutant":
@@ -63,7 +67,7 @@ def main():
             proto = SIPaxos(2, 3, ("a", "b"))
             s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
             s.maxDepth(9)
-        s.table_log2_slots = 22
+        s.table_log2_slots = 23 if mode == "mp_c5" else 22
         rb = int(os.environ.get("DSL_TEST_REPLICATE_BELOW", "0"))
         eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=rb)
         r = eng.bfs(proto.initial_state(), s)

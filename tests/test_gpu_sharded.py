@@ -12,6 +12,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 LAB0 = json.load(open(os.path.join(GOLD, "lab0.json")))
 SIP = json.load(open(os.path.join(GOLD, "sipaxos.json")))
+MPX = json.load(open(os.path.join(GOLD, "multipaxos.json")))
 
 
 @pytest.mark.parametrize("shards,rep", [(2, 0), (3, 0), (8, 0), (3, 40), (8, -1)])
@@ -51,7 +52,8 @@ def test_virtual_shards_terminal_trace(shards, rep):
 
 
 @pytest.mark.parametrize("mode,world,rep", [("lab0", 2, 0), ("sipaxos", 3, 0), ("mutant", 2, 0), ("lab0", 3, 40),
-                                            ("sipaxos", 2, 100), ("mutant", 2, 40)])
+                                            ("sipaxos", 2, 100), ("mutant", 2, 40), ("mp_c5", 2, -1),
+                                            ("mp_c5", 3, -1)])
 def test_multiprocess_shards_one_gpu(mode, world, rep):
     """world processes on cuda:0, one shard each, exchanging through the gloo host transport;
     rep > 0: replicated small levels first (a terminal inside them walks a local chain)."""
@@ -62,6 +64,8 @@ def test_multiprocess_shards_one_gpu(mode, world, rep):
         want = LAB0["lab0_2c10p_exhaustive"]["per_depth"]
     elif mode == "sipaxos":
         want = SIP["sipaxos_2p3a_d9"]["per_depth"]
+    elif mode == "mp_c5":  # the default replicate_below shards C5's largest levels
+        want = MPX["mp_c5_d12"]["per_depth"]
     else:
         want = None
     for r in res:
@@ -72,3 +76,20 @@ def test_multiprocess_shards_one_gpu(mode, world, rep):
             assert r["trace"] == LAB0["lab0_mutant_nocheck"]["pinned"]["trace"]
     if not (mode == "mutant" and rep > 0):
         assert sum(r["exchanged"] for r in res) > 0
+
+
+@pytest.mark.parametrize("shards", [2, 4, 8])
+def test_virtual_shards_c5_default_settings(shards):
+    """BASELINE C5 (d12) with the default replicate_below: the levels above it are hash-sharded
+    (states routed), per-depth counts equal the golden vector."""
+    import argmap
+    case = MPX["mp_c5_d12"]
+    proto = argmap.protocol(case["args"])
+    eng = Engine(proto, virtual_shards=shards)
+    try:
+        r = eng.bfs(proto.initial_state(), argmap.settings(case["args"], proto, table_log2=23))
+        st = eng.kernel_stats()
+    finally:
+        eng.close()
+    assert r.per_depth == case["per_depth"]
+    assert st["exchanged"] > 0 and st["sharded_levels"] > 0
