@@ -253,15 +253,19 @@ struct MultiPaxos {
     put(w, 7, 1, 0);   // electing
     put(w, 11, 3, 0);  // p1bVotes
     int last = 0;
+    // fixed trip counts (predicated on i <= last): every merged[] / log access has a constant
+    // index, so nothing here is a dynamically indexed private array (scratch memory)
     uint32_t merged[kSlots + 1];
+#pragma unroll
     for (int i = 1; i <= kSlots; i++) {
       merged[i] = p1entry(w, i);
       if (e_status(merged[i]) != EMPTY || e_status(entry(w, i)) != EMPTY) last = i;
     }
     w[4] = 0;
     w[5] = 0;
-    for (int i = 1; i <= last; i++) {
-      if (e_status(entry(w, i)) == CHOSEN) continue;
+#pragma unroll
+    for (int i = 1; i <= kSlots; i++) {
+      if (i > last || e_status(entry(w, i)) == CHOSEN) continue;
       if (e_status(merged[i]) == CHOSEN) {
         set_entry(w, i, mk_entry(CHOSEN, 0, e_cmd(merged[i])));
         set_votes2(w, i, 0);
@@ -386,8 +390,9 @@ struct MultiPaxos {
       const int cmd = (int)(m & 7), c = cmd_client(cmd), q = cmd_seq(cmd);
       int last_seq[kMaxClients];
       executed(w, p, slot_out(w), last_seq);
-      if (last_seq[c] >= q) {  // AMO: already executed; an active leader replies from the cache
-        if (active(w) && last_seq[c] == q) {
+      const int ls = c ? last_seq[1] : last_seq[0];
+      if (ls >= q) {  // AMO: already executed; an active leader replies from the cache
+        if (active(w) && ls == q) {
           const uint32_t r = result_of(w, p, slot_out(w), c, q);
           out.send(msg(M_REPLY, s, p.servers + c, (uint64_t)q | ((uint64_t)r << 2)));
         }
