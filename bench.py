@@ -166,12 +166,13 @@ def pmc_traffic(workload: str, depth: int, launches: int, staged_bytes: int = 0)
 
 
 def roofline(stats: dict, workload: str, depth: int) -> dict:
-    """Algorithmic bytes of k_level per launch (SURVEY.md §8d byte model):
-    parents read once (S B), one 64-B bucket line probed per successor, one bucket line written
-    back + 12 B parent/event per new state, S B per successor appended to the next frontier;
-    divided by the summed k_level durations (HIP events on the engine's stream)."""
+    """Algorithmic bytes of k_level per launch (SURVEY.md §8d byte model): every
+    parent read once (its S-byte row + 16-byte fingerprint); one random 64-byte line access (the
+    probe-insert CAS) per probed successor -- a successor that changes nothing is its parent and
+    is not probed; every appended state written once (row + fingerprint + 12 bytes of parent and
+    event); divided by the summed k_level durations (HIP events on the engine's stream)."""
     S = stats["state_bytes"]
-    alg = stats["parents"] * S + stats["work_items"] * 64 + stats["new_states"] * (64 + 12) + stats["appended"] * S
+    alg = stats["parents"] * (S + 16) + stats["probes"] * 64 + stats["appended"] * (S + 16 + 12)
     t = stats["expand_ms"] / 1e3
     achieved = alg / t / 1e9 if t > 0 else 0.0
     launches = max(1, stats["expand_launches"])
