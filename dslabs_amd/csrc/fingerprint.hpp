@@ -85,17 +85,29 @@ struct Table {
 // are performed at the memory side (coherent across the 8 XCD L2s), so a probe is ONE memory
 // round trip whether the state is new or not -- a bucket load followed by a CAS was two for every
 // new state (measured on C5: +18 % at d12, +26 % at d14, profiles/r02_*).
-__device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
+__device__ __forceinline__ uint64_t table_home(const Table& t, const Fp& f) {
+  return ((f.lo & t.bucket_mask) << 3) | ((f.lo >> 28) & 7);
+}
+// The CAS at the home slot, issued now and answered later (table_settle): work placed in between
+// runs while the atomic is in flight.
+__device__ __forceinline__ unsigned long long table_cas_home(const Table& t, const Fp& f) {
+  return atomicCAS(t.slots + table_home(t, f), 0ull, (unsigned long long)(f.hi | 1ull));
+}
+__device__ __forceinline__ int table_settle(const Table& t, const Fp& f, unsigned long long old) {
   const unsigned long long key = (unsigned long long)(f.hi | 1ull);
+  if (old == 0ull) return INS_NEW;
+  if (old == key) return INS_EXISTS;
   const uint64_t nmask = t.bucket_mask * 8 + 7;
-  uint64_t i = ((f.lo & t.bucket_mask) << 3) | ((f.lo >> 28) & 7);
-  for (int probe = 0; probe < 8 * t.max_probes; probe++, i = (i + 1) & nmask) {
-    const unsigned long long old = atomicCAS(t.slots + i, 0ull, key);
+  uint64_t i = table_home(t, f);
+  for (int probe = 1; probe < 8 * t.max_probes; probe++) {
+    i = (i + 1) & nmask;
+    old = atomicCAS(t.slots + i, 0ull, key);
     if (old == 0ull) return INS_NEW;
     if (old == key) return INS_EXISTS;
   }
   return INS_FULL;
 }
+__device__ __forceinline__ int table_insert(const Table& t, const Fp& f) { return table_settle(t, f, table_cas_home(t, f)); }
 #else  // DSL_TABLE_LOAD_FIRST: read the bucket line, CAS only into an empty slot (round 1)
 __device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
   const unsigned long long key = (unsigned long long)(f.hi | 1ull);
