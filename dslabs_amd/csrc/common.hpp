@@ -103,6 +103,27 @@ DSL_HD void sel_put(uint32_t* w, int i, uint32_t v) {
 #pragma unroll
   for (int k = 0; k < N; k++) w[k] = (i == k) ? v : w[k];
 }
+// An opaque copy of v: per-element selects over a private array stay selects of VALUES (the
+// optimizer would otherwise merge them into one access at a computed address, and a dynamically
+// addressed private array -- or a kernel-argument struct -- is copied to scratch memory).
+template <class T>
+DSL_HD T keep_value(T v) {
+#ifdef __HIP_DEVICE_COMPILE__
+  asm("" : "+v"(v));
+#endif
+  return v;
+}
+// a[r][c] of a small parameter table for run-time r, c (a select chain, see keep_value).
+template <int R, int C>
+DSL_HD int sel_param(const int32_t (&a)[R][C], int r, int c) {
+  int v = 0;
+#pragma unroll
+  for (int i = 0; i < R; i++)
+#pragma unroll
+    for (int j = 0; j < C; j++) v = (i == r && j == c) ? keep_value((int)a[i][j]) : v;
+  return v;
+}
+
 // Bit-field get/put over a node's N words (fields never straddle a word).
 template <int N>
 DSL_HD int field_get(const uint32_t* w, int bit, int width) {

@@ -92,17 +92,6 @@ struct SendsDistinct<P, std::void_t<decltype(P::kSendsDistinct)>> : std::integra
 // Every access to r[] uses a compile-time index (fully unrolled loops predicated on i < n), so
 // the list lives in VGPRs; a dynamically indexed per-lane array would be placed in scratch and
 // every send would pay a memory round trip.
-// An opaque copy of v: per-element selects over a private array stay selects of VALUES (the
-// optimizer would otherwise merge them into one store to a computed address, and a dynamically
-// addressed private array lives in scratch memory).
-template <class T>
-DSL_HD T keep_value(T v) {
-#ifdef __HIP_DEVICE_COMPILE__
-  asm("" : "+v"(v));
-#endif
-  return v;
-}
-
 template <class P>
 struct Sender {
   using Rec = typename P::Rec;

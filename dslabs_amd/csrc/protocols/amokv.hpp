@@ -76,7 +76,7 @@ struct AmoKV {
     if (seq == last) {
       r = amo >> 2;
     } else {  // KVStore.execute
-      const int k = seq - 1, op = p.op[c][k], key = p.key[c][k], sym = p.sym[c][k];
+      const int k = seq - 1, op = sel_param(p.op, c, k), key = sel_param(p.key, c, k), sym = sel_param(p.sym, c, k);
       uint32_t v = sel_word<kNodeWords>(w, key);
       if (op == OP_GET) {
         r = v_len(v) ? res(R_GET, v) : res(R_NOTFOUND, 0);
@@ -177,7 +177,7 @@ struct AmoKV {
           const uint32_t* w = v.node(1 + c);
           const int n = nres(w);
           for (int k = 0; k < n; k++)
-            if (p.expected[c][k] >= 0 && sel_word<kNodeWords>(w, 2 + k) != (uint32_t)p.expected[c][k]) return PV_FALSE;
+            if (sel_param(p.expected, c, k) >= 0 && sel_word<kNodeWords>(w, 2 + k) != (uint32_t)sel_param(p.expected, c, k)) return PV_FALSE;
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
@@ -201,11 +201,11 @@ struct AmoKV {
           const uint32_t* w = v.node(1 + c);
           const int nr = nres(w);
           for (int k = 0; k < nr; k++) {
-            if (p.op[c][k] != OP_APPEND) return PV_THREW;  // "Client workers have non-Append Commands"
+            if (sel_param(p.op, c, k) != OP_APPEND) return PV_THREW;  // "Client workers have non-Append Commands"
             const uint32_t r = sel_word<kNodeWords>(w, 2 + k);
             if (r_type(r) != R_APPEND) return PV_FALSE;
             const uint32_t val = r_value(r), len = v_len(val);
-            if (len == 0 || (int)((val >> (4 + 2 * (len - 1))) & 3) != p.sym[c][k]) return PV_FALSE;  // endsWith
+            if (len == 0 || (int)((val >> (4 + 2 * (len - 1))) & 3) != sel_param(p.sym, c, k)) return PV_FALSE;  // endsWith
             all[n++] = val;
           }
         }

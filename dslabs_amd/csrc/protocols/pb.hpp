@@ -72,7 +72,7 @@ struct PB {
     const int last = amo & 3;
     if (seq < last) return -1;
     if (seq == last) return amo >> 2;
-    const int k = seq - 1, op = p.op[c][k], key = p.key[c][k], sym = p.sym[c][k];
+    const int k = seq - 1, op = sel_param(p.op, c, k), key = sel_param(p.key, c, k), sym = sel_param(p.sym, c, k);
     const int vb = 32 + 8 * key;
     int v = get(w, vb, 8), r;
     if (op == OP_GET) {
@@ -342,7 +342,7 @@ struct PB {
         for (int c = 0; c < p.clients; c++) {
           const uint32_t* w = v.node(c0 + c);
           for (int k = 0; k < nres(w); k++)
-            if (p.expected[c][k] >= 0 && result_at(w, k) != p.expected[c][k]) return PV_FALSE;
+            if (sel_param(p.expected, c, k) >= 0 && result_at(w, k) != sel_param(p.expected, c, k)) return PV_FALSE;
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
