@@ -31,7 +31,10 @@ constexpr int kBlock = 256;
 constexpr int kLevelBlock = 256;
 constexpr uint32_t kTermCap = 1024;  // default TerminalRec entries per shard (DSL_TERM_CAP)
 constexpr int kMaxShards = 16;
-constexpr int kWin = 1024;  // work items per class-sorted window of k_level
+#ifndef DSL_KWIN
+#define DSL_KWIN 1024
+#endif
+constexpr int kWin = DSL_KWIN;  // work items per class-sorted window of k_level
 // The next frontier is written into up to kSegs segments, one reservation counter each (a
 // workgroup appends to segment blockIdx % nseg), so every wavefront reserves its rows with one
 // returning atomic and no workgroup barrier, and no counter word carries more than 1/kSegs of
@@ -340,6 +343,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ SegTable s_segs;
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
+  __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kLevelBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[NWAVE];
   __shared__ int s_wsum[NWAVE];
   __shared__ int s_cbase[kWin / 64][NC];
@@ -403,6 +407,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+#ifdef DSL_PHASES_SPLIT0
+    PH_MARK(5);  // (instrumentation variant) the staging alone
+#endif
 #ifdef DSL_X2_STAGE  // cost probe (tools/gpu_r02_x2.sh): the staging again
     stage_lds(reinterpret_cast<const uint4*>(a.cur + p0 * NW), reinterpret_cast<uint4*>(rows), pb * NW / 4);
     stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
@@ -595,7 +602,14 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               if (ins == INS_NEW) {
                 c_new++;
                 int pi = -1;
-                const NodeView view{w, P::kNodeWords, dnode, my_nw};
+                NodeView view{w, P::kNodeWords, dnode, my_nw};
+                if constexpr (NetPreds<P>::value) {  // the new records through LDS (no register addresses)
+                  typename P::Rec* ms = s_sends + tid * P::kMaxSends;
+#pragma unroll
+                  for (int q = 0; q < P::kMaxSends; q++) ms[q] = d.out.r[q];
+                  view.sends = ms;
+                  view.nsends = dn;
+                }
                 const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
 #ifdef DSL_X2_JUDGE  // cost probe: the judge again
                 {
@@ -779,6 +793,7 @@ template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
+  __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_next_work = 0;
   const uint64_t n = a.off[kMaxShards];
@@ -807,7 +822,14 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
         uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
 #pragma unroll
         for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
-        const NodeView view{w, P::kNodeWords, d.node, my_nw};
+        NodeView view{w, P::kNodeWords, d.node, my_nw};
+        if constexpr (NetPreds<P>::value) {
+          typename P::Rec* ms = s_sends + threadIdx.x * P::kMaxSends;
+#pragma unroll
+          for (int q = 0; q < P::kMaxSends; q++) ms[q] = d.out.r[q];
+          view.sends = ms;
+          view.nsends = d.out.n;
+        }
         const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
         if (v == V_VALID) {
           if (Net<P>::size(w) + d.out.n <= P::kNetCap) ship = true;

@@ -81,6 +81,12 @@ struct Net {
   }
 };
 
+// P::kNetPreds: some predicate of P reads the network (StatePredicate.containsMessageMatching),
+// so the judge's view must carry the successor's new records.
+template <class P, class = void>
+struct NetPreds : std::false_type {};
+template <class P>
+struct NetPreds<P, std::void_t<decltype(P::kNetPreds)>> : std::integral_constant<bool, P::kNetPreds> {};
 // P::kSendsDistinct: no handler of P sends one record twice in one step (tests/hostcheck checks
 // it on every explored step), so Sender needs no duplicate check.
 template <class P, class = void>
@@ -123,8 +129,24 @@ struct NodeView {
   int nw;                   // words per node
   int changed;              // node replaced by `over` (-1: none)
   const uint32_t* over;
+  // network predicates (P::kNetPreds): the state's records are the parent row's (base is a whole
+  // row) plus `nsends` new records of type P::Rec at `sends`
+  const void* sends = nullptr;
+  int nsends = 0;
   DSL_HD const uint32_t* node(int i) const { return i == changed ? over : base + i * nw; }
 };
+
+// Any record of the viewed state (parent records + the view's new records) satisfying f.
+template <class P, class F>
+DSL_HD bool view_any_record(const NodeView& v, F f) {
+  const int n = Net<P>::size(v.base);
+  for (int j = 0; j < n; j++)
+    if (f(Net<P>::at(v.base, j))) return true;
+  const auto* r = static_cast<const typename P::Rec*>(v.sends);
+  for (int j = 0; j < v.nsends; j++)
+    if (f(r[j])) return true;
+  return false;
+}
 
 // ---- fingerprint ------------------------------------------------------------------------------
 DSL_HD Fp fp_xor(Fp a, Fp b) { return Fp{a.hi ^ b.hi, a.lo ^ b.lo}; }

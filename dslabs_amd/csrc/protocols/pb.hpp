@@ -34,6 +34,7 @@ struct PB {
   static constexpr int kNodes = 1 + kMaxServers + kMaxClients, kNodeWords = 3, kNetCap = 64, kMaxSends = 3;
   static constexpr int kMsgClasses = 9;  // handler classes of messages (message types 0..8); timers: class 9
   static constexpr int kMaxView = 15;
+  static constexpr bool kNetPreds = true;  // hasViewReply(n, p, b) and initView's goal read the network
   using Rec = uint64_t;
   using State = StateOf<PB>;
   enum { M_PING = 0, M_GETVIEW, M_VIEWREPLY, M_REQUEST, M_REPLY, M_ST, M_STACK, M_FORWARD, M_FORWARDACK,
@@ -361,6 +362,25 @@ struct PB {
         return nres(v.node((int)pr.arg0)) == pr.arg1 ? PV_TRUE : PV_FALSE;
       case DSL_PRED_PB_HAS_VIEW_REPLY:
         return get(v.node(0), 15, 4) >= pr.arg0 ? PV_TRUE : PV_FALSE;
+      case DSL_PRED_PB_VIEW_REPLY_EXACT: {  // StatePredicate.containsMessageMatching over the network
+        const int view = pr.arg0;
+        return view_any_record<PB>(v, [view](Rec r) { return m_type(r) == M_VIEWREPLY && (int)(r & 0xff) == view; })
+                   ? PV_TRUE : PV_FALSE;
+      }
+      case DSL_PRED_PB_VIEW_REPLIES_SENT: {
+        const int view = pr.arg0, prim = v_p(view);
+        uint32_t got = 0;
+        const bool ack = view_any_record<PB>(v, [&](Rec r) {
+          if (m_type(r) == M_VIEWREPLY && (int)(r & 0xff) == view) got |= 1u << rec_to(r);
+          return m_type(r) == M_PING && rec_from(r) == prim && rec_to(r) == 0 && (int)(r & 15) == v_num(view);
+        });
+        if (!ack) return PV_FALSE;  // the ack may come before some replies: finish the scan
+        view_any_record<PB>(v, [&](Rec r) {
+          if (m_type(r) == M_VIEWREPLY && (int)(r & 0xff) == view) got |= 1u << rec_to(r);
+          return false;
+        });
+        return (got & (uint32_t)pr.arg1) == (uint32_t)pr.arg1 ? PV_TRUE : PV_FALSE;
+      }
       default:
         return PV_THREW;
     }
@@ -369,13 +389,15 @@ struct PB {
     const uint32_t clients = ((1u << p.clients) - 1u) << (1 + p.servers);
     switch (pr.id) {
       case DSL_PRED_PB_HAS_VIEW_REPLY: return 1u;  // the viewserver's maxSent (see the header)
+      case DSL_PRED_PB_VIEW_REPLY_EXACT: case DSL_PRED_PB_VIEW_REPLIES_SENT: return kReadsAll;  // the network
       case DSL_PRED_RESULTS_OK: case DSL_PRED_CLIENTS_DONE: case DSL_PRED_CLIENT_DONE: case DSL_PRED_NONE_DECIDED:
       case DSL_PRED_CLIENT_HAS_RESULTS: return clients;
       default: return kReadsAll;
     }
   }
   static bool known_predicate(int id) {
-    return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == DSL_PRED_PB_HAS_VIEW_REPLY;
+    return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) ||
+           (id >= DSL_PRED_PB_HAS_VIEW_REPLY && id <= DSL_PRED_PB_VIEW_REPLIES_SENT);
   }
   static bool valid(const Params& p) {
     if (p.servers < 1 || p.servers > kMaxServers || p.clients < 1 || p.clients > kMaxClients || p.ncmds < 1 ||

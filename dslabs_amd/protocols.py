@@ -484,12 +484,73 @@ class PB(Protocol):
                     ps += [0, 0, 0, -1]
         return ps
 
+    @staticmethod
+    def _view_bits(n: int, p: int, b: int) -> int:
+        return n | (max(p, 0) << 4) | (max(b, 0) << 6)
+
     def predicate(self, name):
+        """hasViewReply:N (viewNum >= N), hasViewReply:N:P:B (exactly View(N, P, B); -1 = null,
+        PrimaryBackupTest.java:104-117) and viewRepliesSent:N:P:B:addr+addr+... (initView's goal,
+        :136-156); P and B are server indices (1 = server1)."""
         from .search import StatePredicate
         if name.startswith("hasViewReply:"):
-            n = int(name.split(":")[1])
-            return StatePredicate(f"ViewReply with viewNum: {n}", 500, n)
+            parts = [int(x) for x in name.split(":")[1:]]
+            if len(parts) == 1:
+                return StatePredicate(f"ViewReply with viewNum: {parts[0]}", 500, parts[0])
+            n, p, b = parts
+            return StatePredicate(f"ViewReply with View({n}, {p}, {b})", 501, self._view_bits(n, p, b))
+        if name.startswith("viewRepliesSent:"):
+            _, n, p, b, to = name.split(":")
+            mask = 0
+            for a in to.split("+"):
+                mask |= 1 << self.address_index(a)
+            return StatePredicate(f"ViewReply for View({n}, {p}, {b}) sent to {to}, primary ack sent", 502,
+                                  self._view_bits(int(n), int(p), int(b)), mask)
         raise KeyError(name)
+
+    def initView(self, viewNum: int, primary: str, backup=None, *clients, start=None, device: int = -1,
+                 max_time_secs: int = 30):
+        """PrimaryBackupTest.initView (PrimaryBackupTest.java:124-187): a BFS (network off except the
+        ViewServer's links and primary <-> backup) for a state where View(viewNum, primary, backup)
+        has ViewReplies sent to the primary, the backup and `clients` and the primary's ack Ping is
+        in the network, without any later view; then those ViewReplies and the ack are delivered in
+        turn (stepMessage). Returns the prepared start state."""
+        from . import _lib
+        from .search import Search, SearchSettings
+        pi = self.address_index(primary)
+        bi = self.address_index(backup) if backup is not None else -1
+        to_init = [primary] + ([backup] if backup is not None else []) + list(clients)
+        n1 = viewNum + 1
+        s = SearchSettings().maxTimeSecs(max_time_secs)
+        s.addPrune(self.predicate(f"hasViewReply:{n1}"))
+        s.addPrune(self.predicate(f"hasViewReply:{viewNum}").and_(
+            self.predicate(f"hasViewReply:{viewNum}:{pi}:{bi}").negate()))
+        s.networkActive(False).nodeActive("viewserver", True)
+        if backup is not None:
+            s.linkActive(primary, backup, True).linkActive(backup, primary, True)
+        s.addGoal(self.predicate(f"viewRepliesSent:{viewNum}:{pi}:{bi}:{'+'.join(to_init)}").and_(
+            self.predicate(f"hasViewReply:{n1}").negate()))
+        r = Search.bfs(start if start is not None else self.initial_state(), s, device)
+        goal = r.goalMatchingState()
+        if goal is None:
+            raise RuntimeError(f"initView: no state with View({viewNum}, {primary}, {backup}) started: "
+                               f"{r.endCondition().name}")
+        view = self._view_bits(viewNum, pi, bi)
+        evs = []
+        for a in to_init:  # the ViewReplies, then the primary's ack
+            e = _lib.dsl_event()
+            e.from_, e.to, e.type, e.n_fields = 0, self.address_index(a), 2, 1
+            e.fields[0] = view
+            evs.append(e)
+        e = _lib.dsl_event()
+        e.from_, e.to, e.type, e.n_fields = pi, 0, 0, 1
+        e.fields[0] = viewNum
+        evs.append(e)
+        rr = Search.replay(goal, SearchSettings(), evs, minimize=False, device=device)
+        st = rr.lastState()
+        if st is None or st.depth() != goal.depth() + len(evs):
+            raise RuntimeError("initView: a prepared message could not be delivered")
+        return st
 
     # ---- rendering in the oracle's toString form ------------------------------------------------
     def _value_str(self, v: int) -> str:

@@ -389,6 +389,11 @@ class SearchResults:
     def endCondition(self) -> EndCondition:
         return self._end
 
+    def lastState(self) -> Optional[SearchState]:
+        """The state a replay ended in (TraceReplaySearch: also when the trace ran out or an event
+        could not be delivered); for a search, its terminal state."""
+        return getattr(self, "_last", None) or self._terminal
+
     def invariantViolatingState(self) -> Optional[SearchState]:
         return self._terminal if self._end == EndCondition.INVARIANT_VIOLATED else None
 
@@ -543,20 +548,26 @@ class Engine:
             per_depth = [r.per_depth[i] for i in range(r.n_levels)]
             end = EndCondition(r.end_condition)
             terminal = None
+            last = None
             pred = None
-            if r.terminal_depth >= 0 and r.terminal_state:
+            if r.terminal_state:
                 raw = [r.trace[i] for i in range(r.trace_len)]
                 events = [self.protocol.render_event(e) for e in raw]
                 packed = bytes(ctypes.cast(r.terminal_state, ctypes.POINTER(ctypes.c_uint8 * r.state_bytes)).contents)
                 base_events = state.trace() if state.packed is not None else []
-                terminal = SearchState(self.protocol, packed, r.terminal_depth, base_events + events,
-                                       [_lib.dsl_event.from_buffer_copy(e) for e in raw], state._dropped)
+                last = SearchState(self.protocol, packed, r.terminal_depth if r.terminal_depth >= 0 else r.max_depth,
+                                   base_events + events, [_lib.dsl_event.from_buffer_copy(e) for e in raw],
+                                   state._dropped)
+                if r.terminal_depth >= 0:
+                    terminal = last
                 if end == EndCondition.INVARIANT_VIOLATED:
                     pred = PredicateResult(settings.invariants()[r.predicate_index], False)
                 elif end == EndCondition.GOAL_FOUND:
                     pred = PredicateResult(settings.goals()[r.predicate_index], True)
-            return SearchResults(end, r.states, per_depth, r.initial_depth, r.max_depth, terminal, pred,
-                                 r.elapsed_s, r.successors)
+            res = SearchResults(end, r.states, per_depth, r.initial_depth, r.max_depth, terminal, pred,
+                                r.elapsed_s, r.successors)
+            res._last = last
+            return res
         finally:
             lib.dsl_result_free(res_p)
 

@@ -103,6 +103,10 @@ typedef enum {
   DSL_PRED_HAS_COMMAND = 404,       /* PaxosTest hasCommand(a, i, c) (:119-123): arg0 = server node,
                                        arg1 = slot << 8 | KV command code (op << 2 | value; 0 = null) */
   DSL_PRED_PB_HAS_VIEW_REPLY = 500, /* PrimaryBackupTest.hasViewReply(n): arg0 = n */
+  DSL_PRED_PB_VIEW_REPLY_EXACT = 501,  /* hasViewReply(n, p, b) (:112-117): arg0 = view (num | p << 4 | b << 6) */
+  DSL_PRED_PB_VIEW_REPLIES_SENT = 502, /* initView's "ViewReply for v sent to nodes ..., primary ack sent"
+                                          (PrimaryBackupTest.java:136-156): arg0 = view, arg1 = mask of
+                                          recipient node indices */
   DSL_PRED_MINI_FOO = 700,          /* SearchAndTraceMinimizerTest foo: !a.foo */
   DSL_PRED_MINI_FOO_EXCEPTION = 701,    /* fooException: throws when a.foo, else true */
   DSL_PRED_MINI_ALWAYS_EXCEPTION = 702, /* alwaysException: always throws */

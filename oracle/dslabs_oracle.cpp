@@ -154,13 +154,19 @@ static Scenario build(const Args& a) {
     cfg.clients = a.geti("clients", 1);
     cfg.kv = amokv::Config::fromArgs(cfg.clients, a.get("workload", "putget"));
     sc.init = pb::initial(cfg, sc.names);
-    sc.pred = [common](const std::string& n) -> Predicate {
+    sc.pred = [common, &sc](const std::string& n) -> Predicate {
       auto p = common(n);
       if (p) return *p;
       if (n.rfind("hasViewReply:", 0) == 0) {  // hasViewReply:N or hasViewReply:N:P:B
         auto parts = split(n, ':');
         if (parts.size() == 2) return pb::hasViewReply(std::stoi(parts[1]));
         return pb::hasViewReplyExact(std::stoi(parts[1]), std::stoi(parts[2]), std::stoi(parts[3]));
+      }
+      if (n.rfind("viewRepliesSent:", 0) == 0) {  // viewRepliesSent:N:P:B:addr1+addr2+...
+        auto parts = split(n, ':');
+        std::vector<int> to;
+        for (auto& nm : split(parts[4], '+')) to.push_back(addrOf(sc.names, nm));
+        return pb::viewRepliesSent(std::stoi(parts[1]), std::stoi(parts[2]), std::stoi(parts[3]), to);
       }
       throw std::runtime_error("unknown predicate " + n);
     };
@@ -226,6 +232,15 @@ static Settings settingsFrom(const Args& a, Scenario& sc) {
   for (auto& n : a.all("inactive")) {  // TestSettings.nodeActive(n, false)
     st.senderActive[addrOf(sc.names, n)] = false;
     st.receiverActive[addrOf(sc.names, n)] = false;
+  }
+  if (a.has("network-off")) st.networkActive = false;  // TestSettings.networkActive(false)
+  for (auto& n : a.all("active")) {  // TestSettings.nodeActive(n, true)
+    st.senderActive[addrOf(sc.names, n)] = true;
+    st.receiverActive[addrOf(sc.names, n)] = true;
+  }
+  for (auto& l : a.all("link")) {  // TestSettings.linkActive(from, to, true): "from,to"
+    auto ft = split(l, ',');
+    st.linkActive[{addrOf(sc.names, ft[0]), addrOf(sc.names, ft[1])}] = true;
   }
   if (a.has("partition")) {  // TestSettings.partition: network off, links inside each group on
     st.networkActive = false;

@@ -363,5 +363,25 @@ inline Predicate hasViewReplyExact(int n, int p, int b) {
           }};
 }
 
+// PrimaryBackupTest.initView's goal (PrimaryBackupTest.java:136-156): a ViewReply for view v was
+// sent to every address of toInit, and the primary's Ping(v.num) to the ViewServer is in the
+// network (AbstractState.network(): the undropped and the dropped messages).
+inline Predicate viewRepliesSent(int n, int p, int b, std::vector<int> toInit) {
+  const View v{n, p, b};
+  return {"ViewReply for " + v.str() + " sent, primary ack sent", [v, toInit](const State& s) {
+            PredResult r;
+            std::set<int> found;
+            bool ack = false;
+            for (const auto* net : {&s.network, &s.dropped})
+              for (auto& e : *net) {
+                if (e.m.type == "Ping" && e.from == v.primary && std::stoi(e.m.f[0]) == v.num) ack = true;
+                else if (e.m.type == "ViewReply" && View::parse(e.m.f[0]) == v) found.insert(e.to);
+              }
+            r.value = ack;
+            for (int a : toInit) r.value = r.value && found.count(a);
+            return r;
+          }};
+}
+
 }  // namespace pb
 }  // namespace oracle

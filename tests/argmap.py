@@ -76,6 +76,12 @@ def settings(args, proto, table_log2=24):
             s.deliverTimers(v, False)
         elif a == "--inactive":
             s.nodeActive(v, False)
+        elif a == "--network-off":
+            s.networkActive(False)
+        elif a == "--active":
+            s.nodeActive(v, True)
+        elif a == "--link":
+            s.linkActive(*v.split(","), True)
         elif a == "--partition":
             s.partition(*[g.split(",") for g in v.split("|")])
         i += 1

@@ -220,6 +220,14 @@ PBF = {
     # a view change is reachable: ViewReply for view 3
     "pb_view3_goal": dict(args=PBA + ["--servers", "2", "--clients", "1", "--workload", "putget", "--goal",
                                       "hasViewReply:3", "--finish-level"], pinned={}),
+    # PrimaryBackupTest.initView(server1, server2, client1) (:124-187): the search for View(2, 1, 2)
+    # started, network off except the ViewServer and server1 <-> server2 (network predicates)
+    "pb_initview_search": dict(args=PBA + ["--servers", "2", "--clients", "1", "--workload", "putget", "--prune",
+                                           "hasViewReply:3", "--prune", "and(hasViewReply:2,!hasViewReply:2:1:2)",
+                                           "--network-off", "--active", "viewserver", "--link", "server1,server2",
+                                           "--link", "server2,server1", "--goal",
+                                           "and(viewRepliesSent:2:1:2:server1+server2+client1,!hasViewReply:3)",
+                                           "--finish-level"], pinned={}),
     # two clients appending to one key with expected results: RESULTS_OK is violated
     "pb_2c_results_violation": dict(args=PBA + ["--servers", "2", "--clients", "2", "--workload",
                                                 "appendappendget", "--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE",

@@ -142,6 +142,8 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       if ((int)per.size() <= d) per.resize(d + 1, 0);
       per[d]++;
       NodeView view{n.s.w, P::kNodeWords, dl.node, dl.nw};
+      view.sends = dl.out.r;
+      view.nsends = dl.out.n;
       v = judge_view<P>(view, prm, set, d, &pi);
       if (n.depth > 0) {  // the kernels' incremental check must give the same verdict
         int pi2 = -1;

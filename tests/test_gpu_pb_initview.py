@@ -1,0 +1,59 @@
+"""BASELINE C4 from PrimaryBackupTest.initView's prepared state (PrimaryBackupTest.java:124-187):
+the initView search (network off except the ViewServer's links and primary <-> backup; prunes on
+later views; goal = the view's replies and the primary's ack in the network, read through the
+device's network predicates) matches the oracle level by level; the prepared messages are then
+delivered (stepMessage) and the C4 search (RESULTS_OK, prune CLIENTS_DONE and hasViewReply(4))
+runs from that state, per-depth equal to the oracle started from the same trace."""
+import json
+import os
+import tempfile
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import CLIENTS_DONE, RESULTS_OK, EndCondition, Search, SearchSettings
+from dslabs_amd.protocols import PB
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+PBA = ["--proto", "pb", "--servers", "2", "--clients", "1", "--workload", "putget"]
+INITVIEW = PBA + ["--prune", "hasViewReply:3", "--prune", "and(hasViewReply:2,!hasViewReply:2:1:2)", "--network-off",
+                  "--active", "viewserver", "--link", "server1,server2", "--link", "server2,server1", "--goal",
+                  "and(viewRepliesSent:2:1:2:server1+server2+client1,!hasViewReply:3)"]
+
+
+def test_initview_search_matches_oracle():
+    gold = json.load(open(os.path.join(HERE, "golden", "pb.json")))["pb_initview_search"]
+    proto = argmap.protocol(INITVIEW)
+    r = Search.bfs(proto.initial_state(), argmap.settings(INITVIEW, proto))
+    assert r.endCondition().name == gold["end"] == "GOAL_FOUND"
+    assert r.per_depth == gold["per_depth"]
+    st = r.goalMatchingState()
+    rep = oracle_util.replay(INITVIEW, st.trace())
+    assert rep["ok"] and rep["goals"][0]["value"], rep
+
+
+@pytest.mark.parametrize("extra", [10, 13])
+def test_c4_from_initview(extra):
+    proto = PB(2, 1, "putget")
+    st = proto.initView(2, "server1", "server2", "client1")
+    assert st.trace()[-4:] == ["Message(viewserver -> server1, ViewReply(View(2, 1, 2)))",
+                               "Message(viewserver -> server2, ViewReply(View(2, 1, 2)))",
+                               "Message(viewserver -> client1, ViewReply(View(2, 1, 2)))",
+                               "Message(server1 -> viewserver, Ping(2))"]
+    s = SearchSettings().addInvariant(RESULTS_OK).addPrune(CLIENTS_DONE).addPrune(proto.predicate("hasViewReply:4"))
+    s.maxDepth(st.depth() + extra)
+    s.table_log2_slots = 24
+    r = Search.bfs(st, s)
+    args = PBA + ["--inv", "RESULTS_OK", "--prune", "CLIENTS_DONE", "--prune", "hasViewReply:4", "--max-depth",
+                  str(st.depth() + extra), "--finish-level"]
+    with tempfile.NamedTemporaryFile("w", suffix=".trace", delete=False) as f:
+        f.write("\n".join(st.trace()) + "\n")
+    try:
+        want = oracle_util.run("bfs", args + ["--start-trace", f.name], timeout=300)
+    finally:
+        os.unlink(f.name)
+    assert r.endCondition().name == want["end"]
+    assert r.per_depth == want["per_depth"][st.depth():]
+    assert r.endCondition() == EndCondition.SPACE_EXHAUSTED

@@ -150,7 +150,9 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
             if (ins == 0) continue;
             c_new++;
             int pidx = -1;
-            const NodeView view{r.w, P::kNodeWords, dl.node, dl.nw};
+            NodeView view{r.w, P::kNodeWords, dl.node, dl.nw};
+            view.sends = dl.out.r;
+            view.nsends = dl.out.n;
             const int v = judge_view<P>(view, prm, set, depth + 1, &pidx, depth > 0);
             if (v >= V_TERM_EXCEPTION) {
               my_best = std::min(my_best, v);
