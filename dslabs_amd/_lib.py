@@ -19,6 +19,7 @@ DSL_MAX_PREDICATES = 16
 DSL_MAX_POOL = 32
 DSL_MAX_PARAMS = 64
 DSL_MAX_EVENT_FIELDS = 8
+DSL_PROTO_PINGPONG_IR = 8  # protocols generated from the IR (dslabs_amd/ir/specs)
 
 # dsl_status
 DSL_OK = 0

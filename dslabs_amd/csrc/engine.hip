@@ -205,6 +205,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_AMOKV: return make_engine<AmoKV>(d, cfg, out);
     case DSL_PROTO_PB: return make_engine<PB>(d, cfg, out);
     case DSL_PROTO_MINITEST: return make_engine<MiniTest>(d, cfg, out);
+    case DSL_PROTO_PINGPONG_IR: return make_engine<PingPongIR>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -289,6 +290,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_AMOKV: return (int)sizeof(dsl::AmoKV::State);
     case DSL_PROTO_PB: return (int)sizeof(dsl::PB::State);
     case DSL_PROTO_MINITEST: return (int)sizeof(dsl::MiniTest::State);
+    case DSL_PROTO_PINGPONG_IR: return (int)sizeof(dsl::PingPongIR::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }
@@ -302,6 +304,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_AMOKV: { using P = dsl::AmoKV; return call; }           \
     case DSL_PROTO_PB: { using P = dsl::PB; return call; }                 \
     case DSL_PROTO_MINITEST: { using P = dsl::MiniTest; return call; }     \
+    case DSL_PROTO_PINGPONG_IR: { using P = dsl::PingPongIR; return call; } \
     default: return DSL_ERR_UNKNOWN_PROTOCOL;                           \
   }
 

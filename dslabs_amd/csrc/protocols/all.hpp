@@ -7,4 +7,5 @@
 #include "pingpong.hpp"
 #include "sipaxos.hpp"
 #include "synthetic.hpp"
+#include "gen/pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
 #define DSL_HAVE_MULTIPAXOS 1

@@ -1,0 +1,237 @@
+// PingPongIR -- GENERATED from the protocol IR (dslabs_amd/ir/specs/pingpong.py) by dslabs_amd/ir/gen_device.py; do not edit.
+// lab0 PingPong in the protocol IR (the same protocol as csrc/protocols/pingpong.hpp, restated):
+// labs/lab0-pingpong/src/dslabs/pingpong/PingServer.java:29-32 (handlePingRequest),
+// PingClient.java:41-87 (sendCommand / handlePongReply / onPingTimer), Timers.java:7-11
+// (PingTimer, RETRY_MILLIS = 10 ms), inside ClientWorker with PingTest's repeatedPings workload
+// (tst/dslabs/pingpong/PingTest.java:44-51): command k is Ping(k), its expected result Pong(k). The
+// README mutants are parameters (README.md:299-306 no timer re-set, :342-347 no value check).
+#pragma once
+#include "../../nodestate.hpp"
+
+namespace dsl {
+
+struct PingPongIR {
+  static constexpr int kNodes = 5, kNodeWords = 5, kNetCap = 120, kMaxSends = 2;
+  static constexpr int kMsgClasses = 2;
+  using Rec = uint32_t;
+  using State = StateOf<PingPongIR>;
+  struct Params {
+    int32_t clients;
+    int32_t pings;
+    int32_t check_value;
+    int32_t reset_timer;
+  };
+  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
+  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
+  static DSL_HD int rec_type(Rec r) { return (int)(r >> 31); }
+  static DSL_HD int rec_from(Rec r) { return (int)((r >> 28) & 7); }
+  static DSL_HD int rec_to(Rec r) { return (int)((r >> 25) & 7); }
+  static DSL_HD int msg_class(Rec r) { return rec_type(r); }
+  // node index -> kind: kinds are laid out in declaration order, instances consecutive
+  static DSL_HD int num_nodes(const Params& p) { return 1 + p.clients; }
+  static DSL_HD int first_pingserver(const Params& p) { (void)p; return 0; }
+  static DSL_HD bool is_pingserver(int i, const Params& p) { return i >= first_pingserver(p) && i < first_pingserver(p) + 1; }
+  static DSL_HD int first_client(const Params& p) { (void)p; return 0 + 1; }
+  static DSL_HD bool is_client(int i, const Params& p) { return i >= first_client(p) && i < first_client(p) + p.clients; }
+  // timer entries: fields from bit 0 in declaration order, the type above them
+  static DSL_HD void tbounds(int type, int& mn, int& mx) {
+    if (type == 0) { mn = 10; mx = 10; }
+  }
+  static DSL_HD int ttype(int e) { return 0; }
+  template <class O>
+  static DSL_HD void push_timer_client(uint32_t* w, int e, O& out) {
+    const int n = get(w, 8, 4);
+    if (n >= 15) { out.overflow = true; return; }
+    put(w, 12 + 4 * n, 4, e);
+    put(w, 8, 4, n + 1);
+  }
+  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)
+  static DSL_HD int deliverable_client(const uint32_t* w, int j) {
+    const int n = get(w, 8, 4);
+    int mm = 0x7fffffff, c = 0;
+    for (int q = 0; q < n; q++) {
+      int mn = 0, mx = 0;
+      tbounds(ttype(get(w, 12 + 4 * q, 4)), mn, mx);
+      if (q > 0 && mn >= mm) continue;
+      if (c == j) return q;
+      c++;
+      if (mx < mm) mm = mx;
+    }
+    return j < 0 ? c : -1;
+  }
+  static DSL_HD void remove_timer_client(uint32_t* w, int e) {  // the first equal entry
+    const int n = get(w, 8, 4);
+    int q0 = n;
+    for (int q = n - 1; q >= 0; q--)
+      if (get(w, 12 + 4 * q, 4) == e) q0 = q;
+    if (q0 >= n) return;
+    for (int q = q0; q + 1 < n; q++) put(w, 12 + 4 * q, 4, get(w, 12 + 4 * (q + 1), 4));
+    put(w, 12 + 4 * (n - 1), 4, 0);
+    put(w, 8, 4, n - 1);
+  }
+  template <class O>
+  static DSL_HD void send_command_client(int i, uint32_t* w, int cmd, O& out, const Params& p) {
+    (void)p;
+    put(w, 0, 4, cmd);
+    put(w, 4, 4, 0);
+    out.send(((Rec)0 << 31) | ((Rec)(i) << 28) | ((Rec)((0 + 1 - 1)) << 25) | ((Rec)((cmd) & 15) << 0));
+    push_timer_client(w, (((cmd) & 15) << 0), out);
+  }
+  // ClientWorker.sendNextCommandWhilePossible (waitingOnResult == |results| < workload size)
+  template <class O>
+  static DSL_HD void client_worker_client(int i, uint32_t* w, O& out, const Params& p) {
+    int n = get(w, 72, 4);
+    const int res = get(w, 4, 4);
+    if (n < p.pings && res != 0) {
+      if (n >= 15) { out.overflow = true; return; }
+      put(w, 76 + 4 * n, 4, res);
+      n++;
+      put(w, 72, 4, n);
+      if (n < p.pings) send_command_client(i, w, n + 1, out, p);
+    }
+  }
+  template <class O>
+  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {
+    if (is_pingserver(i, p)) {
+      return;
+    }
+    if (is_client(i, p)) {
+      if (p.pings > 0) send_command_client(i, w, 1, out, p);
+      return;
+    }
+  }
+  static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {
+    if (is_client(i, p)) return deliverable_client(w, -1);
+    (void)i; (void)w; (void)p;
+    return 0;
+  }
+  template <class O>
+  static DSL_HD int on_message(int i, uint32_t* w, Rec r, O& out, const Params& p) {
+    (void)w; (void)out;
+    if (is_pingserver(i, p)) {
+      if (rec_type(r) == 0) {  // PingRequest
+        out.send(((Rec)1 << 31) | ((Rec)(i) << 28) | ((Rec)(rec_from(r)) << 25) | ((Rec)(((int)((r >> 0) & 15u)) & 15) << 0));
+        return STEP_OK;
+      }
+      return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)
+    }
+    if (is_client(i, p)) {
+      if (rec_type(r) == 1) {  // PongReply
+        if (((p.check_value == 0) || (get(w, 0, 4) == (int)((r >> 0) & 15u)))) {
+          put(w, 4, 4, (int)((r >> 0) & 15u));
+        }
+        client_worker_client(i, w, out, p);
+        return STEP_OK;
+      }
+      return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)
+    }
+    return STEP_EXCEPTION;
+  }
+  template <class O>
+  static DSL_HD int on_timer(int i, uint32_t* w, int j, O& out, const Params& p) {
+    (void)w; (void)j; (void)out;
+    if (is_client(i, p)) {
+      const int q = deliverable_client(w, j);
+      if (q < 0) return STEP_NULL;
+      const int e = get(w, 12 + 4 * q, 4);
+      if (ttype(e) == 0) {  // PingTimer
+        const int tf_value = (e >> 0) & 15;
+        if (((get(w, 0, 4) == tf_value) && (get(w, 4, 4) == 0))) {
+          out.send(((Rec)0 << 31) | ((Rec)(i) << 28) | ((Rec)((0 + 1 - 1)) << 25) | ((Rec)((tf_value) & 15) << 0));
+          if ((p.reset_timer != 0)) {
+            push_timer_client(w, (((tf_value) & 15) << 0), out);
+          }
+        }
+        client_worker_client(i, w, out, p);
+        remove_timer_client(w, e);  // SearchState.stepTimer: the first equal entry
+        return STEP_OK;
+      }
+      return STEP_EXCEPTION;  // no handler for this timer
+    }
+    return STEP_EXCEPTION;
+  }
+  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const Params& p) {
+    const int c0 = first_client(p), nc = p.clients;
+    switch (pr.id) {
+      case DSL_PRED_RESULTS_OK:  // every result equals the workload's expected result
+        for (int c = c0; c < c0 + nc; c++) {
+          const uint32_t* w = v.node(c);
+          const int n = get(w, 72, 4);
+          for (int j = 0; j < n; j++)
+            if (get(w, 76 + 4 * j, 4) != (j + 1)) return PV_FALSE;
+        }
+        return PV_TRUE;
+      case DSL_PRED_CLIENTS_DONE:
+        for (int c = c0; c < c0 + nc; c++)
+          if (get(v.node(c), 72, 4) < p.pings) return PV_FALSE;
+        return PV_TRUE;
+      case DSL_PRED_CLIENT_DONE:
+        if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;
+        return get(v.node((int)pr.arg0), 72, 4) >= p.pings ? PV_TRUE : PV_FALSE;
+      case DSL_PRED_NONE_DECIDED:
+        for (int c = c0; c < c0 + nc; c++)
+          if (get(v.node(c), 72, 4) > 0) return PV_FALSE;
+        return PV_TRUE;
+      case DSL_PRED_CLIENT_HAS_RESULTS:
+        if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;
+        return get(v.node((int)pr.arg0), 72, 4) == pr.arg1 ? PV_TRUE : PV_FALSE;
+      default:
+        return PV_THREW;
+    }
+  }
+  static uint32_t pred_reads(const DevPred& pr, const Params& p) {
+    const uint32_t clients = ((1u << (p.clients)) - 1u) << first_client(p);
+    return (pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) ? clients : kReadsAll;
+  }
+  static bool known_predicate(int id) { return id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS; }
+  static bool valid(const Params& p) {
+    return p.clients >= 1 && p.clients <= 4 &&
+           p.pings >= 1 && p.pings <= 15 &&
+           p.check_value >= 0 && p.check_value <= 1 &&
+           p.reset_timer >= 0 && p.reset_timer <= 1 &&
+           p.clients >= 1 && p.clients <= 4;
+  }
+  static Params from_desc(const dsl_protocol_desc& d) {
+    Params p{};
+    p.clients = d.n_params > 0 ? (int32_t)d.params[0] : 1;
+    p.pings = d.n_params > 1 ? (int32_t)d.params[1] : 10;
+    p.check_value = d.n_params > 2 ? (int32_t)d.params[2] : 1;
+    p.reset_timer = d.n_params > 3 ? (int32_t)d.params[3] : 1;
+    return p;
+  }
+  static void describe_message(Rec r, dsl_event* e) {
+    e->from = rec_from(r);
+    e->to = rec_to(r);
+    e->type = rec_type(r);
+    e->n_fields = 0;
+    if (e->type == 0) {
+      e->n_fields = 1;
+      e->fields[0] = (int64_t)((r >> 0) & 15u);
+    }
+    if (e->type == 1) {
+      e->n_fields = 1;
+      e->fields[0] = (int64_t)((r >> 0) & 15u);
+    }
+  }
+  static void describe_timer(int i, const uint32_t* w, int j, const Params& p, dsl_event* e) {
+    e->is_timer = 1;
+    e->from = e->to = i;
+    (void)w; (void)j; (void)p;
+    if (is_client(i, p)) {
+      const int q = deliverable_client(w, j);
+      if (q < 0) return;
+      const int x = get(w, 12 + 4 * q, 4);
+      e->type = 2 + ttype(x);
+      int mn = 0, mx = 0;
+      tbounds(ttype(x), mn, mx);
+      e->timer_min = mn;
+      e->timer_max = mx;
+      if (ttype(x) == 0) {
+        e->n_fields = 1;
+        e->fields[0] = (x >> 0) & 15;
+      }
+    }
+  }
+};
+
+}  // namespace dsl

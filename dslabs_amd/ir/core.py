@@ -1,0 +1,413 @@
+"""Protocol IR: a small declarative description of a DSLabs protocol -- node kinds and their fields,
+message and timer records, handlers as statement lists -- from which both forms the engine needs
+are generated (dslabs_amd/ir/gen_device.py: the packed device protocol for csrc/protocols/;
+gen_oracle.py: the object form on the oracle's Node / Ctx / TimerQueue model). The reference
+dispatches to handlers by name over Java objects (framework/src/dslabs/framework/Node.java:479-562);
+here a handler is a Python function run once at generation time against a recorder, so its
+statements become C++ for both targets, and one description is the single source of both.
+
+Scope: integer fields of fixed bit width, bounded lists, messages / timers with integer fields,
+sends, timer sets (TimerQueue semantics with static (min, max) per timer type), conditionals and
+exceptions; client nodes run inside the reference's ClientWorker command loop (ClientWorker.java:
+174-251) with the workload "command k = k" (1-based) and expected results given by an expression
+of k. Values are plain integers (interned by the spec author); 0 means null.
+"""
+from __future__ import annotations
+
+import itertools
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+
+# ---- expressions -------------------------------------------------------------------------------
+class Expr:
+    """An integer / boolean expression with its C++ text for the device and the oracle."""
+
+    def __init__(self, dev: str, orc: str):
+        self.dev, self.orc = dev, orc
+
+    def _bin(self, o, op):
+        o = lit(o)
+        return Expr(f"({self.dev} {op} {o.dev})", f"({self.orc} {op} {o.orc})")
+
+    def _rbin(self, o, op):
+        return lit(o)._bin(self, op)
+
+    __add__ = lambda s, o: s._bin(o, "+")
+    __radd__ = lambda s, o: s._rbin(o, "+")
+    __sub__ = lambda s, o: s._bin(o, "-")
+    __rsub__ = lambda s, o: s._rbin(o, "-")
+    __mul__ = lambda s, o: s._bin(o, "*")
+    __eq__ = lambda s, o: s._bin(o, "==")
+    __ne__ = lambda s, o: s._bin(o, "!=")
+    __lt__ = lambda s, o: s._bin(o, "<")
+    __le__ = lambda s, o: s._bin(o, "<=")
+    __gt__ = lambda s, o: s._bin(o, ">")
+    __ge__ = lambda s, o: s._bin(o, ">=")
+    __and__ = lambda s, o: s._bin(o, "&&")
+    __or__ = lambda s, o: s._bin(o, "||")
+
+    def __invert__(self):
+        return Expr(f"(!{self.dev})", f"(!{self.orc})")
+
+    def __hash__(self):
+        return id(self)
+
+    def __bool__(self):
+        raise TypeError("IR expressions are symbolic: use h.if_(...) instead of a Python if")
+
+
+def lit(v) -> Expr:
+    if isinstance(v, Expr):
+        return v
+    if isinstance(v, bool):
+        v = int(v)
+    return Expr(str(int(v)), str(int(v)))
+
+
+def select(c, a, b) -> Expr:
+    c, a, b = lit(c), lit(a), lit(b)
+    return Expr(f"({c.dev} ? {a.dev} : {b.dev})", f"({c.orc} ? {a.orc} : {b.orc})")
+
+
+# ---- declarations ------------------------------------------------------------------------------
+@dataclass
+class Param:
+    name: str
+    default: int
+    lo: int
+    hi: int
+
+
+@dataclass
+class RecordType:
+    """A message or timer type: integer fields of fixed widths, in declaration order."""
+    name: str
+    fields: List[Tuple[str, int]]
+    index: int = 0
+    millis: Tuple[int, int] = (0, 0)  # timers: (min, max)
+
+
+@dataclass
+class FieldDecl:
+    name: str
+    bits: int
+    cap: int = 0  # > 0: a bounded list of `cap` elements of `bits` each, with a length
+    off: int = 0
+    len_off: int = 0
+    len_bits: int = 0
+
+
+@dataclass
+class NodeKind:
+    name: str                      # address prefix ("client" -> client1, client2, ...)
+    count: object                  # int, or the name of a Param
+    max_count: int
+    fields: List[FieldDecl] = field(default_factory=list)
+    client: bool = False           # runs inside ClientWorker
+    single_name: Optional[str] = None  # address of a one-instance kind ("pingserver")
+    result_field: str = ""         # client: the field holding the current result (0 = none)
+    timer_cap: int = 0
+    results_cap: int = 0
+    handlers: Dict[str, Callable] = field(default_factory=dict)   # message name -> fn(h)
+    timer_handlers: Dict[str, Callable] = field(default_factory=dict)
+    init_fn: Optional[Callable] = None
+    send_command_fn: Optional[Callable] = None
+    first: int = 0                 # node index of the first instance
+
+    def on(self, msg: RecordType):
+        def deco(fn):
+            self.handlers[msg.name] = fn
+            return fn
+        return deco
+
+    def on_timer(self, t: RecordType):
+        def deco(fn):
+            self.timer_handlers[t.name] = fn
+            return fn
+        return deco
+
+    def init(self, fn):
+        self.init_fn = fn
+        return fn
+
+    def send_command(self, fn):
+        self.send_command_fn = fn
+        return fn
+
+
+class Protocol:
+    def __init__(self, name: str, proto_id: int, cxx_name: str, doc: str = ""):
+        self.name, self.proto_id, self.cxx_name, self.doc = name, proto_id, cxx_name, doc
+        self.params: List[Param] = []
+        self.messages: List[RecordType] = []
+        self.timers: List[RecordType] = []
+        self.kinds: List[NodeKind] = []
+        self.net_cap = 32
+        self.max_sends = 4
+        self.workload_size = ""       # Param name: commands per client
+        self.expected_result: Optional[Callable] = None  # k (1-based Expr) -> expected result Expr
+
+    # declarations
+    def param(self, name: str, default: int, lo: int = 0, hi: int = 1 << 30) -> Param:
+        p = Param(name, default, lo, hi)
+        self.params.append(p)
+        return p
+
+    def message(self, name: str, **fields: int) -> RecordType:
+        r = RecordType(name, list(fields.items()), len(self.messages))
+        self.messages.append(r)
+        return r
+
+    def timer(self, name: str, millis: Tuple[int, int], **fields: int) -> RecordType:
+        r = RecordType(name, list(fields.items()), len(self.timers), millis)
+        self.timers.append(r)
+        return r
+
+    def node(self, name: str, count=1, max_count: int = 1, single_name: Optional[str] = None, **fields: int) -> NodeKind:
+        k = NodeKind(name, count, max_count, [FieldDecl(n, b) for n, b in fields.items()], single_name=single_name)
+        self.kinds.append(k)
+        return k
+
+    def client_worker(self, name: str, count, max_count: int, result: str, results_cap: int, timer_cap: int,
+                      **fields: int) -> NodeKind:
+        k = self.node(name, count, max_count, **fields)
+        k.client, k.result_field, k.results_cap, k.timer_cap = True, result, results_cap, timer_cap
+        return k
+
+    # derived layout ------------------------------------------------------------------------------
+    def layout(self):
+        """Node indices (kinds in declaration order, instances consecutive), node word layout
+        (fields never straddle a 32-bit word), record layout (type, from, to, fields)."""
+        idx = 0
+        for k in self.kinds:
+            k.first = idx
+            idx += k.max_count
+        self.max_nodes = idx
+        words = 1
+        for k in self.kinds:
+            if k.timer_cap and not any(f.name == "_timers" for f in k.fields):
+                k.fields.append(FieldDecl("_timers", self.timer_entry_bits(), k.timer_cap))
+            if k.client and not any(f.name == "_results" for f in k.fields):
+                rb = max(f.bits for f in k.fields if f.name == k.result_field)
+                k.fields.append(FieldDecl("_results", rb, k.results_cap))
+            bit = 0
+
+            def place(width):
+                nonlocal bit
+                if (bit % 32) + width > 32:
+                    bit = (bit // 32 + 1) * 32
+                o = bit
+                bit += width
+                return o
+
+            for f in k.fields:
+                if f.cap:
+                    f.len_bits = max(1, f.cap.bit_length())
+                    f.len_off = place(f.len_bits)
+                    assert f.bits <= 32
+                    f.off = place(f.bits)
+                    for _ in range(f.cap - 1):
+                        place(f.bits)  # consecutive elements (each within one word)
+                else:
+                    f.off = place(f.bits)
+            words = max(words, (bit + 31) // 32)
+        self.node_words = words
+        # records
+        self.type_bits = max(1, (len(self.messages) - 1).bit_length())
+        self.addr_bits = max(1, (self.max_nodes - 1).bit_length())
+        width = self.type_bits + 2 * self.addr_bits + max(sum(b for _, b in m.fields) for m in self.messages)
+        self.rec_bits = 32 if width <= 32 else 64
+        assert width <= 64, "records wider than 64 bits"
+        for m in self.messages:
+            off, offs = 0, []
+            for n, b in m.fields:
+                offs.append((n, b, off))
+                off += b
+            m.offs = offs
+        self.type_off = self.rec_bits - self.type_bits
+        self.from_off = self.type_off - self.addr_bits
+        self.to_off = self.from_off - self.addr_bits
+
+    def timer_entry_bits(self) -> int:
+        tb = max(1, (len(self.timers) - 1).bit_length()) if len(self.timers) > 1 else 0
+        fb = max([sum(b for _, b in t.fields) for t in self.timers] + [0])
+        return tb + fb
+
+    def address_names(self, args: Dict[str, int]) -> List[str]:
+        out = []
+        for k in self.kinds:
+            n = self.count_of(k, args)
+            if k.single_name and k.max_count == 1:
+                out.append(k.single_name)
+            else:
+                out += [f"{k.name}{i}" for i in range(1, n + 1)]
+        return out
+
+    def count_of(self, k: NodeKind, args: Dict[str, int]) -> int:
+        return k.count if isinstance(k.count, int) else int(args[k.count])
+
+
+# ---- handler recorder ---------------------------------------------------------------------------
+class Stmt:
+    pass
+
+
+@dataclass
+class Assign(Stmt):
+    fld: FieldDecl
+    value: Expr
+
+
+@dataclass
+class SendS(Stmt):
+    msg: RecordType
+    to: Expr
+    vals: List[Expr]
+
+
+@dataclass
+class SetTimerS(Stmt):
+    timer: RecordType
+    vals: List[Expr]
+
+
+@dataclass
+class IfS(Stmt):
+    cond: Expr
+    then: List[Stmt]
+    other: List[Stmt]
+
+
+@dataclass
+class ThrowS(Stmt):
+    what: str
+
+
+class _Fields:
+    def __init__(self, h):
+        object.__setattr__(self, "_h", h)
+
+    def __getattr__(self, name):
+        return self._h._field_expr(name)
+
+
+class _Rec:
+    def __init__(self, h, kind):
+        self._h, self._kind = h, kind
+
+    def __getattr__(self, name):
+        return self._h._rec_field(self._kind, name)
+
+
+class Handler:
+    """What a handler function sees: h.f.<field> (the node's fields), h.msg.<field> /
+    h.timer.<field> (the event's fields), h.sender, h.self, h.param(name), and the statements
+    h.set(field, value), h.send(Msg, to, **fields), h.set_timer(Timer, **fields),
+    `with h.if_(cond):` / `with h.else_():`, h.throw(why)."""
+
+    def __init__(self, proto: Protocol, kind: NodeKind, event: Optional[RecordType] = None, is_timer=False,
+                 cmd: Optional[Expr] = None):
+        self.p, self.kind, self.event, self.is_timer = proto, kind, event, is_timer
+        self.stmts: List[Stmt] = []
+        self._stack = [self.stmts]
+        self._last_if: Optional[IfS] = None
+        self.f = _Fields(self)
+        self.msg = _Rec(self, "msg")
+        self.timer = _Rec(self, "timer")
+        self.cmd = cmd
+
+    # expressions
+    def _fd(self, name) -> FieldDecl:
+        for f in self.kind.fields:
+            if f.name == name:
+                return f
+        raise KeyError(f"{self.kind.name} has no field {name}")
+
+    def _field_expr(self, name) -> Expr:
+        f = self._fd(name)
+        assert not f.cap, "lists are read with h.at(field, i)"
+        return Expr(f"get(w, {f.off}, {f.bits})", f"{name}")
+
+    def _rec_field(self, which, name) -> Expr:
+        ev = self.event
+        if ev is None:
+            raise KeyError("no event")
+        for i, (n, b, *rest) in enumerate(getattr(ev, "offs", [(n, b, 0) for n, b in ev.fields])):
+            if n == name:
+                if which == "msg":
+                    off = rest[0]
+                    return Expr(f"(int)((r >> {off}) & {(1 << b) - 1}u)", f"std::stoi(m.f[{i}])")
+                return Expr(f"tf_{name}", f"std::stoi(t.f[{i}])")
+        raise KeyError(f"{ev.name} has no field {name}")
+
+    @property
+    def sender(self) -> Expr:
+        return Expr("rec_from(r)", "from")
+
+    @property
+    def self(self) -> Expr:
+        return Expr("i", "self")
+
+    def param(self, name) -> Expr:
+        return Expr(f"p.{name}", f"prm.{name}")
+
+    def node(self, kind: NodeKind, k=1) -> Expr:
+        """Address of instance k (1-based) of a node kind."""
+        k = lit(k)
+        return Expr(f"({kind.first} + {k.dev} - 1)", f"({kind.first} + {k.orc} - 1)")
+
+    # statements
+    def _emit(self, s: Stmt):
+        self._stack[-1].append(s)
+        if not isinstance(s, IfS):
+            self._last_if = None
+
+    def set(self, name: str, value):
+        self._emit(Assign(self._fd(name), lit(value)))
+
+    def send(self, msg: RecordType, to, **vals):
+        self._emit(SendS(msg, lit(to), [lit(vals[n]) for n, _ in msg.fields]))
+
+    def set_timer(self, t: RecordType, **vals):
+        self._emit(SetTimerS(t, [lit(vals[n]) for n, _ in t.fields]))
+
+    def throw(self, why: str):
+        self._emit(ThrowS(why))
+
+    def if_(self, cond):
+        h = self
+        s = IfS(lit(cond), [], [])
+
+        class _Ctx:
+            def __enter__(self_):
+                h._emit(s)
+                h._stack.append(s.then)
+
+            def __exit__(self_, *a):
+                h._stack.pop()
+                h._last_if = s
+        return _Ctx()
+
+    def else_(self):
+        h = self
+        s = self._last_if
+        assert s is not None, "else_ must follow an if_ block"
+
+        class _Ctx:
+            def __enter__(self_):
+                h._stack.append(s.other)
+
+            def __exit__(self_, *a):
+                h._stack.pop()
+                h._last_if = None
+        return _Ctx()
+
+
+def record(proto: Protocol, kind: NodeKind, fn: Callable, event=None, is_timer=False, cmd=None) -> List[Stmt]:
+    h = Handler(proto, kind, event, is_timer, cmd)
+    if cmd is not None:
+        fn(h, cmd)
+    else:
+        fn(h)
+    return h.stmts

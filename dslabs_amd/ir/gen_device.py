@@ -1,0 +1,344 @@
+"""IR -> packed device protocol (a csrc/protocols/*.hpp struct with the interface nodestate.hpp
+and the kernels use: layout constants, Params, record encoding, init / events / handlers,
+ClientWorker loop, predicates, event descriptions). Every field access is a constant-offset
+bit-field access (field_get / field_put); list elements use select chains, so nothing here is a
+dynamically indexed private array."""
+from __future__ import annotations
+
+from typing import List
+
+from .core import Assign, Expr, IfS, NodeKind, Protocol, SendS, SetTimerS, Stmt, ThrowS, lit, record
+
+
+def _ind(n):
+    return "  " * n
+
+
+def _rec_expr(p: Protocol, s: SendS) -> str:
+    parts = [f"((Rec){s.msg.index} << {p.type_off})", f"((Rec)(i) << {p.from_off})",
+             f"((Rec)({s.to.dev}) << {p.to_off})"]
+    for (n, b, off), v in zip(s.msg.offs, s.vals):
+        parts.append(f"((Rec)(({v.dev}) & {(1 << b) - 1}) << {off})")
+    return " | ".join(parts)
+
+
+def _timer_entry(p: Protocol, t, vals: List[Expr]) -> str:
+    parts, off = [], 0
+    for (n, b), v in zip(t.fields, vals):
+        parts.append(f"((({v.dev}) & {(1 << b) - 1}) << {off})")
+        off += b
+    fb = max([sum(b for _, b in x.fields) for x in p.timers] + [0])
+    if len(p.timers) > 1:
+        parts.append(f"({t.index} << {fb})")
+    return " | ".join(parts) if parts else "0"
+
+
+def _stmts(p: Protocol, k: NodeKind, ss: List[Stmt], d: int) -> List[str]:
+    out = []
+    for s in ss:
+        if isinstance(s, Assign):
+            out.append(f"{_ind(d)}put(w, {s.fld.off}, {s.fld.bits}, {s.value.dev});")
+        elif isinstance(s, SendS):
+            out.append(f"{_ind(d)}out.send({_rec_expr(p, s)});")
+        elif isinstance(s, SetTimerS):
+            tf = next(f for f in k.fields if f.name == "_timers")
+            out.append(f"{_ind(d)}push_timer_{k.name}(w, {_timer_entry(p, s.timer, s.vals)}, out);")
+        elif isinstance(s, ThrowS):
+            out.append(f"{_ind(d)}return STEP_EXCEPTION;  // {s.what}")
+        elif isinstance(s, IfS):
+            out.append(f"{_ind(d)}if ({s.cond.dev}) {{")
+            out += _stmts(p, k, s.then, d + 1)
+            if s.other:
+                out.append(f"{_ind(d)}}} else {{")
+                out += _stmts(p, k, s.other, d + 1)
+            out.append(f"{_ind(d)}}}")
+    return out
+
+
+def generate(p: Protocol, source: str) -> str:
+    p.layout()
+    N = p.cxx_name
+    rec_t = "uint32_t" if p.rec_bits == 32 else "uint64_t"
+    L = []
+    a = L.append
+    a(f"// {N} -- GENERATED from the protocol IR ({source}) by dslabs_amd/ir/gen_device.py; do not edit.")
+    for line in p.doc.strip().splitlines():
+        a(f"// {line}")
+    a("#pragma once")
+    a('#include "../../nodestate.hpp"')
+    a("")
+    a("namespace dsl {")
+    a("")
+    a(f"struct {N} {{")
+    a(f"  static constexpr int kNodes = {p.max_nodes}, kNodeWords = {p.node_words}, kNetCap = {p.net_cap}, "
+      f"kMaxSends = {p.max_sends};")
+    a(f"  static constexpr int kMsgClasses = {len(p.messages)};")
+    a(f"  using Rec = {rec_t};")
+    a(f"  using State = StateOf<{N}>;")
+    a("  struct Params {")
+    for q in p.params:
+        a(f"    int32_t {q.name};")
+    a("  };")
+    a("  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }")
+    a("  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }")
+    am = (1 << p.addr_bits) - 1
+    a(f"  static DSL_HD int rec_type(Rec r) {{ return (int)(r >> {p.type_off}); }}")
+    a(f"  static DSL_HD int rec_from(Rec r) {{ return (int)((r >> {p.from_off}) & {am}); }}")
+    a(f"  static DSL_HD int rec_to(Rec r) {{ return (int)((r >> {p.to_off}) & {am}); }}")
+    a("  static DSL_HD int msg_class(Rec r) { return rec_type(r); }")
+    # node kinds
+    a("  // node index -> kind: kinds are laid out in declaration order, instances consecutive")
+    cnt = lambda k: str(k.count) if isinstance(k.count, int) else f"p.{k.count}"
+    a("  static DSL_HD int num_nodes(const Params& p) { return " + " + ".join(cnt(k) for k in p.kinds) + "; }")
+    for ki, k in enumerate(p.kinds):
+        first = " + ".join(["0"] + [cnt(x) for x in p.kinds[:ki]])
+        a(f"  static DSL_HD int first_{k.name}(const Params& p) {{ (void)p; return {first}; }}")
+        a(f"  static DSL_HD bool is_{k.name}(int i, const Params& p) {{ return i >= first_{k.name}(p) && "
+          f"i < first_{k.name}(p) + {cnt(k)}; }}")
+    # timer queues
+    fb = max([sum(b for _, b in t.fields) for t in p.timers] + [0])
+    a("  // timer entries: fields from bit 0 in declaration order, the type above them")
+    a("  static DSL_HD void tbounds(int type, int& mn, int& mx) {")
+    for t in p.timers:
+        a(f"    if (type == {t.index}) {{ mn = {t.millis[0]}; mx = {t.millis[1]}; }}")
+    a("  }")
+    a(f"  static DSL_HD int ttype(int e) {{ return {'e >> ' + str(fb) if len(p.timers) > 1 else '0'}; }}")
+    for k in p.kinds:
+        if not k.timer_cap:
+            continue
+        tf = next(f for f in k.fields if f.name == "_timers")
+        a(f"  template <class O>")
+        a(f"  static DSL_HD void push_timer_{k.name}(uint32_t* w, int e, O& out) {{")
+        a(f"    const int n = get(w, {tf.len_off}, {tf.len_bits});")
+        a(f"    if (n >= {tf.cap}) {{ out.overflow = true; return; }}")
+        a(f"    put(w, {tf.off} + {tf.bits} * n, {tf.bits}, e);")
+        a(f"    put(w, {tf.len_off}, {tf.len_bits}, n + 1);")
+        a("  }")
+        # deliverable entries (TimerQueue.deliverable): yield in order; skip min >= min(max yielded)
+        a(f"  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)")
+        a(f"  static DSL_HD int deliverable_{k.name}(const uint32_t* w, int j) {{")
+        a(f"    const int n = get(w, {tf.len_off}, {tf.len_bits});")
+        a("    int mm = 0x7fffffff, c = 0;")
+        a(f"    for (int q = 0; q < n; q++) {{")
+        a(f"      int mn = 0, mx = 0;")
+        a(f"      tbounds(ttype(get(w, {tf.off} + {tf.bits} * q, {tf.bits})), mn, mx);")
+        a("      if (q > 0 && mn >= mm) continue;")
+        a("      if (c == j) return q;")
+        a("      c++;")
+        a("      if (mx < mm) mm = mx;")
+        a("    }")
+        a("    return j < 0 ? c : -1;")
+        a("  }")
+        a(f"  static DSL_HD void remove_timer_{k.name}(uint32_t* w, int e) {{  // the first equal entry")
+        a(f"    const int n = get(w, {tf.len_off}, {tf.len_bits});")
+        a("    int q0 = n;")
+        a(f"    for (int q = n - 1; q >= 0; q--)")
+        a(f"      if (get(w, {tf.off} + {tf.bits} * q, {tf.bits}) == e) q0 = q;")
+        a("    if (q0 >= n) return;")
+        a(f"    for (int q = q0; q + 1 < n; q++) put(w, {tf.off} + {tf.bits} * q, {tf.bits}, "
+          f"get(w, {tf.off} + {tf.bits} * (q + 1), {tf.bits}));")
+        a(f"    put(w, {tf.off} + {tf.bits} * (n - 1), {tf.bits}, 0);")
+        a(f"    put(w, {tf.len_off}, {tf.len_bits}, n - 1);")
+        a("  }")
+    # client worker
+    from .core import Expr as E
+    for k in p.kinds:
+        if not k.client:
+            continue
+        rf = next(f for f in k.fields if f.name == k.result_field)
+        rl = next(f for f in k.fields if f.name == "_results")
+        body = record(p, k, k.send_command_fn, cmd=E("cmd", "cmd"))
+        a("  template <class O>")
+        a(f"  static DSL_HD void send_command_{k.name}(int i, uint32_t* w, int cmd, O& out, const Params& p) {{")
+        a("    (void)p;")
+        L.extend(_stmts(p, k, body, 2))
+        a("  }")
+        a("  // ClientWorker.sendNextCommandWhilePossible (waitingOnResult == |results| < workload size)")
+        a("  template <class O>")
+        a(f"  static DSL_HD void client_worker_{k.name}(int i, uint32_t* w, O& out, const Params& p) {{")
+        a(f"    int n = get(w, {rl.len_off}, {rl.len_bits});")
+        a(f"    const int res = get(w, {rf.off}, {rf.bits});")
+        a(f"    if (n < p.{p.workload_size} && res != 0) {{")
+        a(f"      if (n >= {rl.cap}) {{ out.overflow = true; return; }}")
+        a(f"      put(w, {rl.off} + {rl.bits} * n, {rl.bits}, res);")
+        a("      n++;")
+        a(f"      put(w, {rl.len_off}, {rl.len_bits}, n);")
+        a(f"      if (n < p.{p.workload_size}) send_command_{k.name}(i, w, n + 1, out, p);")
+        a("    }")
+        a("  }")
+    # init
+    a("  template <class O>")
+    a("  static DSL_HD void init_node(int i, uint32_t* w, O& out, const Params& p) {")
+    for k in p.kinds:
+        a(f"    if (is_{k.name}(i, p)) {{")
+        if k.init_fn:
+            L.extend(_stmts(p, k, record(p, k, k.init_fn), 3))
+        if k.client:  # ClientWorker.init: the first command
+            a(f"      if (p.{p.workload_size} > 0) send_command_{k.name}(i, w, 1, out, p);")
+        a("      return;")
+        a("    }")
+    a("  }")
+    a("  static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {")
+    for k in p.kinds:
+        if k.timer_cap:
+            a(f"    if (is_{k.name}(i, p)) return deliverable_{k.name}(w, -1);")
+    a("    (void)i; (void)w; (void)p;")
+    a("    return 0;")
+    a("  }")
+    # message handlers
+    a("  template <class O>")
+    a("  static DSL_HD int on_message(int i, uint32_t* w, Rec r, O& out, const Params& p) {")
+    a("    (void)w; (void)out;")
+    for k in p.kinds:
+        a(f"    if (is_{k.name}(i, p)) {{")
+        for m in p.messages:
+            fn = k.handlers.get(m.name)
+            if fn is None:
+                continue
+            a(f"      if (rec_type(r) == {m.index}) {{  // {m.name}")
+            L.extend(_stmts(p, k, record(p, k, fn, event=m), 4))
+            if k.client:
+                a(f"        client_worker_{k.name}(i, w, out, p);")
+            a("        return STEP_OK;")
+            a("      }")
+        a("      return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)")
+        a("    }")
+    a("    return STEP_EXCEPTION;")
+    a("  }")
+    # timer handlers
+    a("  template <class O>")
+    a("  static DSL_HD int on_timer(int i, uint32_t* w, int j, O& out, const Params& p) {")
+    a("    (void)w; (void)j; (void)out;")
+    for k in p.kinds:
+        if not k.timer_cap:
+            continue
+        tf = next(f for f in k.fields if f.name == "_timers")
+        a(f"    if (is_{k.name}(i, p)) {{")
+        a(f"      const int q = deliverable_{k.name}(w, j);")
+        a("      if (q < 0) return STEP_NULL;")
+        a(f"      const int e = get(w, {tf.off} + {tf.bits} * q, {tf.bits});")
+        for t in p.timers:
+            fn = k.timer_handlers.get(t.name)
+            if fn is None:
+                continue
+            a(f"      if (ttype(e) == {t.index}) {{  // {t.name}")
+            off = 0
+            for n, b in t.fields:
+                a(f"        const int tf_{n} = (e >> {off}) & {(1 << b) - 1};")
+                off += b
+            L.extend(_stmts(p, k, record(p, k, fn, event=t, is_timer=True), 4))
+            if k.client:
+                a(f"        client_worker_{k.name}(i, w, out, p);")
+            a(f"        remove_timer_{k.name}(w, e);  // SearchState.stepTimer: the first equal entry")
+            a("        return STEP_OK;")
+            a("      }")
+        a("      return STEP_EXCEPTION;  // no handler for this timer")
+        a("    }")
+    a("    return STEP_EXCEPTION;")
+    a("  }")
+    # predicates (ClientWorker)
+    ck = [k for k in p.kinds if k.client]
+    a("  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const Params& p) {")
+    if ck:
+        k = ck[0]
+        rl = next(f for f in k.fields if f.name == "_results")
+        exp = p.expected_result(E("(j + 1)", "(j + 1)")).dev
+        fc, nc = f"first_{k.name}(p)", cnt(k)
+        a(f"    const int c0 = {fc}, nc = {nc};")
+        a("    switch (pr.id) {")
+        a("      case DSL_PRED_RESULTS_OK:  // every result equals the workload's expected result")
+        a("        for (int c = c0; c < c0 + nc; c++) {")
+        a("          const uint32_t* w = v.node(c);")
+        a(f"          const int n = get(w, {rl.len_off}, {rl.len_bits});")
+        a(f"          for (int j = 0; j < n; j++)")
+        a(f"            if (get(w, {rl.off} + {rl.bits} * j, {rl.bits}) != {exp}) return PV_FALSE;")
+        a("        }")
+        a("        return PV_TRUE;")
+        a("      case DSL_PRED_CLIENTS_DONE:")
+        a("        for (int c = c0; c < c0 + nc; c++)")
+        a(f"          if (get(v.node(c), {rl.len_off}, {rl.len_bits}) < p.{p.workload_size}) return PV_FALSE;")
+        a("        return PV_TRUE;")
+        a("      case DSL_PRED_CLIENT_DONE:")
+        a("        if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;")
+        a(f"        return get(v.node((int)pr.arg0), {rl.len_off}, {rl.len_bits}) >= p.{p.workload_size} ? PV_TRUE : PV_FALSE;")
+        a("      case DSL_PRED_NONE_DECIDED:")
+        a("        for (int c = c0; c < c0 + nc; c++)")
+        a(f"          if (get(v.node(c), {rl.len_off}, {rl.len_bits}) > 0) return PV_FALSE;")
+        a("        return PV_TRUE;")
+        a("      case DSL_PRED_CLIENT_HAS_RESULTS:")
+        a("        if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;")
+        a(f"        return get(v.node((int)pr.arg0), {rl.len_off}, {rl.len_bits}) == pr.arg1 ? PV_TRUE : PV_FALSE;")
+        a("      default:")
+        a("        return PV_THREW;")
+        a("    }")
+    else:
+        a("    (void)pr; (void)v; (void)p;")
+        a("    return PV_THREW;")
+    a("  }")
+    a("  static uint32_t pred_reads(const DevPred& pr, const Params& p) {")
+    if ck:
+        k = ck[0]
+        a(f"    const uint32_t clients = ((1u << ({cnt(k)})) - 1u) << first_{k.name}(p);")
+        a("    return (pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) ? clients : kReadsAll;")
+    else:
+        a("    (void)pr; (void)p;")
+        a("    return kReadsAll;")
+    a("  }")
+    a("  static bool known_predicate(int id) { return id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS; }")
+    a("  static bool valid(const Params& p) {")
+    conds = [f"p.{q.name} >= {q.lo} && p.{q.name} <= {q.hi}" for q in p.params]
+    for k in p.kinds:
+        if not isinstance(k.count, int):
+            conds.append(f"p.{k.count} >= 1 && p.{k.count} <= {k.max_count}")
+    a("    return " + (" &&\n           ".join(conds) if conds else "true") + ";")
+    a("  }")
+    a("  static Params from_desc(const dsl_protocol_desc& d) {")
+    a("    Params p{};")
+    for qi, q in enumerate(p.params):
+        a(f"    p.{q.name} = d.n_params > {qi} ? (int32_t)d.params[{qi}] : {q.default};")
+    a("    return p;")
+    a("  }")
+    # descriptions
+    a("  static void describe_message(Rec r, dsl_event* e) {")
+    a("    e->from = rec_from(r);")
+    a("    e->to = rec_to(r);")
+    a("    e->type = rec_type(r);")
+    a("    e->n_fields = 0;")
+    for m in p.messages:
+        a(f"    if (e->type == {m.index}) {{")
+        a(f"      e->n_fields = {len(m.fields)};")
+        for fi, (n, b, off) in enumerate(m.offs):
+            a(f"      e->fields[{fi}] = (int64_t)((r >> {off}) & {(1 << b) - 1}u);")
+        a("    }")
+    a("  }")
+    a("  static void describe_timer(int i, const uint32_t* w, int j, const Params& p, dsl_event* e) {")
+    a("    e->is_timer = 1;")
+    a("    e->from = e->to = i;")
+    a("    (void)w; (void)j; (void)p;")
+    for k in p.kinds:
+        if not k.timer_cap:
+            continue
+        tf = next(f for f in k.fields if f.name == "_timers")
+        a(f"    if (is_{k.name}(i, p)) {{")
+        a(f"      const int q = deliverable_{k.name}(w, j);")
+        a("      if (q < 0) return;")
+        a(f"      const int x = get(w, {tf.off} + {tf.bits} * q, {tf.bits});")
+        a(f"      e->type = {len(p.messages)} + ttype(x);")
+        a("      int mn = 0, mx = 0;")
+        a("      tbounds(ttype(x), mn, mx);")
+        a("      e->timer_min = mn;")
+        a("      e->timer_max = mx;")
+        for t in p.timers:
+            a(f"      if (ttype(x) == {t.index}) {{")
+            a(f"        e->n_fields = {len(t.fields)};")
+            off = 0
+            for fi, (n, b) in enumerate(t.fields):
+                a(f"        e->fields[{fi}] = (x >> {off}) & {(1 << b) - 1};")
+                off += b
+            a("      }")
+        a("    }")
+    a("  }")
+    a("};")
+    a("")
+    a("}  // namespace dsl")
+    return "\n".join(L) + "\n"

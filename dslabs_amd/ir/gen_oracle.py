@@ -1,0 +1,155 @@
+"""IR -> object form on the oracle's model (oracle/oracle_core.hpp: Node / Client, Ctx, TimerQueue,
+ClientWorker, Workload). Fields become int members, messages and timers Rec{type, decimal fields};
+handlers the same statements over those members. TEST INFRASTRUCTURE: the generated header is part
+of oracle/ and is only built into the oracle binary."""
+from __future__ import annotations
+
+from typing import List
+
+from .core import Assign, Expr, IfS, NodeKind, Protocol, SendS, SetTimerS, Stmt, ThrowS, record
+
+
+def _ind(n):
+    return "  " * n
+
+
+def _rec(t, vals: List[Expr]) -> str:
+    return "Rec{\"" + t.name + "\", {" + ", ".join(f"std::to_string({v.orc})" for v in vals) + "}}"
+
+
+def _stmts(p: Protocol, k: NodeKind, ss: List[Stmt], d: int) -> List[str]:
+    out = []
+    for s in ss:
+        if isinstance(s, Assign):
+            out.append(f"{_ind(d)}{s.fld.name} = {s.value.orc};")
+        elif isinstance(s, SendS):
+            out.append(f"{_ind(d)}ctx.send({_rec(s.msg, s.vals)}, {s.to.orc});")
+        elif isinstance(s, SetTimerS):
+            out.append(f"{_ind(d)}ctx.set({_rec(s.timer, s.vals)}, {s.timer.millis[0]}, {s.timer.millis[1]});")
+        elif isinstance(s, ThrowS):
+            out.append(f"{_ind(d)}throw HandlerException(\"{s.what}\");")
+        elif isinstance(s, IfS):
+            out.append(f"{_ind(d)}if ({s.cond.orc}) {{")
+            out += _stmts(p, k, s.then, d + 1)
+            if s.other:
+                out.append(f"{_ind(d)}}} else {{")
+                out += _stmts(p, k, s.other, d + 1)
+            out.append(f"{_ind(d)}}}")
+    return out
+
+
+def generate(p: Protocol, source: str) -> str:
+    p.layout()
+    ns = p.name
+    L = []
+    a = L.append
+    a(f"// GENERATED from the protocol IR ({source}) by dslabs_amd/ir/gen_oracle.py; do not edit.")
+    a("// oracle/ -- TEST INFRASTRUCTURE ONLY (see oracle_core.hpp).")
+    a("#pragma once")
+    a('#include "../oracle_core.hpp"')
+    a("")
+    a("namespace oracle {")
+    a(f"namespace {ns} {{")
+    a("")
+    a("struct Params {")
+    for q in p.params:
+        a(f"  int {q.name} = {q.default};")
+    a("};")
+    a("")
+    for k in p.kinds:
+        user = [f for f in k.fields if not f.name.startswith("_")]
+        base = "Client" if k.client else "Node"
+        cls = "N_" + k.name
+        a(f"struct {cls} : {base} {{")
+        a("  Params prm;")
+        a("  int self = 0;")
+        for f in user:
+            a(f"  int {f.name} = 0;")
+        a(f"  std::shared_ptr<Node> clone() const override {{ return std::make_shared<{cls}>(*this); }}")
+        a("  void key(std::string& out) const override {")
+        a(f"    out += \"{k.name}{{\";")
+        for f in user:
+            a(f"    out += std::to_string({f.name}) + \",\";")
+        a("    out += \"}\";")
+        a("  }")
+        a("  std::string str() const override {")
+        parts = " + \", \" + ".join([f"\"{f.name}=\" + std::to_string({f.name})" for f in user]) or "std::string()"
+        a(f"    return std::string(\"{k.name}(\") + {parts} + \")\";")
+        a("  }")
+        if k.init_fn:
+            a("  void init(Ctx& ctx) override {")
+            L.extend(_stmts(p, k, record(p, k, k.init_fn), 2))
+            a("  }")
+        a("  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {")
+        a("    (void)from; (void)ctx;")
+        for msg in p.messages:
+            fn = k.handlers.get(msg.name)
+            if fn is None:
+                continue
+            a(f"    if (m.type == \"{msg.name}\") {{")
+            L.extend(_stmts(p, k, record(p, k, fn, event=msg), 3))
+            a("      return;")
+            a("    }")
+        a("    throw HandlerException(\"no handler\");")
+        a("  }")
+        a("  void onTimer(const Rec& t, Ctx& ctx) override {")
+        a("    (void)ctx;")
+        for t in p.timers:
+            fn = k.timer_handlers.get(t.name)
+            if fn is None:
+                continue
+            a(f"    if (t.type == \"{t.name}\") {{")
+            L.extend(_stmts(p, k, record(p, k, fn, event=t, is_timer=True), 3))
+            a("      return;")
+            a("    }")
+        a("    throw HandlerException(\"no timer handler\");")
+        a("  }")
+        if k.client:
+            a("  void sendCommand(const Rec& c, Ctx& ctx) override {")
+            a("    const int cmd = std::stoi(c.f[0]);")
+            L.extend(_stmts(p, k, record(p, k, k.send_command_fn, cmd=Expr("cmd", "cmd")), 2))
+            a("  }")
+            a(f"  bool hasResult() const override {{ return {k.result_field} != 0; }}")
+            a(f"  Rec getResult() const override {{ return Rec{{\"Result\", {{std::to_string({k.result_field})}}}}; }}")
+        a("};")
+        a("")
+    # initial state
+    a("// Addresses: node kinds in declaration order, instances consecutive.")
+    a("inline std::shared_ptr<State> initial(const Params& prm, Names& names) {")
+    a("  std::vector<std::shared_ptr<Node>> nodes;")
+    a("  std::vector<Kind> kinds;")
+    for k in p.kinds:
+        cls = "N_" + k.name
+        count = str(k.count) if isinstance(k.count, int) else f"prm.{k.count}"
+        a(f"  for (int c = 1; c <= {count}; c++) {{")
+        if k.single_name and k.max_count == 1:
+            a(f"    names.addr.push_back(\"{k.single_name}\");")
+        else:
+            a(f"    names.addr.push_back(\"{k.name}\" + std::to_string(c));")
+        a(f"    auto n = std::make_shared<{cls}>();")
+        a("    n->prm = prm;")
+        a("    n->self = (int)nodes.size();")
+        if k.client:
+            exp = p.expected_result(Expr("k", "k")).orc
+            a("    auto cw = std::make_shared<ClientWorker>();")
+            a("    cw->client = n;")
+            a("    cw->addrName = names.addr.back();")
+            a("    cw->workload.cmds = {\"%i\"};")
+            a("    cw->workload.results = {\"%i\"};")
+            a(f"    cw->workload.numTimes = prm.{p.workload_size};")
+            a("    cw->workload.parser = [](const std::string& c, const std::string& r) {")
+            a("      const int k = std::stoi(r);")
+            a(f"      return std::make_pair(Rec{{\"Command\", {{c}}}}, Rec{{\"Result\", {{std::to_string({exp})}}}});")
+            a("    };")
+            a("    nodes.push_back(cw);")
+            a("    kinds.push_back(Kind::ClientWorker);")
+        else:
+            a("    nodes.push_back(n);")
+            a("    kinds.push_back(Kind::Server);")
+        a("  }")
+    a("  return makeInitial(nodes, kinds);")
+    a("}")
+    a("")
+    a(f"}}  // namespace {ns}")
+    a("}  // namespace oracle")
+    return "\n".join(L) + "\n"

@@ -643,3 +643,38 @@ class MiniTest(Protocol):
         e.to = self.address_index(to)
         e.type = {"Foo": 0, "Bar": 1}[name]
         return e
+
+
+class IRProtocol(Protocol):
+    """A protocol generated from the protocol IR (dslabs_amd/ir/specs/<spec>.py; device form
+    csrc/protocols/gen/, oracle form oracle/gen/). Parameters by the spec's names; events render
+    as the oracle's object form does (integer fields)."""
+
+    def __init__(self, spec: str, **params):
+        import importlib
+        self.spec = importlib.import_module(f"dslabs_amd.ir.specs.{spec}").P
+        self.proto_id = self.spec.proto_id
+        known = {p.name for p in self.spec.params}
+        bad = set(params) - known
+        if bad:
+            raise ValueError(f"unknown parameters {sorted(bad)} for {spec}")
+        self.values = {p.name: int(params.get(p.name, p.default)) for p in self.spec.params}
+        self.addresses = self.spec.address_names(self.values)
+
+    def params(self):
+        return [self.values[p.name] for p in self.spec.params]
+
+    def render_event(self, e) -> str:
+        a = self.addresses
+        fields = ", ".join(str(e.fields[i]) for i in range(e.n_fields))
+        if e.is_timer:
+            return f"Timer(-> {a[e.to]}, {self.spec.timers[e.type - len(self.spec.messages)].name}({fields}))"
+        return f"Message({a[e.from_]} -> {a[e.to]}, {self.spec.messages[e.type].name}({fields}))"
+
+
+class PingPongIR(IRProtocol):
+    """lab0 PingPong generated from the protocol IR (dslabs_amd/ir/specs/pingpong.py)."""
+
+    def __init__(self, clients: int = 1, pings: int = 10, check_value: bool = True, reset_timer: bool = True):
+        super().__init__("pingpong", clients=clients, pings=pings, check_value=int(check_value),
+                         reset_timer=int(reset_timer))

@@ -25,6 +25,7 @@
 #include "proto_pingpong.hpp"
 #include "proto_sipaxos.hpp"
 #include "proto_synthetic.hpp"
+#include "gen/proto_pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
 
 using namespace oracle;
 
@@ -97,6 +98,18 @@ static Scenario build(const Args& a) {
   if (a.proto == "pingpong") {
     sc.init = pingpong::initial(a.geti("clients", 1), a.geti("pings", 10), !a.has("mutant-no-check"),
                                 !a.has("mutant-no-reset"), sc.names);
+    sc.pred = [common](const std::string& n) {
+      auto p = common(n);
+      if (!p) throw std::runtime_error("unknown predicate " + n);
+      return *p;
+    };
+  } else if (a.proto == "pingpong_ir") {  // the same protocol, generated from the IR
+    pingpong_ir::Params prm;
+    prm.clients = a.geti("clients", 1);
+    prm.pings = a.geti("pings", 10);
+    prm.check_value = a.has("mutant-no-check") ? 0 : 1;
+    prm.reset_timer = a.has("mutant-no-reset") ? 0 : 1;
+    sc.init = pingpong_ir::initial(prm, sc.names);
     sc.pred = [common](const std::string& n) {
       auto p = common(n);
       if (!p) throw std::runtime_error("unknown predicate " + n);

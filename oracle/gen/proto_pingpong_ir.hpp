@@ -1,0 +1,124 @@
+// GENERATED from the protocol IR (dslabs_amd/ir/specs/pingpong.py) by dslabs_amd/ir/gen_oracle.py; do not edit.
+// oracle/ -- TEST INFRASTRUCTURE ONLY (see oracle_core.hpp).
+#pragma once
+#include "../oracle_core.hpp"
+
+namespace oracle {
+namespace pingpong_ir {
+
+struct Params {
+  int clients = 1;
+  int pings = 10;
+  int check_value = 1;
+  int reset_timer = 1;
+};
+
+struct N_pingserver : Node {
+  Params prm;
+  int self = 0;
+  std::shared_ptr<Node> clone() const override { return std::make_shared<N_pingserver>(*this); }
+  void key(std::string& out) const override {
+    out += "pingserver{";
+    out += "}";
+  }
+  std::string str() const override {
+    return std::string("pingserver(") + std::string() + ")";
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    (void)from; (void)ctx;
+    if (m.type == "PingRequest") {
+      ctx.send(Rec{"PongReply", {std::to_string(std::stoi(m.f[0]))}}, from);
+      return;
+    }
+    throw HandlerException("no handler");
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    (void)ctx;
+    throw HandlerException("no timer handler");
+  }
+};
+
+struct N_client : Client {
+  Params prm;
+  int self = 0;
+  int ping = 0;
+  int pong = 0;
+  std::shared_ptr<Node> clone() const override { return std::make_shared<N_client>(*this); }
+  void key(std::string& out) const override {
+    out += "client{";
+    out += std::to_string(ping) + ",";
+    out += std::to_string(pong) + ",";
+    out += "}";
+  }
+  std::string str() const override {
+    return std::string("client(") + "ping=" + std::to_string(ping) + ", " + "pong=" + std::to_string(pong) + ")";
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    (void)from; (void)ctx;
+    if (m.type == "PongReply") {
+      if (((prm.check_value == 0) || (ping == std::stoi(m.f[0])))) {
+        pong = std::stoi(m.f[0]);
+      }
+      return;
+    }
+    throw HandlerException("no handler");
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    (void)ctx;
+    if (t.type == "PingTimer") {
+      if (((ping == std::stoi(t.f[0])) && (pong == 0))) {
+        ctx.send(Rec{"PingRequest", {std::to_string(std::stoi(t.f[0]))}}, (0 + 1 - 1));
+        if ((prm.reset_timer != 0)) {
+          ctx.set(Rec{"PingTimer", {std::to_string(std::stoi(t.f[0]))}}, 10, 10);
+        }
+      }
+      return;
+    }
+    throw HandlerException("no timer handler");
+  }
+  void sendCommand(const Rec& c, Ctx& ctx) override {
+    const int cmd = std::stoi(c.f[0]);
+    ping = cmd;
+    pong = 0;
+    ctx.send(Rec{"PingRequest", {std::to_string(cmd)}}, (0 + 1 - 1));
+    ctx.set(Rec{"PingTimer", {std::to_string(cmd)}}, 10, 10);
+  }
+  bool hasResult() const override { return pong != 0; }
+  Rec getResult() const override { return Rec{"Result", {std::to_string(pong)}}; }
+};
+
+// Addresses: node kinds in declaration order, instances consecutive.
+inline std::shared_ptr<State> initial(const Params& prm, Names& names) {
+  std::vector<std::shared_ptr<Node>> nodes;
+  std::vector<Kind> kinds;
+  for (int c = 1; c <= 1; c++) {
+    names.addr.push_back("pingserver");
+    auto n = std::make_shared<N_pingserver>();
+    n->prm = prm;
+    n->self = (int)nodes.size();
+    nodes.push_back(n);
+    kinds.push_back(Kind::Server);
+  }
+  for (int c = 1; c <= prm.clients; c++) {
+    names.addr.push_back("client" + std::to_string(c));
+    auto n = std::make_shared<N_client>();
+    n->prm = prm;
+    n->self = (int)nodes.size();
+    auto cw = std::make_shared<ClientWorker>();
+    cw->client = n;
+    cw->addrName = names.addr.back();
+    cw->workload.cmds = {"%i"};
+    cw->workload.results = {"%i"};
+    cw->workload.numTimes = prm.pings;
+    cw->workload.parser = [](const std::string& c, const std::string& r) {
+      const int k = std::stoi(r);
+      return std::make_pair(Rec{"Command", {c}}, Rec{"Result", {std::to_string(k)}});
+    };
+    nodes.push_back(cw);
+    kinds.push_back(Kind::ClientWorker);
+  }
+  return makeInitial(nodes, kinds);
+}
+
+}  // namespace pingpong_ir
+}  // namespace oracle

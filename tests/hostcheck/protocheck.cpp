@@ -323,6 +323,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_AMOKV: return run<AmoKV>(d, set);
     case DSL_PROTO_PB: return run<PB>(d, set);
     case DSL_PROTO_MINITEST: return run<MiniTest>(d, set);
+    case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, set);
   }
   return 2;
 }

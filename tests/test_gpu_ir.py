@@ -1,0 +1,42 @@
+"""The IR-generated PingPong (dslabs_amd/ir/specs/pingpong.py -> csrc/protocols/gen/pingpong_ir.hpp)
+on the MI355X engine: the hand-written protocol's golden vectors, and counterexample traces that
+replay on the IR-generated oracle form."""
+import json
+import os
+
+import pytest
+
+import argmap
+import oracle_util
+from dslabs_amd import EndCondition, Engine
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+LAB0 = json.load(open(os.path.join(HERE, "golden", "lab0.json")))
+NAMES = sorted(n for n in LAB0 if "--finish-level" in LAB0[n]["args"] or LAB0[n]["end"] == "SPACE_EXHAUSTED")
+
+
+def _ir(args):
+    return ["pingpong_ir" if a == "pingpong" else a for a in args]
+
+
+@pytest.mark.parametrize("shards", [0, 3])
+@pytest.mark.parametrize("name", NAMES)
+def test_ir_pingpong_matches_golden(name, shards):
+    case = LAB0[name]
+    args = _ir(case["args"])
+    proto = argmap.protocol(args)
+    e = Engine(proto, virtual_shards=shards, replicate_below=0 if shards else -1)
+    try:
+        r = e.bfs(proto.initial_state(), argmap.settings(args, proto, table_log2=20))
+    finally:
+        e.close()
+    assert r.endCondition().name == case["end"]
+    assert r.per_depth == case["per_depth"]
+    st = r.invariantViolatingState() or r.goalMatchingState()
+    if st is not None:
+        rep = oracle_util.replay([a for a in args if a != "--finish-level"], st.trace())
+        assert rep["ok"], rep["error"]
+        assert rep["depth"] == st.depth()
+        if r.endCondition() == EndCondition.INVARIANT_VIOLATED:
+            assert not all(i["value"] for i in rep["invariants"])

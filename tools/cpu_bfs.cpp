@@ -224,6 +224,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_AMOKV: return run<AmoKV>(d, s, threads, log2, repeat);
     case DSL_PROTO_PB: return run<PB>(d, s, threads, log2, repeat);
     case DSL_PROTO_MINITEST: return run<MiniTest>(d, s, threads, log2, repeat);
+    case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, s, threads, log2, repeat);
   }
   return fprintf(stderr, "unknown protocol\n"), 2;
 }
