@@ -206,6 +206,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_PB: return make_engine<PB>(d, cfg, out);
     case DSL_PROTO_MINITEST: return make_engine<MiniTest>(d, cfg, out);
     case DSL_PROTO_PINGPONG_IR: return make_engine<PingPongIR>(d, cfg, out);
+    case DSL_PROTO_AMOKV_IR: return make_engine<AmoKVIR>(d, cfg, out);
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;
@@ -291,6 +292,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_PB: return (int)sizeof(dsl::PB::State);
     case DSL_PROTO_MINITEST: return (int)sizeof(dsl::MiniTest::State);
     case DSL_PROTO_PINGPONG_IR: return (int)sizeof(dsl::PingPongIR::State);
+    case DSL_PROTO_AMOKV_IR: return (int)sizeof(dsl::AmoKVIR::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }
@@ -305,6 +307,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_PB: { using P = dsl::PB; return call; }                 \
     case DSL_PROTO_MINITEST: { using P = dsl::MiniTest; return call; }     \
     case DSL_PROTO_PINGPONG_IR: { using P = dsl::PingPongIR; return call; } \
+    case DSL_PROTO_AMOKV_IR: { using P = dsl::AmoKVIR; return call; }       \
     default: return DSL_ERR_UNKNOWN_PROTOCOL;                           \
   }
 

@@ -8,4 +8,5 @@
 #include "sipaxos.hpp"
 #include "synthetic.hpp"
 #include "gen/pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
+#include "gen/amokv_ir.hpp"
 #define DSL_HAVE_MULTIPAXOS 1

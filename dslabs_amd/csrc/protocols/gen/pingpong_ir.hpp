@@ -11,7 +11,7 @@
 namespace dsl {
 
 struct PingPongIR {
-  static constexpr int kNodes = 5, kNodeWords = 5, kNetCap = 120, kMaxSends = 2;
+  static constexpr int kNodes = 5, kNodeWords = 6, kNetCap = 120, kMaxSends = 2;
   static constexpr int kMsgClasses = 2;
   using Rec = uint32_t;
   using State = StateOf<PingPongIR>;
@@ -38,12 +38,12 @@ struct PingPongIR {
     if (type == 0) { mn = 10; mx = 10; }
   }
   static DSL_HD int ttype(int e) { return 0; }
-  template <class O>
-  static DSL_HD void push_timer_client(uint32_t* w, int e, O& out) {
+  static DSL_HD bool push_timer_client(uint32_t* w, int e) {
     const int n = get(w, 8, 4);
-    if (n >= 15) { out.overflow = true; return; }
-    put(w, 12 + 4 * n, 4, e);
+    if (n >= 15) return false;
+    put(w, 32 + 4 * (n), 4, e);
     put(w, 8, 4, n + 1);
+    return true;
   }
   // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)
   static DSL_HD int deliverable_client(const uint32_t* w, int j) {
@@ -51,7 +51,7 @@ struct PingPongIR {
     int mm = 0x7fffffff, c = 0;
     for (int q = 0; q < n; q++) {
       int mn = 0, mx = 0;
-      tbounds(ttype(get(w, 12 + 4 * q, 4)), mn, mx);
+      tbounds(ttype(get(w, 32 + 4 * (q), 4)), mn, mx);
       if (q > 0 && mn >= mm) continue;
       if (c == j) return q;
       c++;
@@ -63,31 +63,32 @@ struct PingPongIR {
     const int n = get(w, 8, 4);
     int q0 = n;
     for (int q = n - 1; q >= 0; q--)
-      if (get(w, 12 + 4 * q, 4) == e) q0 = q;
+      if (get(w, 32 + 4 * (q), 4) == e) q0 = q;
     if (q0 >= n) return;
-    for (int q = q0; q + 1 < n; q++) put(w, 12 + 4 * q, 4, get(w, 12 + 4 * (q + 1), 4));
-    put(w, 12 + 4 * (n - 1), 4, 0);
+    for (int q = q0; q + 1 < n; q++) put(w, 32 + 4 * (q), 4, get(w, 32 + 4 * (q + 1), 4));
+    put(w, 32 + 4 * (n - 1), 4, 0);
     put(w, 8, 4, n - 1);
   }
   template <class O>
-  static DSL_HD void send_command_client(int i, uint32_t* w, int cmd, O& out, const Params& p) {
+  static DSL_HD int send_command_client(int i, uint32_t* w, int cmd, O& out, const Params& p) {
     (void)p;
     put(w, 0, 4, cmd);
     put(w, 4, 4, 0);
     out.send(((Rec)0 << 31) | ((Rec)(i) << 28) | ((Rec)((0 + 1 - 1)) << 25) | ((Rec)((cmd) & 15) << 0));
-    push_timer_client(w, (((cmd) & 15) << 0), out);
+    if (!push_timer_client(w, (((cmd) & 15) << 0))) return STEP_OVERFLOW;
+    return STEP_OK;
   }
   // ClientWorker.sendNextCommandWhilePossible (waitingOnResult == |results| < workload size)
   template <class O>
   static DSL_HD void client_worker_client(int i, uint32_t* w, O& out, const Params& p) {
-    int n = get(w, 72, 4);
+    int n = get(w, 96, 4);
     const int res = get(w, 4, 4);
     if (n < p.pings && res != 0) {
       if (n >= 15) { out.overflow = true; return; }
-      put(w, 76 + 4 * n, 4, res);
+      put(w, 128 + 4 * (n), 4, res);
       n++;
-      put(w, 72, 4, n);
-      if (n < p.pings) send_command_client(i, w, n + 1, out, p);
+      put(w, 96, 4, n);
+      if (n < p.pings && send_command_client(i, w, n + 1, out, p) != STEP_OK) out.overflow = true;
     }
   }
   template <class O>
@@ -96,7 +97,7 @@ struct PingPongIR {
       return;
     }
     if (is_client(i, p)) {
-      if (p.pings > 0) send_command_client(i, w, 1, out, p);
+      if (p.pings > 0 && send_command_client(i, w, 1, out, p) != STEP_OK) out.overflow = true;
       return;
     }
   }
@@ -106,22 +107,46 @@ struct PingPongIR {
     return 0;
   }
   template <class O>
+  static DSL_HD int hm_pingserver_PingRequest(int i, uint32_t* w, Rec r, O& out, const Params& p) {
+    (void)i; (void)w; (void)r; (void)out; (void)p;
+    out.send(((Rec)1 << 31) | ((Rec)(i) << 28) | ((Rec)(rec_from(r)) << 25) | ((Rec)(((int)((r >> 0) & 15u)) & 15) << 0));
+    return STEP_OK;
+  }
+  template <class O>
+  static DSL_HD int hm_client_PongReply(int i, uint32_t* w, Rec r, O& out, const Params& p) {
+    (void)i; (void)w; (void)r; (void)out; (void)p;
+    if (((p.check_value == 0) || (get(w, 0, 4) == (int)((r >> 0) & 15u)))) {
+      put(w, 4, 4, (int)((r >> 0) & 15u));
+    }
+    return STEP_OK;
+  }
+  template <class O>
+  static DSL_HD int ht_client_PingTimer(int i, uint32_t* w, int e, O& out, const Params& p) {
+    (void)i; (void)w; (void)out; (void)p;
+    const int tf_value = (e >> 0) & 15;
+    if (((get(w, 0, 4) == tf_value) && (get(w, 4, 4) == 0))) {
+      out.send(((Rec)0 << 31) | ((Rec)(i) << 28) | ((Rec)((0 + 1 - 1)) << 25) | ((Rec)((tf_value) & 15) << 0));
+      if ((p.reset_timer != 0)) {
+        if (!push_timer_client(w, (((tf_value) & 15) << 0))) return STEP_OVERFLOW;
+      }
+    }
+    return STEP_OK;
+  }
+  template <class O>
   static DSL_HD int on_message(int i, uint32_t* w, Rec r, O& out, const Params& p) {
     (void)w; (void)out;
     if (is_pingserver(i, p)) {
       if (rec_type(r) == 0) {  // PingRequest
-        out.send(((Rec)1 << 31) | ((Rec)(i) << 28) | ((Rec)(rec_from(r)) << 25) | ((Rec)(((int)((r >> 0) & 15u)) & 15) << 0));
-        return STEP_OK;
+        const int rc = hm_pingserver_PingRequest(i, w, r, out, p);
+        return rc;
       }
       return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)
     }
     if (is_client(i, p)) {
       if (rec_type(r) == 1) {  // PongReply
-        if (((p.check_value == 0) || (get(w, 0, 4) == (int)((r >> 0) & 15u)))) {
-          put(w, 4, 4, (int)((r >> 0) & 15u));
-        }
-        client_worker_client(i, w, out, p);
-        return STEP_OK;
+        const int rc = hm_client_PongReply(i, w, r, out, p);
+        if (rc == STEP_OK) client_worker_client(i, w, out, p);
+        return rc;
       }
       return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)
     }
@@ -133,15 +158,10 @@ struct PingPongIR {
     if (is_client(i, p)) {
       const int q = deliverable_client(w, j);
       if (q < 0) return STEP_NULL;
-      const int e = get(w, 12 + 4 * q, 4);
+      const int e = get(w, 32 + 4 * (q), 4);
       if (ttype(e) == 0) {  // PingTimer
-        const int tf_value = (e >> 0) & 15;
-        if (((get(w, 0, 4) == tf_value) && (get(w, 4, 4) == 0))) {
-          out.send(((Rec)0 << 31) | ((Rec)(i) << 28) | ((Rec)((0 + 1 - 1)) << 25) | ((Rec)((tf_value) & 15) << 0));
-          if ((p.reset_timer != 0)) {
-            push_timer_client(w, (((tf_value) & 15) << 0), out);
-          }
-        }
+        const int rc = ht_client_PingTimer(i, w, e, out, p);
+        if (rc != STEP_OK) return rc;
         client_worker_client(i, w, out, p);
         remove_timer_client(w, e);  // SearchState.stepTimer: the first equal entry
         return STEP_OK;
@@ -156,25 +176,27 @@ struct PingPongIR {
       case DSL_PRED_RESULTS_OK:  // every result equals the workload's expected result
         for (int c = c0; c < c0 + nc; c++) {
           const uint32_t* w = v.node(c);
-          const int n = get(w, 72, 4);
-          for (int j = 0; j < n; j++)
-            if (get(w, 76 + 4 * j, 4) != (j + 1)) return PV_FALSE;
+          const int n = get(w, 96, 4);
+          for (int j = 0; j < n; j++) {
+            const int x = (j + 1);
+            if (x >= 0 && get(w, 128 + 4 * (j), 4) != x) return PV_FALSE;
+          }
         }
         return PV_TRUE;
       case DSL_PRED_CLIENTS_DONE:
         for (int c = c0; c < c0 + nc; c++)
-          if (get(v.node(c), 72, 4) < p.pings) return PV_FALSE;
+          if (get(v.node(c), 96, 4) < p.pings) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_DONE:
         if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;
-        return get(v.node((int)pr.arg0), 72, 4) >= p.pings ? PV_TRUE : PV_FALSE;
+        return get(v.node((int)pr.arg0), 96, 4) >= p.pings ? PV_TRUE : PV_FALSE;
       case DSL_PRED_NONE_DECIDED:
         for (int c = c0; c < c0 + nc; c++)
-          if (get(v.node(c), 72, 4) > 0) return PV_FALSE;
+          if (get(v.node(c), 96, 4) > 0) return PV_FALSE;
         return PV_TRUE;
       case DSL_PRED_CLIENT_HAS_RESULTS:
         if (pr.arg0 < c0 || pr.arg0 >= c0 + nc) return PV_THREW;
-        return get(v.node((int)pr.arg0), 72, 4) == pr.arg1 ? PV_TRUE : PV_FALSE;
+        return get(v.node((int)pr.arg0), 96, 4) == pr.arg1 ? PV_TRUE : PV_FALSE;
       default:
         return PV_THREW;
     }
@@ -220,7 +242,7 @@ struct PingPongIR {
     if (is_client(i, p)) {
       const int q = deliverable_client(w, j);
       if (q < 0) return;
-      const int x = get(w, 12 + 4 * q, 4);
+      const int x = get(w, 32 + 4 * (q), 4);
       e->type = 2 + ttype(x);
       int mn = 0, mx = 0;
       tbounds(ttype(x), mn, mx);

@@ -50,6 +50,19 @@ class Expr:
     def __invert__(self):
         return Expr(f"(!{self.dev})", f"(!{self.orc})")
 
+    # bit operations (integers): explicit names, since & and | are the logical connectives
+    def shl(self, n):
+        return self._bin(n, "<<")
+
+    def shr(self, n):
+        return self._bin(n, ">>")
+
+    def band(self, m):
+        return self._bin(m, "&")
+
+    def bor(self, m):
+        return self._bin(m, "|")
+
     def __hash__(self):
         return id(self)
 
@@ -80,6 +93,17 @@ class Param:
 
 
 @dataclass
+class ParamTable:
+    """A per-(row, column) parameter table, e.g. a workload's command table by (client, command)."""
+    name: str
+    rows: int
+    cols: int
+    lo: int
+    hi: int
+    default: int = 0
+
+
+@dataclass
 class RecordType:
     """A message or timer type: integer fields of fixed widths, in declaration order."""
     name: str
@@ -93,9 +117,19 @@ class FieldDecl:
     name: str
     bits: int
     cap: int = 0  # > 0: a bounded list of `cap` elements of `bits` each, with a length
+    array: bool = False  # with cap: a fixed-size array (no length), indexed by h.at / h.set_at
     off: int = 0
     len_off: int = 0
     len_bits: int = 0
+    per: int = 1  # list / array elements per 32-bit word
+
+    def elem(self, j: str) -> str:
+        """C++ bit offset of element j (an index expression)."""
+        if self.per == 1:
+            return f"{self.off} + 32 * ({j})"
+        if 32 % self.bits == 0:
+            return f"{self.off} + {self.bits} * ({j})"
+        return f"{self.off} + ({j}) / {self.per} * 32 + ({j}) % {self.per} * {self.bits}"
 
 
 @dataclass
@@ -140,13 +174,15 @@ class Protocol:
     def __init__(self, name: str, proto_id: int, cxx_name: str, doc: str = ""):
         self.name, self.proto_id, self.cxx_name, self.doc = name, proto_id, cxx_name, doc
         self.params: List[Param] = []
+        self.tables: List[ParamTable] = []
         self.messages: List[RecordType] = []
         self.timers: List[RecordType] = []
         self.kinds: List[NodeKind] = []
         self.net_cap = 32
         self.max_sends = 4
         self.workload_size = ""       # Param name: commands per client
-        self.expected_result: Optional[Callable] = None  # k (1-based Expr) -> expected result Expr
+        # (client index c from 0, command k from 1) -> expected result Expr; < 0: not checked
+        self.expected_result: Optional[Callable] = None
 
     # declarations
     def param(self, name: str, default: int, lo: int = 0, hi: int = 1 << 30) -> Param:
@@ -164,15 +200,25 @@ class Protocol:
         self.timers.append(r)
         return r
 
-    def node(self, name: str, count=1, max_count: int = 1, single_name: Optional[str] = None, **fields: int) -> NodeKind:
-        k = NodeKind(name, count, max_count, [FieldDecl(n, b) for n, b in fields.items()], single_name=single_name)
+    def param_table(self, name: str, rows: int, cols: int, lo: int = -(1 << 30), hi: int = 1 << 30,
+                    default: int = 0) -> ParamTable:
+        t = ParamTable(name, rows, cols, lo, hi, default)
+        self.tables.append(t)
+        return t
+
+    def node(self, name: str, count=1, max_count: int = 1, single_name: Optional[str] = None,
+             arrays: Optional[Dict[str, Tuple[int, int]]] = None, **fields: int) -> NodeKind:
+        """fields: name -> bits; arrays: name -> (bits, size) fixed-size arrays."""
+        fl = [FieldDecl(n, b) for n, b in fields.items()]
+        fl += [FieldDecl(n, b, cap, array=True) for n, (b, cap) in (arrays or {}).items()]
+        k = NodeKind(name, count, max_count, fl, single_name=single_name)
         self.kinds.append(k)
         return k
 
-    def client_worker(self, name: str, count, max_count: int, result: str, results_cap: int, timer_cap: int,
-                      **fields: int) -> NodeKind:
-        k = self.node(name, count, max_count, **fields)
-        k.client, k.result_field, k.results_cap, k.timer_cap = True, result, results_cap, timer_cap
+    def client_worker(self, name: str, count, max_count: int, result_field: str, results_cap: int, timer_cap: int,
+                      arrays=None, **fields: int) -> NodeKind:
+        k = self.node(name, count, max_count, arrays=arrays, **fields)
+        k.client, k.result_field, k.results_cap, k.timer_cap = True, result_field, results_cap, timer_cap
         return k
 
     # derived layout ------------------------------------------------------------------------------
@@ -203,12 +249,15 @@ class Protocol:
 
             for f in k.fields:
                 if f.cap:
-                    f.len_bits = max(1, f.cap.bit_length())
-                    f.len_off = place(f.len_bits)
+                    if not f.array:
+                        f.len_bits = max(1, f.cap.bit_length())
+                        f.len_off = place(f.len_bits)
                     assert f.bits <= 32
-                    f.off = place(f.bits)
-                    for _ in range(f.cap - 1):
-                        place(f.bits)  # consecutive elements (each within one word)
+                    # word-aligned; `per` elements per word, none straddling a word
+                    f.per = 32 // f.bits
+                    bit = (bit + 31) // 32 * 32
+                    f.off = bit
+                    bit += (f.cap + f.per - 1) // f.per * 32
                 else:
                     f.off = place(f.bits)
             words = max(words, (bit + 31) // 32)
@@ -284,6 +333,42 @@ class ThrowS(Stmt):
     what: str
 
 
+@dataclass
+class LetS(Stmt):
+    name: str
+    value: Expr
+
+
+@dataclass
+class VarS(Stmt):
+    name: str
+    value: Expr
+    mutable: bool = True
+
+
+@dataclass
+class SetVarS(Stmt):
+    name: str
+    value: Expr
+
+
+@dataclass
+class SetAtS(Stmt):
+    fld: FieldDecl
+    index: Expr
+    value: Expr
+
+
+@dataclass
+class RetS(Stmt):
+    pass
+
+
+@dataclass
+class OverflowS(Stmt):
+    what: str
+
+
 class _Fields:
     def __init__(self, h):
         object.__setattr__(self, "_h", h)
@@ -328,6 +413,44 @@ class Handler:
         f = self._fd(name)
         assert not f.cap, "lists are read with h.at(field, i)"
         return Expr(f"get(w, {f.off}, {f.bits})", f"{name}")
+
+    def at(self, name, index) -> Expr:
+        """Element `index` of an array field."""
+        f, i = self._fd(name), lit(index)
+        assert f.array
+        return Expr(f"get(w, {f.elem(i.dev)}, {f.bits})", f"{name}[{i.orc}]")
+
+    def ptab(self, name, r, c) -> Expr:
+        """Parameter table entry [r][c]."""
+        r, c = lit(r), lit(c)
+        return Expr(f"sel_param(p.{name}, {r.dev}, {c.dev})", f"prm.{name}[{r.orc}][{c.orc}]")
+
+    def let(self, name: str, value) -> Expr:
+        """A named intermediate value (a local constant in both forms)."""
+        self._emit(LetS("l_" + name, lit(value)))
+        return Expr("l_" + name, "l_" + name)
+
+    def var(self, name: str, init=0) -> Expr:
+        """A mutable local (h.assign(name, value) changes it)."""
+        self._emit(VarS("l_" + name, lit(init)))
+        return Expr("l_" + name, "l_" + name)
+
+    def assign(self, name: str, value):
+        self._emit(SetVarS("l_" + name, lit(value)))
+
+    def set_at(self, name: str, index, value):
+        f = self._fd(name)
+        assert f.array
+        self._emit(SetAtS(f, lit(index), lit(value)))
+
+    def ret(self):
+        """Return from the handler (the ClientWorker loop still runs for a client)."""
+        self._emit(RetS())
+
+    def overflow(self, what: str):
+        """A bounded container of the packed form is full: a hard error on the device
+        (DSL_ERR_STATE_OVERFLOW); the oracle's objects are unbounded."""
+        self._emit(OverflowS(what))
 
     def _rec_field(self, which, name) -> Expr:
         ev = self.event

@@ -7,7 +7,8 @@ from __future__ import annotations
 
 from typing import List
 
-from .core import Assign, Expr, IfS, NodeKind, Protocol, SendS, SetTimerS, Stmt, ThrowS, lit, record
+from .core import (Assign, Expr, IfS, LetS, SetVarS, VarS, NodeKind, OverflowS, Protocol, RetS, SendS, SetAtS, SetTimerS, Stmt,
+                   ThrowS, lit, record)
 
 
 def _ind(n):
@@ -42,9 +43,21 @@ def _stmts(p: Protocol, k: NodeKind, ss: List[Stmt], d: int) -> List[str]:
             out.append(f"{_ind(d)}out.send({_rec_expr(p, s)});")
         elif isinstance(s, SetTimerS):
             tf = next(f for f in k.fields if f.name == "_timers")
-            out.append(f"{_ind(d)}push_timer_{k.name}(w, {_timer_entry(p, s.timer, s.vals)}, out);")
+            out.append(f"{_ind(d)}if (!push_timer_{k.name}(w, {_timer_entry(p, s.timer, s.vals)})) return STEP_OVERFLOW;")
         elif isinstance(s, ThrowS):
             out.append(f"{_ind(d)}return STEP_EXCEPTION;  // {s.what}")
+        elif isinstance(s, VarS):
+            out.append(f"{_ind(d)}int {s.name} = {s.value.dev};")
+        elif isinstance(s, SetVarS):
+            out.append(f"{_ind(d)}{s.name} = {s.value.dev};")
+        elif isinstance(s, LetS):
+            out.append(f"{_ind(d)}const int {s.name} = {s.value.dev};")
+        elif isinstance(s, SetAtS):
+            out.append(f"{_ind(d)}put(w, {s.fld.elem(s.index.dev)}, {s.fld.bits}, {s.value.dev});")
+        elif isinstance(s, RetS):
+            out.append(f"{_ind(d)}return STEP_OK;")
+        elif isinstance(s, OverflowS):
+            out.append(f"{_ind(d)}return STEP_OVERFLOW;  // {s.what}")
         elif isinstance(s, IfS):
             out.append(f"{_ind(d)}if ({s.cond.dev}) {{")
             out += _stmts(p, k, s.then, d + 1)
@@ -78,6 +91,8 @@ def generate(p: Protocol, source: str) -> str:
     a("  struct Params {")
     for q in p.params:
         a(f"    int32_t {q.name};")
+    for t in p.tables:
+        a(f"    int32_t {t.name}[{t.rows}][{t.cols}];")
     a("  };")
     a("  static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }")
     a("  static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }")
@@ -107,12 +122,12 @@ def generate(p: Protocol, source: str) -> str:
         if not k.timer_cap:
             continue
         tf = next(f for f in k.fields if f.name == "_timers")
-        a(f"  template <class O>")
-        a(f"  static DSL_HD void push_timer_{k.name}(uint32_t* w, int e, O& out) {{")
+        a(f"  static DSL_HD bool push_timer_{k.name}(uint32_t* w, int e) {{")
         a(f"    const int n = get(w, {tf.len_off}, {tf.len_bits});")
-        a(f"    if (n >= {tf.cap}) {{ out.overflow = true; return; }}")
-        a(f"    put(w, {tf.off} + {tf.bits} * n, {tf.bits}, e);")
+        a(f"    if (n >= {tf.cap}) return false;")
+        a(f"    put(w, {tf.elem('n')}, {tf.bits}, e);")
         a(f"    put(w, {tf.len_off}, {tf.len_bits}, n + 1);")
+        a("    return true;")
         a("  }")
         # deliverable entries (TimerQueue.deliverable): yield in order; skip min >= min(max yielded)
         a(f"  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)")
@@ -121,7 +136,7 @@ def generate(p: Protocol, source: str) -> str:
         a("    int mm = 0x7fffffff, c = 0;")
         a(f"    for (int q = 0; q < n; q++) {{")
         a(f"      int mn = 0, mx = 0;")
-        a(f"      tbounds(ttype(get(w, {tf.off} + {tf.bits} * q, {tf.bits})), mn, mx);")
+        a(f"      tbounds(ttype(get(w, {tf.elem('q')}, {tf.bits})), mn, mx);")
         a("      if (q > 0 && mn >= mm) continue;")
         a("      if (c == j) return q;")
         a("      c++;")
@@ -133,11 +148,11 @@ def generate(p: Protocol, source: str) -> str:
         a(f"    const int n = get(w, {tf.len_off}, {tf.len_bits});")
         a("    int q0 = n;")
         a(f"    for (int q = n - 1; q >= 0; q--)")
-        a(f"      if (get(w, {tf.off} + {tf.bits} * q, {tf.bits}) == e) q0 = q;")
+        a(f"      if (get(w, {tf.elem('q')}, {tf.bits}) == e) q0 = q;")
         a("    if (q0 >= n) return;")
-        a(f"    for (int q = q0; q + 1 < n; q++) put(w, {tf.off} + {tf.bits} * q, {tf.bits}, "
-          f"get(w, {tf.off} + {tf.bits} * (q + 1), {tf.bits}));")
-        a(f"    put(w, {tf.off} + {tf.bits} * (n - 1), {tf.bits}, 0);")
+        a(f"    for (int q = q0; q + 1 < n; q++) put(w, {tf.elem('q')}, {tf.bits}, "
+          f"get(w, {tf.elem('q + 1')}, {tf.bits}));")
+        a(f"    put(w, {tf.elem('n - 1')}, {tf.bits}, 0);")
         a(f"    put(w, {tf.len_off}, {tf.len_bits}, n - 1);")
         a("  }")
     # client worker
@@ -149,9 +164,10 @@ def generate(p: Protocol, source: str) -> str:
         rl = next(f for f in k.fields if f.name == "_results")
         body = record(p, k, k.send_command_fn, cmd=E("cmd", "cmd"))
         a("  template <class O>")
-        a(f"  static DSL_HD void send_command_{k.name}(int i, uint32_t* w, int cmd, O& out, const Params& p) {{")
+        a(f"  static DSL_HD int send_command_{k.name}(int i, uint32_t* w, int cmd, O& out, const Params& p) {{")
         a("    (void)p;")
         L.extend(_stmts(p, k, body, 2))
+        a("    return STEP_OK;")
         a("  }")
         a("  // ClientWorker.sendNextCommandWhilePossible (waitingOnResult == |results| < workload size)")
         a("  template <class O>")
@@ -160,10 +176,10 @@ def generate(p: Protocol, source: str) -> str:
         a(f"    const int res = get(w, {rf.off}, {rf.bits});")
         a(f"    if (n < p.{p.workload_size} && res != 0) {{")
         a(f"      if (n >= {rl.cap}) {{ out.overflow = true; return; }}")
-        a(f"      put(w, {rl.off} + {rl.bits} * n, {rl.bits}, res);")
+        a(f"      put(w, {rl.elem('n')}, {rl.bits}, res);")
         a("      n++;")
         a(f"      put(w, {rl.len_off}, {rl.len_bits}, n);")
-        a(f"      if (n < p.{p.workload_size}) send_command_{k.name}(i, w, n + 1, out, p);")
+        a(f"      if (n < p.{p.workload_size} && send_command_{k.name}(i, w, n + 1, out, p) != STEP_OK) out.overflow = true;")
         a("    }")
         a("  }")
     # init
@@ -172,9 +188,9 @@ def generate(p: Protocol, source: str) -> str:
     for k in p.kinds:
         a(f"    if (is_{k.name}(i, p)) {{")
         if k.init_fn:
-            L.extend(_stmts(p, k, record(p, k, k.init_fn), 3))
+            a(f"      if (init_{k.name}(i, w, out, p) != STEP_OK) out.overflow = true;")
         if k.client:  # ClientWorker.init: the first command
-            a(f"      if (p.{p.workload_size} > 0) send_command_{k.name}(i, w, 1, out, p);")
+            a(f"      if (p.{p.workload_size} > 0 && send_command_{k.name}(i, w, 1, out, p) != STEP_OK) out.overflow = true;")
         a("      return;")
         a("    }")
     a("  }")
@@ -185,7 +201,40 @@ def generate(p: Protocol, source: str) -> str:
     a("    (void)i; (void)w; (void)p;")
     a("    return 0;")
     a("  }")
-    # message handlers
+    # handler bodies (one function each: an early return still reaches the ClientWorker loop)
+    for k in p.kinds:
+        if k.init_fn:
+            a("  template <class O>")
+            a(f"  static DSL_HD int init_{k.name}(int i, uint32_t* w, O& out, const Params& p) {{")
+            a("    (void)i; (void)p; (void)out;")
+            L.extend(_stmts(p, k, record(p, k, k.init_fn), 2))
+            a("    return STEP_OK;")
+            a("  }")
+        for m in p.messages:
+            fn = k.handlers.get(m.name)
+            if fn is None:
+                continue
+            a("  template <class O>")
+            a(f"  static DSL_HD int hm_{k.name}_{m.name}(int i, uint32_t* w, Rec r, O& out, const Params& p) {{")
+            a("    (void)i; (void)w; (void)r; (void)out; (void)p;")
+            L.extend(_stmts(p, k, record(p, k, fn, event=m), 2))
+            a("    return STEP_OK;")
+            a("  }")
+        for t in p.timers:
+            fn = k.timer_handlers.get(t.name)
+            if fn is None:
+                continue
+            a("  template <class O>")
+            a(f"  static DSL_HD int ht_{k.name}_{t.name}(int i, uint32_t* w, int e, O& out, const Params& p) {{")
+            a("    (void)i; (void)w; (void)out; (void)p;")
+            off = 0
+            for n, b in t.fields:
+                a(f"    const int tf_{n} = (e >> {off}) & {(1 << b) - 1};")
+                off += b
+            L.extend(_stmts(p, k, record(p, k, fn, event=t, is_timer=True), 2))
+            a("    return STEP_OK;")
+            a("  }")
+  # message handlers
     a("  template <class O>")
     a("  static DSL_HD int on_message(int i, uint32_t* w, Rec r, O& out, const Params& p) {")
     a("    (void)w; (void)out;")
@@ -196,10 +245,10 @@ def generate(p: Protocol, source: str) -> str:
             if fn is None:
                 continue
             a(f"      if (rec_type(r) == {m.index}) {{  // {m.name}")
-            L.extend(_stmts(p, k, record(p, k, fn, event=m), 4))
+            a(f"        const int rc = hm_{k.name}_{m.name}(i, w, r, out, p);")
             if k.client:
-                a(f"        client_worker_{k.name}(i, w, out, p);")
-            a("        return STEP_OK;")
+                a(f"        if (rc == STEP_OK) client_worker_{k.name}(i, w, out, p);")
+            a("        return rc;")
             a("      }")
         a("      return STEP_EXCEPTION;  // no handler for this message (Node.handleMessage throws)")
         a("    }")
@@ -216,17 +265,14 @@ def generate(p: Protocol, source: str) -> str:
         a(f"    if (is_{k.name}(i, p)) {{")
         a(f"      const int q = deliverable_{k.name}(w, j);")
         a("      if (q < 0) return STEP_NULL;")
-        a(f"      const int e = get(w, {tf.off} + {tf.bits} * q, {tf.bits});")
+        a(f"      const int e = get(w, {tf.elem('q')}, {tf.bits});")
         for t in p.timers:
             fn = k.timer_handlers.get(t.name)
             if fn is None:
                 continue
             a(f"      if (ttype(e) == {t.index}) {{  // {t.name}")
-            off = 0
-            for n, b in t.fields:
-                a(f"        const int tf_{n} = (e >> {off}) & {(1 << b) - 1};")
-                off += b
-            L.extend(_stmts(p, k, record(p, k, fn, event=t, is_timer=True), 4))
+            a(f"        const int rc = ht_{k.name}_{t.name}(i, w, e, out, p);")
+            a("        if (rc != STEP_OK) return rc;")
             if k.client:
                 a(f"        client_worker_{k.name}(i, w, out, p);")
             a(f"        remove_timer_{k.name}(w, e);  // SearchState.stepTimer: the first equal entry")
@@ -242,7 +288,7 @@ def generate(p: Protocol, source: str) -> str:
     if ck:
         k = ck[0]
         rl = next(f for f in k.fields if f.name == "_results")
-        exp = p.expected_result(E("(j + 1)", "(j + 1)")).dev
+        exp = lit(p.expected_result(E("(c - c0)", "(c - c0)"), E("(j + 1)", "(j + 1)"))).dev
         fc, nc = f"first_{k.name}(p)", cnt(k)
         a(f"    const int c0 = {fc}, nc = {nc};")
         a("    switch (pr.id) {")
@@ -250,8 +296,10 @@ def generate(p: Protocol, source: str) -> str:
         a("        for (int c = c0; c < c0 + nc; c++) {")
         a("          const uint32_t* w = v.node(c);")
         a(f"          const int n = get(w, {rl.len_off}, {rl.len_bits});")
-        a(f"          for (int j = 0; j < n; j++)")
-        a(f"            if (get(w, {rl.off} + {rl.bits} * j, {rl.bits}) != {exp}) return PV_FALSE;")
+        a(f"          for (int j = 0; j < n; j++) {{")
+        a(f"            const int x = {exp};")
+        a(f"            if (x >= 0 && get(w, {rl.elem('j')}, {rl.bits}) != x) return PV_FALSE;")
+        a("          }")
         a("        }")
         a("        return PV_TRUE;")
         a("      case DSL_PRED_CLIENTS_DONE:")
@@ -290,12 +338,24 @@ def generate(p: Protocol, source: str) -> str:
     for k in p.kinds:
         if not isinstance(k.count, int):
             conds.append(f"p.{k.count} >= 1 && p.{k.count} <= {k.max_count}")
+    for t in p.tables:
+        a(f"    for (int r = 0; r < {t.rows}; r++)")
+        a(f"      for (int c = 0; c < {t.cols}; c++)")
+        a(f"        if (p.{t.name}[r][c] < {t.lo} || p.{t.name}[r][c] > {t.hi}) return false;")
     a("    return " + (" &&\n           ".join(conds) if conds else "true") + ";")
     a("  }")
     a("  static Params from_desc(const dsl_protocol_desc& d) {")
     a("    Params p{};")
     for qi, q in enumerate(p.params):
         a(f"    p.{q.name} = d.n_params > {qi} ? (int32_t)d.params[{qi}] : {q.default};")
+    base = len(p.params)
+    for t in p.tables:
+        a(f"    for (int r = 0; r < {t.rows}; r++)")
+        a(f"      for (int c = 0; c < {t.cols}; c++) {{")
+        a(f"        const int q = {base} + r * {t.cols} + c;")
+        a(f"        p.{t.name}[r][c] = d.n_params > q ? (int32_t)d.params[q] : {t.default};")
+        a("      }")
+        base += t.rows * t.cols
     a("    return p;")
     a("  }")
     # descriptions
@@ -322,7 +382,7 @@ def generate(p: Protocol, source: str) -> str:
         a(f"    if (is_{k.name}(i, p)) {{")
         a(f"      const int q = deliverable_{k.name}(w, j);")
         a("      if (q < 0) return;")
-        a(f"      const int x = get(w, {tf.off} + {tf.bits} * q, {tf.bits});")
+        a(f"      const int x = get(w, {tf.elem('q')}, {tf.bits});")
         a(f"      e->type = {len(p.messages)} + ttype(x);")
         a("      int mn = 0, mx = 0;")
         a("      tbounds(ttype(x), mn, mx);")

@@ -6,7 +6,8 @@ from __future__ import annotations
 
 from typing import List
 
-from .core import Assign, Expr, IfS, NodeKind, Protocol, SendS, SetTimerS, Stmt, ThrowS, record
+from .core import (Assign, Expr, IfS, LetS, SetVarS, VarS, NodeKind, OverflowS, Protocol, RetS, SendS, SetAtS, SetTimerS, Stmt,
+                   ThrowS, lit, record)
 
 
 def _ind(n):
@@ -28,6 +29,18 @@ def _stmts(p: Protocol, k: NodeKind, ss: List[Stmt], d: int) -> List[str]:
             out.append(f"{_ind(d)}ctx.set({_rec(s.timer, s.vals)}, {s.timer.millis[0]}, {s.timer.millis[1]});")
         elif isinstance(s, ThrowS):
             out.append(f"{_ind(d)}throw HandlerException(\"{s.what}\");")
+        elif isinstance(s, VarS):
+            out.append(f"{_ind(d)}int {s.name} = {s.value.orc};")
+        elif isinstance(s, SetVarS):
+            out.append(f"{_ind(d)}{s.name} = {s.value.orc};")
+        elif isinstance(s, LetS):
+            out.append(f"{_ind(d)}const int {s.name} = {s.value.orc};")
+        elif isinstance(s, SetAtS):
+            out.append(f"{_ind(d)}{s.fld.name}[{s.index.orc}] = {s.value.orc};")
+        elif isinstance(s, RetS):
+            out.append(f"{_ind(d)}return;")
+        elif isinstance(s, OverflowS):
+            out.append(f"{_ind(d)}// {s.what}: bounded on the device only")
         elif isinstance(s, IfS):
             out.append(f"{_ind(d)}if ({s.cond.orc}) {{")
             out += _stmts(p, k, s.then, d + 1)
@@ -54,7 +67,21 @@ def generate(p: Protocol, source: str) -> str:
     a("struct Params {")
     for q in p.params:
         a(f"  int {q.name} = {q.default};")
+    for t in p.tables:
+        a(f"  int {t.name}[{t.rows}][{t.cols}] = {{}};")
     a("};")
+    a("// Params from the engine's parameter vector (dsl_protocol_desc.params order)")
+    a("inline Params from_vector(const std::vector<long long>& v) {")
+    a("  Params p;")
+    a("  size_t q = 0;")
+    for q in p.params:
+        a(f"  if (q < v.size()) p.{q.name} = (int)v[q];")
+        a("  q++;")
+    for t in p.tables:
+        a(f"  for (int r = 0; r < {t.rows}; r++)")
+        a(f"    for (int c = 0; c < {t.cols}; c++, q++) p.{t.name}[r][c] = q < v.size() ? (int)v[q] : {t.default};")
+    a("  return p;")
+    a("}")
     a("")
     for k in p.kinds:
         user = [f for f in k.fields if not f.name.startswith("_")]
@@ -64,16 +91,20 @@ def generate(p: Protocol, source: str) -> str:
         a("  Params prm;")
         a("  int self = 0;")
         for f in user:
-            a(f"  int {f.name} = 0;")
+            a(f"  std::vector<int> {f.name} = std::vector<int>({f.cap}, 0);" if f.array else f"  int {f.name} = 0;")
         a(f"  std::shared_ptr<Node> clone() const override {{ return std::make_shared<{cls}>(*this); }}")
         a("  void key(std::string& out) const override {")
         a(f"    out += \"{k.name}{{\";")
         for f in user:
-            a(f"    out += std::to_string({f.name}) + \",\";")
+            if f.array:
+                a(f"    for (int x : {f.name}) out += std::to_string(x) + \",\";")
+            else:
+                a(f"    out += std::to_string({f.name}) + \",\";")
         a("    out += \"}\";")
         a("  }")
         a("  std::string str() const override {")
-        parts = " + \", \" + ".join([f"\"{f.name}=\" + std::to_string({f.name})" for f in user]) or "std::string()"
+        parts = " + \", \" + ".join([f"\"{f.name}=\" + std::to_string({f.name})" for f in user if not f.array]) \
+            or "std::string()"
         a(f"    return std::string(\"{k.name}(\") + {parts} + \")\";")
         a("  }")
         if k.init_fn:
@@ -130,14 +161,17 @@ def generate(p: Protocol, source: str) -> str:
         a("    n->prm = prm;")
         a("    n->self = (int)nodes.size();")
         if k.client:
-            exp = p.expected_result(Expr("k", "k")).orc
+            exp = lit(p.expected_result(Expr("ci", "ci"), Expr("k", "k"))).orc
+            exp1 = lit(p.expected_result(Expr("ci", "ci"), Expr("1", "1"))).orc
             a("    auto cw = std::make_shared<ClientWorker>();")
             a("    cw->client = n;")
             a("    cw->addrName = names.addr.back();")
+            a("    const int ci = c - 1;")
             a("    cw->workload.cmds = {\"%i\"};")
-            a("    cw->workload.results = {\"%i\"};")
+            a(f"    if ({exp1} >= 0) cw->workload.results = {{\"%i\"}};  // a workload with expected results")
             a(f"    cw->workload.numTimes = prm.{p.workload_size};")
-            a("    cw->workload.parser = [](const std::string& c, const std::string& r) {")
+            a("    cw->workload.parser = [ci, prm](const std::string& c, const std::string& r) {")
+            a("      (void)ci; (void)prm;")
             a("      const int k = std::stoi(r);")
             a(f"      return std::make_pair(Rec{{\"Command\", {{c}}}}, Rec{{\"Result\", {{std::to_string({exp})}}}});")
             a("    };")

@@ -13,7 +13,7 @@ P.param("pings", 10, 1, 15)
 P.param("check_value", 1, 0, 1)
 P.param("reset_timer", 1, 0, 1)
 P.workload_size = "pings"
-P.expected_result = lambda k: k
+P.expected_result = lambda c, k: k
 P.net_cap = 120
 P.max_sends = 2
 
@@ -22,7 +22,7 @@ PongReply = P.message("PongReply", value=4)
 PingTimer = P.timer("PingTimer", (10, 10), value=4)
 
 server = P.node("pingserver", count=1, max_count=1, single_name="pingserver")
-client = P.client_worker("client", count="clients", max_count=4, result="pong", results_cap=15, timer_cap=15,
+client = P.client_worker("client", count="clients", max_count=4, result_field="pong", results_cap=15, timer_cap=15,
                          ping=4, pong=4)
 
 

@@ -678,3 +678,33 @@ class PingPongIR(IRProtocol):
     def __init__(self, clients: int = 1, pings: int = 10, check_value: bool = True, reset_timer: bool = True):
         super().__init__("pingpong", clients=clients, pings=pings, check_value=int(check_value),
                          reset_timer=int(reset_timer))
+
+
+class AmoKVIR(IRProtocol):
+    """lab1 AMO KV generated from the protocol IR (dslabs_amd/ir/specs/amokv.py), with AmoKV's
+    workloads (the same command tables and result encodings)."""
+
+    def __init__(self, clients: int = 2, workload: str = "diffkey3"):
+        kv = AmoKV(clients, workload)
+        tables = {n: [[0] * 3 for _ in range(3)] for n in ("op", "key", "sym")}
+        tables["expected"] = [[-1] * 3 for _ in range(3)]
+        ps = kv.params()[2:]
+        for c in range(3):
+            for k in range(3):
+                op, key, sym, exp = ps[4 * (3 * c + k): 4 * (3 * c + k) + 4]
+                tables["op"][c][k], tables["key"][c][k], tables["sym"][c][k] = op, key, sym
+                tables["expected"][c][k] = exp
+        super().__init__("amokv", clients=clients, ncmds=kv.ncmds)
+        self.kv = kv
+        self._tables = tables
+
+    def params(self):
+        ps = super().params()
+        for n in ("op", "key", "sym", "expected"):
+            for row in self._tables[n]:
+                ps += row
+        return ps
+
+    def oracle_args(self):
+        return ["--proto", "amokv_ir", "--clients", str(self.values["clients"]), "--ir-params",
+                ",".join(str(x) for x in self.params())]

@@ -26,6 +26,7 @@
 #include "proto_sipaxos.hpp"
 #include "proto_synthetic.hpp"
 #include "gen/proto_pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
+#include "gen/proto_amokv_ir.hpp"
 
 using namespace oracle;
 
@@ -110,6 +111,15 @@ static Scenario build(const Args& a) {
     prm.check_value = a.has("mutant-no-check") ? 0 : 1;
     prm.reset_timer = a.has("mutant-no-reset") ? 0 : 1;
     sc.init = pingpong_ir::initial(prm, sc.names);
+    sc.pred = [common](const std::string& n) {
+      auto p = common(n);
+      if (!p) throw std::runtime_error("unknown predicate " + n);
+      return *p;
+    };
+  } else if (a.proto == "amokv_ir") {  // --ir-params: the engine's parameter vector, comma-separated
+    std::vector<long long> v;
+    for (auto& x : split(a.get("ir-params"), ',')) v.push_back(std::stoll(x));
+    sc.init = amokv_ir::initial(amokv_ir::from_vector(v), sc.names);
     sc.pred = [common](const std::string& n) {
       auto p = common(n);
       if (!p) throw std::runtime_error("unknown predicate " + n);

@@ -1,0 +1,187 @@
+// GENERATED from the protocol IR (dslabs_amd/ir/specs/amokv.py) by dslabs_amd/ir/gen_oracle.py; do not edit.
+// oracle/ -- TEST INFRASTRUCTURE ONLY (see oracle_core.hpp).
+#pragma once
+#include "../oracle_core.hpp"
+
+namespace oracle {
+namespace amokv_ir {
+
+struct Params {
+  int clients = 2;
+  int ncmds = 3;
+  int op[3][3] = {};
+  int key[3][3] = {};
+  int sym[3][3] = {};
+  int expected[3][3] = {};
+};
+// Params from the engine's parameter vector (dsl_protocol_desc.params order)
+inline Params from_vector(const std::vector<long long>& v) {
+  Params p;
+  size_t q = 0;
+  if (q < v.size()) p.clients = (int)v[q];
+  q++;
+  if (q < v.size()) p.ncmds = (int)v[q];
+  q++;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++, q++) p.op[r][c] = q < v.size() ? (int)v[q] : 0;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++, q++) p.key[r][c] = q < v.size() ? (int)v[q] : 0;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++, q++) p.sym[r][c] = q < v.size() ? (int)v[q] : 0;
+  for (int r = 0; r < 3; r++)
+    for (int c = 0; c < 3; c++, q++) p.expected[r][c] = q < v.size() ? (int)v[q] : -1;
+  return p;
+}
+
+struct N_server : Node {
+  Params prm;
+  int self = 0;
+  std::vector<int> kv = std::vector<int>(3, 0);
+  std::vector<int> amo = std::vector<int>(3, 0);
+  std::shared_ptr<Node> clone() const override { return std::make_shared<N_server>(*this); }
+  void key(std::string& out) const override {
+    out += "server{";
+    for (int x : kv) out += std::to_string(x) + ",";
+    for (int x : amo) out += std::to_string(x) + ",";
+    out += "}";
+  }
+  std::string str() const override {
+    return std::string("server(") + std::string() + ")";
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    (void)from; (void)ctx;
+    if (m.type == "Request") {
+      const int l_c = (from - 1);
+      const int l_seq = std::stoi(m.f[0]);
+      if (((((l_c < 0) || (l_c >= prm.clients)) || (l_seq < 1)) || (l_seq > prm.ncmds))) {
+        throw HandlerException("request from an unknown client or command");
+      }
+      const int l_amo = amo[l_c];
+      const int l_last = (l_amo & 3);
+      if ((l_seq < l_last)) {
+        return;
+      }
+      int l_r = (l_amo >> 2);
+      if ((l_seq > l_last)) {
+        const int l_k = (l_seq - 1);
+        const int l_op = prm.op[l_c][l_k];
+        const int l_key = prm.key[l_c][l_k];
+        const int l_sym = prm.sym[l_c][l_k];
+        const int l_v = kv[l_key];
+        if ((l_op == 0)) {
+          if (((l_v & 15) != 0)) {
+            l_r = ((l_v << 2) | 1);
+          } else {
+            l_r = 2;
+          }
+        }
+        if ((l_op == 1)) {
+          kv[l_key] = ((l_sym << 4) | 1);
+          l_r = 3;
+        }
+        if ((l_op == 2)) {
+          const int l_n = (l_v & 15);
+          if ((l_n >= 9)) {
+            // value longer than 9 tokens: bounded on the device only
+          }
+          const int l_v2 = (((l_v - l_n) | (l_n + 1)) | (l_sym << ((l_n * 2) + 4)));
+          kv[l_key] = l_v2;
+          l_r = (l_v2 << 2);
+        }
+        amo[l_c] = (l_seq | (l_r << 2));
+      }
+      ctx.send(Rec{"Reply", {std::to_string(l_seq), std::to_string(l_r)}}, from);
+      return;
+    }
+    throw HandlerException("no handler");
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    (void)ctx;
+    throw HandlerException("no timer handler");
+  }
+};
+
+struct N_client : Client {
+  Params prm;
+  int self = 0;
+  int seq = 0;
+  int result = 0;
+  std::shared_ptr<Node> clone() const override { return std::make_shared<N_client>(*this); }
+  void key(std::string& out) const override {
+    out += "client{";
+    out += std::to_string(seq) + ",";
+    out += std::to_string(result) + ",";
+    out += "}";
+  }
+  std::string str() const override {
+    return std::string("client(") + "seq=" + std::to_string(seq) + ", " + "result=" + std::to_string(result) + ")";
+  }
+  void handleMessage(const Rec& m, int from, int, Ctx& ctx) override {
+    (void)from; (void)ctx;
+    if (m.type == "Reply") {
+      if (((result == 0) && (std::stoi(m.f[0]) == seq))) {
+        result = std::stoi(m.f[1]);
+      }
+      return;
+    }
+    throw HandlerException("no handler");
+  }
+  void onTimer(const Rec& t, Ctx& ctx) override {
+    (void)ctx;
+    if (t.type == "ClientTimer") {
+      if (((result == 0) && (std::stoi(t.f[0]) == seq))) {
+        ctx.send(Rec{"Request", {std::to_string(std::stoi(t.f[0]))}}, (0 + 1 - 1));
+        ctx.set(Rec{"ClientTimer", {std::to_string(std::stoi(t.f[0]))}}, 100, 100);
+      }
+      return;
+    }
+    throw HandlerException("no timer handler");
+  }
+  void sendCommand(const Rec& c, Ctx& ctx) override {
+    const int cmd = std::stoi(c.f[0]);
+    seq = cmd;
+    result = 0;
+    ctx.send(Rec{"Request", {std::to_string(cmd)}}, (0 + 1 - 1));
+    ctx.set(Rec{"ClientTimer", {std::to_string(cmd)}}, 100, 100);
+  }
+  bool hasResult() const override { return result != 0; }
+  Rec getResult() const override { return Rec{"Result", {std::to_string(result)}}; }
+};
+
+// Addresses: node kinds in declaration order, instances consecutive.
+inline std::shared_ptr<State> initial(const Params& prm, Names& names) {
+  std::vector<std::shared_ptr<Node>> nodes;
+  std::vector<Kind> kinds;
+  for (int c = 1; c <= 1; c++) {
+    names.addr.push_back("server");
+    auto n = std::make_shared<N_server>();
+    n->prm = prm;
+    n->self = (int)nodes.size();
+    nodes.push_back(n);
+    kinds.push_back(Kind::Server);
+  }
+  for (int c = 1; c <= prm.clients; c++) {
+    names.addr.push_back("client" + std::to_string(c));
+    auto n = std::make_shared<N_client>();
+    n->prm = prm;
+    n->self = (int)nodes.size();
+    auto cw = std::make_shared<ClientWorker>();
+    cw->client = n;
+    cw->addrName = names.addr.back();
+    const int ci = c - 1;
+    cw->workload.cmds = {"%i"};
+    if (prm.expected[ci][1 - 1] >= 0) cw->workload.results = {"%i"};  // a workload with expected results
+    cw->workload.numTimes = prm.ncmds;
+    cw->workload.parser = [ci, prm](const std::string& c, const std::string& r) {
+      (void)ci; (void)prm;
+      const int k = std::stoi(r);
+      return std::make_pair(Rec{"Command", {c}}, Rec{"Result", {std::to_string(prm.expected[ci][k - 1])}});
+    };
+    nodes.push_back(cw);
+    kinds.push_back(Kind::ClientWorker);
+  }
+  return makeInitial(nodes, kinds);
+}
+
+}  // namespace amokv_ir
+}  // namespace oracle

@@ -12,6 +12,20 @@ struct Params {
   int check_value = 1;
   int reset_timer = 1;
 };
+// Params from the engine's parameter vector (dsl_protocol_desc.params order)
+inline Params from_vector(const std::vector<long long>& v) {
+  Params p;
+  size_t q = 0;
+  if (q < v.size()) p.clients = (int)v[q];
+  q++;
+  if (q < v.size()) p.pings = (int)v[q];
+  q++;
+  if (q < v.size()) p.check_value = (int)v[q];
+  q++;
+  if (q < v.size()) p.reset_timer = (int)v[q];
+  q++;
+  return p;
+}
 
 struct N_pingserver : Node {
   Params prm;
@@ -107,10 +121,12 @@ inline std::shared_ptr<State> initial(const Params& prm, Names& names) {
     auto cw = std::make_shared<ClientWorker>();
     cw->client = n;
     cw->addrName = names.addr.back();
+    const int ci = c - 1;
     cw->workload.cmds = {"%i"};
-    cw->workload.results = {"%i"};
+    if (1 >= 0) cw->workload.results = {"%i"};  // a workload with expected results
     cw->workload.numTimes = prm.pings;
-    cw->workload.parser = [](const std::string& c, const std::string& r) {
+    cw->workload.parser = [ci, prm](const std::string& c, const std::string& r) {
+      (void)ci; (void)prm;
       const int k = std::stoi(r);
       return std::make_pair(Rec{"Command", {c}}, Rec{"Result", {std::to_string(k)}});
     };

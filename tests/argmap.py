@@ -1,7 +1,7 @@
 """Maps oracle CLI arguments (tests/golden/*.json "args") onto the engine's Python API, so each
 committed oracle fixture is replayed on the GPU with the same meaning."""
 from dslabs_amd import CLIENTS_DONE, NONE_DECIDED, RESULTS_OK, SearchSettings, clientDone
-from dslabs_amd.protocols import PB, AmoKV, MiniTest, MultiPaxos, PingPong, PingPongIR, SIPaxos, Synthetic
+from dslabs_amd.protocols import PB, AmoKV, AmoKVIR, MiniTest, MultiPaxos, PingPong, PingPongIR, SIPaxos, Synthetic
 
 
 def _opt(args, name, default=None):
@@ -13,6 +13,8 @@ def protocol(args):
     if p == "pingpong":
         return PingPong(int(_opt(args, "--clients", 1)), int(_opt(args, "--pings", 10)),
                         check_value="--mutant-no-check" not in args, reset_timer="--mutant-no-reset" not in args)
+    if p == "amokv_ir":  # tests give --clients / --workload (the oracle takes AmoKVIR.oracle_args())
+        return AmoKVIR(int(_opt(args, "--clients", 2)), _opt(args, "--workload", "diffkey3"))
     if p == "pingpong_ir":
         return PingPongIR(int(_opt(args, "--clients", 1)), int(_opt(args, "--pings", 10)),
                           check_value="--mutant-no-check" not in args, reset_timer="--mutant-no-reset" not in args)

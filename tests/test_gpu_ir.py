@@ -40,3 +40,24 @@ def test_ir_pingpong_matches_golden(name, shards):
         assert rep["depth"] == st.depth()
         if r.endCondition() == EndCondition.INVARIANT_VIOLATED:
             assert not all(i["value"] for i in rep["invariants"])
+
+
+KV = json.load(open(os.path.join(HERE, "golden", "amokv.json")))
+KV_NAMES = sorted(n for n in KV if "APPENDS_LINEARIZABLE" not in KV[n]["args"])
+
+
+@pytest.mark.parametrize("name", KV_NAMES)
+def test_ir_amokv_matches_golden(name):
+    """The IR-generated AMO-KV (dslabs_amd/ir/specs/amokv.py) against the hand-written
+    protocol's golden vectors; traces replay on the IR-generated oracle form."""
+    from test_ir import _kv_ir
+    case = KV[name]
+    proto, rest = _kv_ir(case["args"])
+    r = Engine(proto).bfs(proto.initial_state(), argmap.settings(rest, proto, table_log2=22))
+    assert r.endCondition().name == case["end"]
+    assert r.per_depth == case["per_depth"]
+    st = r.invariantViolatingState() or r.goalMatchingState()
+    if st is not None:
+        rep = oracle_util.replay(proto.oracle_args() + [a for a in rest if a != "--finish-level"], st.trace())
+        assert rep["ok"], rep["error"]
+        assert rep["depth"] == st.depth()

@@ -19,6 +19,9 @@ from tools import cpu_baseline
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LAB0 = json.load(open(os.path.join(HERE, "golden", "lab0.json")))
+KV = json.load(open(os.path.join(HERE, "golden", "amokv.json")))
+# AMO-KV fixtures whose predicates the IR covers (RESULTS_OK / CLIENTS_DONE; not APPENDS_LINEARIZABLE)
+KV_NAMES = sorted(n for n in KV if "APPENDS_LINEARIZABLE" not in KV[n]["args"])
 # the engine finishes a terminal's level (--finish-level fixtures) or exhausts the space
 NAMES = sorted(n for n in LAB0 if "--finish-level" in LAB0[n]["args"] or LAB0[n]["end"] == "SPACE_EXHAUSTED")
 
@@ -67,3 +70,36 @@ def test_ir_device_form_host_bfs(protocheck, ps, oracle_args):  # noqa: F811
     want = oracle_util.run("bfs", oracle_args)
     assert got["per_depth"] == want["per_depth"]
     assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
+
+
+def _kv_ir(args):
+    from dslabs_amd.protocols import AmoKVIR
+    c, wl = int(args[args.index("--clients") + 1]), args[args.index("--workload") + 1]
+    rest, i = [], 0
+    while i < len(args):
+        if args[i] in ("--proto", "--clients", "--workload"):
+            i += 2
+            continue
+        rest.append(args[i])
+        i += 1
+    return AmoKVIR(c, wl), rest
+
+
+@pytest.mark.parametrize("name", KV_NAMES)
+def test_ir_amokv_oracle_matches_golden(name):
+    case = KV[name]
+    proto, rest = _kv_ir(case["args"])
+    r = oracle_util.run("bfs", proto.oracle_args() + rest, timeout=600)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
+
+
+@pytest.mark.parametrize("name", KV_NAMES)
+def test_ir_amokv_device_form_on_cpu(name):
+    case = KV[name]
+    if "--finish-level" not in case["args"] and case["end"] != "SPACE_EXHAUSTED":
+        pytest.skip("the oracle stopped mid-level (no --finish-level)")
+    proto, rest = _kv_ir(case["args"])
+    r = cpu_baseline.run(proto, argmap.settings(rest, proto, table_log2=22), threads=2)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]

@@ -225,6 +225,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_PB: return run<PB>(d, s, threads, log2, repeat);
     case DSL_PROTO_MINITEST: return run<MiniTest>(d, s, threads, log2, repeat);
     case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, s, threads, log2, repeat);
+    case DSL_PROTO_AMOKV_IR: return run<AmoKVIR>(d, s, threads, log2, repeat);
   }
   return fprintf(stderr, "unknown protocol\n"), 2;
 }
