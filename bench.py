@@ -25,6 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355X"
+CPU_SAMPLE_S = 10.0  # seconds of timed CPU-baseline searches (a bounded sample)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
 WORKLOADS = {
@@ -109,19 +110,19 @@ def cpu_baseline(proto, settings, depth: int, gpu_per_depth, oracle_args, oracle
     """SURVEY.md §8(d)'s CPU baseline: the multithreaded level-synchronous BFS of
     tools/cpu_bfs.cpp (the reference's BFS worker scheme, Search.java:241-348, over the same packed
     transition functions, a lock-free visited set and a barrier per level) on this host's cores,
-    on the SAME workload and maxDepth as the GPU line; run twice, the second run reported (the
-    first grows its buffers, as the GPU's warmup step does). `oracle_sample` is the scalar
+    on the SAME workload and maxDepth as the GPU line; a warm-up search (it grows the buffers,
+    as the GPU's warmup step does), then repeated searches for a bounded ~10 s sample. `oracle_sample` is the scalar
     string-keyed oracle (oracle/, the reference's object model restated) on a smaller maxDepth: a
     reference-semantics sample, not the baseline."""
     sys.path.insert(0, ROOT)
     from tools import cpu_baseline as cb
     s = settings.clone()
     s.maxDepth(depth)
-    r = cb.run(proto, s, repeat=2)
+    r = cb.run(proto, s, repeat=2, min_seconds=CPU_SAMPLE_S)
     out = {"value": round(r["states_per_s"], 1), "unit": "states/s", "cores": r["threads"],
            "kind": "cpu_ref multithreaded",
-           "sample": f"same workload, maxDepth {depth} ({r['states']} states, {r['elapsed_s']:.3f} s, "
-                     f"{r['threads']} threads, tools/cpu_bfs.cpp)",
+           "sample": f"same workload, maxDepth {depth}: {r['runs']} searches of {r['states']} states in "
+                     f"{r['timed_s']:.2f} s on {r['threads']} threads (tools/cpu_bfs.cpp)",
            "per_depth_equal_gpu": r["per_depth"] == gpu_per_depth[:len(r["per_depth"])]}
     if oracle_depth > 0:
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)

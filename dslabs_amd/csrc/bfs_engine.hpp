@@ -30,6 +30,9 @@
 
 // LDS budget for a k_level chunk's parent rows: with the kernel's ~11 KB of static LDS, 4
 // resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
+#ifndef DSL_QGRID_MIN
+#define DSL_QGRID_MIN 1024  // fewest workgroups of a queued k_level launch
+#endif
 #ifndef DSL_ROWS_LDS_KB
 #define DSL_ROWS_LDS_KB 24
 #endif
@@ -318,8 +321,11 @@ struct BfsEngine : EngineBase {
   // Parents per workgroup chunk: about three passes of 256 lanes at the observed branching,
   // within the LDS budget of 4 resident workgroups per CU; a small level is spread over at least
   // ~1024 workgroups instead (one short pass each), since its time is the serial latency chain
-  // of one chunk, not throughput.
+  // of one chunk, not throughput; a large level gets equal chunks in whole rounds of the
+  // resident workgroups (balanced_chunk).
   static constexpr uint64_t kLevelGrid = 256ull * 16;
+  // k_level workgroups resident at once: 4 per CU (4 waves/SIMD, 256 CUs)
+  static constexpr int kSlots = 1024;
   // Frontier size below which a multi-shard search runs the level replicated (see run()):
   // dsl_engine_config.replicate_below, -1 = default, 0 = never.
   uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 16) : (uint64_t)cfg.replicate_below; }
@@ -327,9 +333,7 @@ struct BfsEngine : EngineBase {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / per);
     int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
-    const int spread = (int)std::max<uint64_t>(1, (F + 1023) / 1024);
-    int pb = std::max(1, std::min({want, lds_max, kLevelBlock, spread}));
-    return pb;
+    return balanced_chunk(F, std::max(1, std::min({want, lds_max, kLevelBlock})), kSlots);
   }
 
   // Enqueues up to kQueue levels of shard 0 (see the members above); returns how many ran.
@@ -372,10 +376,10 @@ struct BfsEngine : EngineBase {
     const int pb_max = std::max(1, std::min({(int)((DSL_ROWS_LDS_KB * 1024) / per), kLevelBlock,
                                              (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) /
                                                    std::max<uint64_t>(avg_events_x16, 1))}));
-    const int spread = 1024;
+    const int spread = kSlots;
     SegTable t0{};
     t0.n = (int32_t)S.seg_cnt.size();
-    t0.pb = (int)std::min<uint64_t>((uint64_t)pb_max, std::max<uint64_t>(1, (S.F + spread - 1) / spread));
+    t0.pb = balanced_chunk(S.F, pb_max, spread);
     for (int q = 0; q < t0.n; q++) {
       t0.base[q] = S.seg_base[q];
       t0.cnt[q] = S.seg_cnt[q];
@@ -419,7 +423,7 @@ struct BfsEngine : EngineBase {
       if (j == 0) DSL_HIP(hipEventRecord(qev[0], stream));
       // grid: one chunk per workgroup at the predicted frontier size (the kernel loops over more)
       const double fpred = (double)S.F * std::pow(growth, (double)j);
-      const int grid = (int)std::min<double>(kLevelGrid, std::max<double>(1024, std::ceil(1.5 * fpred / pb_max)));
+      const int grid = (int)std::min<double>(kLevelGrid, std::max<double>(DSL_QGRID_MIN, std::ceil(1.5 * fpred / pb_max)));
       hipLaunchKernelGGL((k_level<P, false>), dim3(grid), dim3(kLevelBlock), lds, stream, a, prm, dset);
       DSL_HIP(hipGetLastError());
     }

@@ -198,6 +198,9 @@ static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg,
 
 static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, EngineBase** out) {
   switch (d.protocol) {
+#ifdef DSL_ONLY_MULTIPAXOS  // measurement variants (tools/build_variant.sh): one protocol, fast builds
+    case DSL_PROTO_MULTIPAXOS: return make_engine<MultiPaxos>(d, cfg, out);
+#else
     case DSL_PROTO_PINGPONG: return make_engine<PingPong>(d, cfg, out);
     case DSL_PROTO_SIPAXOS: return make_engine<SIPaxos>(d, cfg, out);
     case DSL_PROTO_MULTIPAXOS: return make_engine<MultiPaxos>(d, cfg, out);
@@ -207,6 +210,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_MINITEST: return make_engine<MiniTest>(d, cfg, out);
     case DSL_PROTO_PINGPONG_IR: return make_engine<PingPongIR>(d, cfg, out);
     case DSL_PROTO_AMOKV_IR: return make_engine<AmoKVIR>(d, cfg, out);
+#endif
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
       return DSL_ERR_UNKNOWN_PROTOCOL;

@@ -180,30 +180,37 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 // `base + pidx * NW`, its canonical delta `d`) to be written to `dst`. The rows are written one
 // after another by the whole wavefront, lane L producing words L, L+64, ... of the row
 // (nodestate.hpp: emit_word), so each store instruction covers 256 contiguous bytes and the
-// destination is never read back. The parent row is read with uniform addresses (LDS broadcast
-// or one cache line per 16 lanes). Must be called by all lanes of the wave.
+// destination is never read back. The source lane's delta is read with v_readlane into scalar
+// registers (no LDS round trip per field), every send's merge position is an independent ballot
+// over the parent's records (one per lane), and the parent words are read from `base` (LDS in
+// k_level) with uniform row addresses. Must be called by all lanes of the wave.
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int src) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int src) {
+  return (uint64_t)rl32((uint32_t)v, src) | ((uint64_t)rl32((uint32_t)(v >> 32), src) << 32);
+}
+
 template <class P>
 __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
                                           uint32_t* dst) {
   using L = Layout<P>;
   using Rec = typename P::Rec;
   constexpr int NW = L::kWords, T = (NW + 63) / 64;
+  constexpr int TR = (P::kNetCap + 63) / 64;  // parent records per lane (kNetCap <= 64 * TR)
   unsigned long long mask = __ballot(active);
   const int lane = __lane_id();
   while (mask) {
     const int src = __ffsll((long long)mask) - 1;
     mask &= mask - 1;
-    const uint32_t* pw = base + (uint64_t)__shfl((unsigned long long)pidx, src) * NW;
-    uint32_t* ow = reinterpret_cast<uint32_t*>(__shfl((unsigned long long)(uintptr_t)dst, src));
-    const int node = __shfl(d.node, src);
-    const int m = __shfl(d.out.n, src);
+    const uint32_t* pw = base + rl64(pidx, src) * NW;
+    uint32_t* ow = reinterpret_cast<uint32_t*>(rl64((uint64_t)(uintptr_t)dst, src));
+    const int node = (int)rl32((uint32_t)d.node, src);
+    const int m = (int)rl32((uint32_t)d.out.n, src);
     uint32_t nw[P::kNodeWords];
 #pragma unroll
-    for (int i = 0; i < P::kNodeWords; i++) nw[i] = __shfl(d.nw[i], src);
+    for (int i = 0; i < P::kNodeWords; i++) nw[i] = rl32(d.nw[i], src);
     const int n = Net<P>::size(pw);
-    // the parent's records, one per lane (kNetCap <= 64 * TR): a send's lower bound in the sorted
-    // record array is then one ballot + popcount instead of a dependent binary-search chain
-    constexpr int TR = (P::kNetCap + 63) / 64;
+    // the parent's records, one per lane: a send's lower bound in the sorted record array is one
+    // ballot + popcount
     Rec pr[TR];
 #pragma unroll
     for (int t = 0; t < TR; t++) {
@@ -217,11 +224,8 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
     for (int i = 0; i < P::kMaxSends; i++) {  // constant indices: the send list stays in VGPRs
       if (i < m) {
         Rec r;
-        if constexpr (sizeof(Rec) == 8) {
-          r = (Rec)__shfl((unsigned long long)d.out.r[i], src);
-        } else {
-          r = (Rec)__shfl((unsigned)d.out.r[i], src);
-        }
+        if constexpr (sizeof(Rec) == 8) r = (Rec)rl64((uint64_t)d.out.r[i], src);
+        else r = (Rec)rl32((uint32_t)d.out.r[i], src);
         int lb = 0;
 #pragma unroll
         for (int t = 0; t < TR; t++) lb += __popcll(__ballot(pr[t] < r));
@@ -274,6 +278,16 @@ struct LevelArgs {
   int32_t find;                      // find mode (no table, no rows): the successor whose terminal
   uint64_t find_key;                 // key equals find_key is recorded in terms[0]
 };
+
+// Parents per chunk of a level of F parents: at most pbmax, and the chunks come in whole rounds
+// of `slots` (the workgroups resident at once) -- R = ceil(F / (slots pbmax)) rounds of equal
+// chunks, so the level has no partly filled last round (a round lasts as long as its chunks).
+__host__ __device__ inline int balanced_chunk(uint64_t F, int pbmax, int slots) {
+  const uint64_t per_round = (uint64_t)slots * (uint64_t)(pbmax > 0 ? pbmax : 1);
+  const uint64_t R = F ? (F + per_round - 1) / per_round : 1;
+  const uint64_t pb = (F + (uint64_t)slots * R - 1) / ((uint64_t)slots * R);
+  return (int)(pb < 1 ? 1 : pb > (uint64_t)pbmax ? (uint64_t)pbmax : pb);
+}
 
 // The queue's stop rule: after a level with any of these, the host must act before the next one.
 __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
@@ -335,7 +349,9 @@ template <class P, bool ROUTE>
 __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   constexpr int NWAVE = kLevelBlock / 64;
-  constexpr int NC = P::kMsgClasses + 1;  // handler classes; the last one is the timers'
+  // handler classes: messages, timers, then the events whose handler surely changes nothing
+  // (NoopFilter: counted as successors and never run; they sort last and the passes stop before them)
+  constexpr int NC = P::kMsgClasses + 2;
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // a.PB (max) * NW
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
@@ -349,7 +365,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ int s_cbase[kWin / 64][NC];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
-  __shared__ int s_stop;
+  __shared__ int s_stop, s_weff;
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
   const bool find = a.find != 0;
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
@@ -364,7 +380,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
       const uint64_t c = q < a.nseg ? min<uint64_t>(a.qprev_seg[q * kSegStride], a.segcap) : 0ull;
       uint64_t F = c;
       for (int o = 32; o > 0; o >>= 1) F += __shfl_xor(F, o);
-      const int pb = (int)min<uint64_t>((uint64_t)a.PB, max<uint64_t>(1, (F + a.qspread - 1) / a.qspread));
+      const int pb = balanced_chunk(F, a.PB, a.qspread);
       uint64_t inc = (c + pb - 1) / pb;
       for (int o = 1; o < 64; o <<= 1) {
         const uint64_t v = __shfl_up(inc, o);
@@ -460,7 +476,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const uint32_t* w = rows + j * NW;
           for (int q = lo + sub; q < hi; q += tpp) {
             s_par[q - w0] = (uint8_t)j;
-            s_cls[q - w0] = (uint8_t)event_class<P>(w, prm, set, q - e0);
+            s_cls[q - w0] = (uint8_t)event_class_skip<P>(w, prm, set, q - e0);
           }
         }
       }
@@ -475,7 +491,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const int e0 = off[j];
           const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
           const uint32_t* w = rows + j * NW;
-          for (int q = lo + sub; q < hi; q += tpp) s_cls[q - w0] = (uint8_t)event_class<P>(w, prm, set, q - e0);
+          for (int q = lo + sub; q < hi; q += tpp) s_cls[q - w0] = (uint8_t)event_class_skip<P>(w, prm, set, q - e0);
         }
       }
       __syncthreads();
@@ -504,6 +520,10 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           if (lane >= o) inc += y;
         }
         int run = inc - tot;
+        if (lane == NC - 1) {  // the skipped events: counted, never run
+          s_weff = run;
+          c_succ += (uint32_t)tot;
+        }
         if (lane < NC)
           for (int gr = 0; gr < ng; gr++) {
             const int v = s_cbase[gr][lane];
@@ -526,7 +546,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
       }
       __syncthreads();
       PH_MARK(7);  // classify + sort
-      for (int base = 0; base < wn; base += kLevelBlock) {
+      const int wrun = s_weff;  // the window's events whose handler runs (a prefix of s_perm)
+      for (int base = 0; base < wrun; base += kLevelBlock) {
         const int t = base + tid;
         bool is_valid = false, route = false;
         int dest = 0, j = 0, k = 0, tv = 0, tpi = -1;
@@ -535,7 +556,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         Delta<P> d;  // the successor as a canonical delta of its parent
         d.node = 0;
         d.out.n = 0;
-        if (t < wn) {
+        if (t < wrun) {
           const int u = s_perm[t];
           j = s_par[u];
           k = w0 + u - off[j];
@@ -651,6 +672,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           // a VALID successor reserves a row of its workgroup's segment (one returning atomic per
           // wavefront), then the wavefront writes its rows cooperatively
           const unsigned long long li = wave_reserve(&a.seg_ctr[seg * kSegStride], is_valid);
+#ifdef DSL_X2_RESERVE  // cost probe: a second returning reservation atomic (on a spare counter word)
+          if (wave_reserve(&a.seg_ctr[seg * kSegStride + 8], is_valid) == 0x7777777ull) c_succ += 1000000u;
+#endif
           PH_MARK(5);  // terminal fold + reservation
           const bool fits = is_valid && li < a.segcap;
           const uint64_t idx = (uint64_t)seg * a.segcap + li;
@@ -660,8 +684,22 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
             a.next_event[idx] = (uint32_t)k;
             c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
+#ifdef DSL_X2_NWORK  // cost probe: the successor's event count again
+            {
+              int ne0 = off[j + 1] - off[j];
+              asm volatile("" : "+v"(ne0));
+              if (delta_event_count<P>(w, ne0, d, prm, set) == 77777) c_succ += 1000000u;
+            }
+#endif
           }
           wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+#ifdef DSL_X2_EMIT  // cost probe: the rows written twice (same bytes, same places)
+          {
+            uint64_t j2 = (uint64_t)j;
+            asm volatile("" : "+v"(j2));
+            wave_emit<P>(fits, rows, j2, d, a.next + idx * NW);
+          }
+#endif
           PH_MARK(6);  // history + row emission
           // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
           const bool spill = is_valid && !fits;

@@ -249,9 +249,52 @@ DSL_HD int locate_event(const uint32_t* w, const typename P::Params& prm, const 
 // Handler class of event k (messages: P::msg_class < P::kMsgClasses, timers: P::kMsgClasses).
 template <class P>
 DSL_HD int event_class(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
-  static_assert(P::kMsgClasses >= 1 && P::kMsgClasses < 16, "at most 15 message classes + the timer class");
+  static_assert(P::kMsgClasses >= 1 && P::kMsgClasses < 15, "at most 14 message classes + the timer and skip classes");
   const int e = locate_event<P>(w, prm, set, k);
   return e >= 0 ? P::msg_class(Net<P>::at(w, e)) : P::kMsgClasses;
+}
+
+// Events whose handler surely changes nothing: a protocol may provide
+//   static bool surely_noop(int node, const uint32_t* w, Rec r, const Params&)
+//   static bool surely_noop_timer(int node, const uint32_t* w, int timer, const Params&)
+// (w = the whole state row) returning true only when the event surely returns STEP_OK with the
+// node's words unchanged and every send already in the network (the successor is the parent;
+// `false` whenever unsure). k_level counts such an event as a successor (Search.java:481-485: it
+// is generated, then found in the visited set) without running its handler; tests/hostcheck
+// checks the implication on every explored event. event_class_skip returns kMsgClasses + 1 for them.
+template <class P, class = void>
+struct NoopFilter {
+  static DSL_HD bool msg(int, const uint32_t*, typename P::Rec, const typename P::Params&) { return false; }
+};
+template <class P>
+struct NoopFilter<P, std::void_t<decltype(&P::surely_noop)>> {
+  static DSL_HD bool msg(int i, const uint32_t* w, typename P::Rec r, const typename P::Params& prm) {
+    return P::surely_noop(i, w, r, prm);
+  }
+};
+template <class P, class = void>
+struct NoopTimerFilter {
+  static DSL_HD bool timer(int, const uint32_t*, int, const typename P::Params&) { return false; }
+};
+template <class P>
+struct NoopTimerFilter<P, std::void_t<decltype(&P::surely_noop_timer)>> {
+  static DSL_HD bool timer(int i, const uint32_t* w, int t, const typename P::Params& prm) {
+    return P::surely_noop_timer(i, w, t, prm);
+  }
+};
+
+template <class P>
+DSL_HD int event_class_skip(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
+  const int e = locate_event<P>(w, prm, set, k);
+  if (e < 0) {
+    if (e == INT32_MIN) return P::kMsgClasses;
+    const int x = -1 - e;
+    return NoopTimerFilter<P>::timer(x >> 8, w, x & 255, prm) ? P::kMsgClasses + 1 : P::kMsgClasses;
+  }
+  const auto r = Net<P>::at(w, e);
+  const int i = P::rec_to(r);
+  if (i < P::num_nodes(prm) && NoopFilter<P>::msg(i, w, r, prm)) return P::kMsgClasses + 1;
+  return P::msg_class(r);
 }
 
 // A successor as a delta of its parent.

@@ -91,7 +91,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
   const char* end = "SPACE_EXHAUSTED";
   int tdepth = -1;
   long long nterm[3] = {0, 0, 0};
-  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0, dup_sends = 0;
+  long long fp_mismatch = 0, emit_mismatch = 0, judge_mismatch = 0, noop = 0, succ = 0, dup_sends = 0, skipped = 0, skip_mismatch = 0;
   if (v >= V_TERM_EXCEPTION) {
     end = v == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
     tdepth = 0;
@@ -107,6 +107,11 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     for (int k = 0; k < ne; k++) {
       Delta<P> dl;
       const int rc = delta_step<P>(n.s.w, k, dl, prm, set);
+      if (event_class_skip<P>(n.s.w, prm, set, k) == P::kMsgClasses + 1) {  // the kernels skip its handler
+        skipped++;
+        if (rc != STEP_OK || dl.out.n != 0 || !same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords))
+          skip_mismatch++;
+      }
       if (rc == STEP_NULL) continue;
       if (rc == STEP_OVERFLOW) {
         printf("{\"error\":\"overflow\"}\n");
@@ -122,7 +127,9 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
         best = std::min(best, (int)V_TERM_EXCEPTION);
         continue;
       }
-      if (dl.out.n == 0 && same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords)) noop++;
+      const bool is_noop = dl.out.n == 0 && same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords);
+      if (is_noop) noop++;
+
       if constexpr (SendsDistinct<P>::value) {  // P::kSendsDistinct: no record sent twice in one step
         if (!sends_distinct<P>(n.s.w, k, prm, set)) dup_sends++;
       }
@@ -166,8 +173,8 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     end = best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN" : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED" : "GOAL_FOUND";
   unsigned long long total = 0;
   printf("{\"end\":\"%s\",\"terminal_depth\":%d,\"state_bytes\":%d,\"fp_mismatch\":%lld,\"emit_mismatch\":%lld,"
-         "\"judge_mismatch\":%lld,\"dup_sends\":%lld,\"per_depth\":[", end, tdepth, (int)sizeof(S), fp_mismatch,
-         emit_mismatch, judge_mismatch, dup_sends);
+         "\"judge_mismatch\":%lld,\"dup_sends\":%lld,\"skip_mismatch\":%lld,\"skipped\":%lld,\"per_depth\":[", end, tdepth,
+         (int)sizeof(S), fp_mismatch, emit_mismatch, judge_mismatch, dup_sends, skip_mismatch, skipped);
   for (size_t i = 0; i < per.size(); i++) {
     printf("%s%llu", i ? "," : "", per[i]);
     total += per[i];

@@ -136,6 +136,7 @@ def test_encoding_matches_oracle(protocheck, name):
     assert got["per_depth"] == want["per_depth"]
     assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
     assert got["dup_sends"] == 0
+    assert got["skip_mismatch"] == 0  # every event k_level skips (NoopFilter) is a true no-op
 
 
 def test_device_viewserver_passes_reference_unit_tests(protocheck):

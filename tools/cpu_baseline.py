@@ -52,7 +52,7 @@ def default_threads() -> int:
 
 
 def run(proto, settings, threads: int | None = None, table_log2: int | None = None, repeat: int = 1,
-        timeout: float = 600) -> dict:
+        timeout: float = 600, min_seconds: float = 0.0) -> dict:
     exe = build()
     state = proto.initial_state()
     blob = bytes(proto.desc()) + bytes(settings._encode(state))
@@ -63,7 +63,7 @@ def run(proto, settings, threads: int | None = None, table_log2: int | None = No
         f.write(blob)
         path = f.name
     try:
-        out = subprocess.run([exe, path, str(threads), str(log2), str(repeat)], check=True, capture_output=True, text=True,
+        out = subprocess.run([exe, path, str(threads), str(log2), str(repeat), str(min_seconds)], check=True, capture_output=True, text=True,
                              timeout=timeout)
     finally:
         os.unlink(path)

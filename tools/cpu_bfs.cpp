@@ -13,11 +13,13 @@
 // counts follow exploreNode (every new successor counts, terminal and pruned ones included), so
 // per-depth vectors equal the GPU's and the oracle's (tests/test_cpu_bfs.py).
 //
-// usage: cpu_bfs <blob> <threads> <table_log2> [repeat]
+// usage: cpu_bfs <blob> <threads> <table_log2> [repeat [min_seconds]]
 //   blob = dsl_protocol_desc bytes followed by dsl_settings bytes (bench.py writes it); with
-//   repeat > 1 the search runs that many times on the same buffers and the last run is reported
-//   (the first one grows the frontier buffers, as bench.py's GPU warmup step does)
-// prints one JSON line: end, per_depth, states, elapsed_s, threads, states_per_s
+//   repeat > 1 the search runs that many times on the same buffers and the runs after the first
+//   are timed (the first one grows the frontier buffers, as bench.py's GPU warmup step does);
+//   min_seconds > 0 repeats the timed runs until they add up to that much time
+// prints one JSON line: end, per_depth, states (per run), elapsed_s (last run), threads,
+// states_per_s (timed runs' states / their time), runs, timed_s
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -55,7 +57,8 @@ struct VisitedSet {
 };
 
 template <class P>
-int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int table_log2, int repeat) {
+int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int table_log2, int repeat,
+        double min_s) {
   const typename P::Params prm = P::from_desc(d);
   if (!P::valid(prm)) return fprintf(stderr, "invalid params\n"), 2;
   DevSettings set;
@@ -79,8 +82,11 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
   std::vector<unsigned long long> per;
   int best = 99;
   const char* err = nullptr;
-  double el = 0;
-  for (int run = 0; run < repeat && !err; run++) {
+  double el = 0, timed = 0;
+  int timed_runs = 0;
+  // the first run only grows the buffers (the GPU's warmup step); with min_s > 0 the timed runs
+  // repeat until they add up to at least min_s seconds (a bounded sample of ~10 s of CPU work)
+  for (int run = 0; !err && (run < repeat || (min_s > 0 && timed < min_s)); run++) {
   const auto t0 = std::chrono::steady_clock::now();
   {  // the visited set starts empty (cleared by all threads)
     std::vector<std::thread> pool;
@@ -188,6 +194,10 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
     std::swap(cur, nxt);
   }
   el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (run > 0 || repeat == 1) {
+    timed += el;
+    timed_runs++;
+  }
   }
   if (err) return fprintf(stderr, "error: %s\n", err), 3;
   while (per.size() > 1 && per.back() == 0) per.pop_back();
@@ -197,8 +207,9 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
                     : best == V_TERM_EXCEPTION ? "EXCEPTION_THROWN"
                     : best == V_TERM_INVARIANT ? "INVARIANT_VIOLATED"
                                                : "GOAL_FOUND";
-  printf("{\"end\":\"%s\",\"states\":%llu,\"elapsed_s\":%.6f,\"threads\":%d,\"states_per_s\":%.1f,\"per_depth\":[",
-         end, total, el, threads, total / el);
+  printf("{\"end\":\"%s\",\"states\":%llu,\"elapsed_s\":%.6f,\"threads\":%d,\"states_per_s\":%.1f,"
+         "\"runs\":%d,\"timed_s\":%.6f,\"per_depth\":[",
+         end, total, el, threads, (double)total * timed_runs / timed, timed_runs, timed);
   for (size_t i = 0; i < per.size(); i++) printf("%s%llu", i ? "," : "", per[i]);
   printf("]}\n");
   return 0;
@@ -207,7 +218,7 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
 }  // namespace
 
 int main(int argc, char** argv) {
-  if (argc < 4) return fprintf(stderr, "usage: cpu_bfs <blob> <threads> <table_log2> [repeat]\n"), 2;
+  if (argc < 4) return fprintf(stderr, "usage: cpu_bfs <blob> <threads> <table_log2> [repeat [min_seconds]]\n"), 2;
   dsl_protocol_desc d;
   dsl_settings s;
   FILE* f = fopen(argv[1], "rb");
@@ -216,16 +227,17 @@ int main(int argc, char** argv) {
   fclose(f);
   const int threads = std::max(1, atoi(argv[2])), log2 = std::max(10, std::min(36, atoi(argv[3])));
   const int repeat = argc > 4 ? std::max(1, atoi(argv[4])) : 1;
+  const double min_s = argc > 5 ? atof(argv[5]) : 0.0;
   switch (d.protocol) {
-    case DSL_PROTO_PINGPONG: return run<PingPong>(d, s, threads, log2, repeat);
-    case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, s, threads, log2, repeat);
-    case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, s, threads, log2, repeat);
-    case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, s, threads, log2, repeat);
-    case DSL_PROTO_AMOKV: return run<AmoKV>(d, s, threads, log2, repeat);
-    case DSL_PROTO_PB: return run<PB>(d, s, threads, log2, repeat);
-    case DSL_PROTO_MINITEST: return run<MiniTest>(d, s, threads, log2, repeat);
-    case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, s, threads, log2, repeat);
-    case DSL_PROTO_AMOKV_IR: return run<AmoKVIR>(d, s, threads, log2, repeat);
+    case DSL_PROTO_PINGPONG: return run<PingPong>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_SIPAXOS: return run<SIPaxos>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_MULTIPAXOS: return run<MultiPaxos>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_SYNTHETIC: return run<Synthetic>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_AMOKV: return run<AmoKV>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_PB: return run<PB>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_MINITEST: return run<MiniTest>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, s, threads, log2, repeat, min_s);
+    case DSL_PROTO_AMOKV_IR: return run<AmoKVIR>(d, s, threads, log2, repeat, min_s);
   }
   return fprintf(stderr, "unknown protocol\n"), 2;
 }
