@@ -213,12 +213,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
+    # DSL_BENCH_SHARE_DEVICE=1 (rehearsal on a one-GPU box, never a bench line): every rank on
+    # device 0, torch's own group over gloo; the engine's RCCL communicator is the one under test
+    share = os.environ.get("DSL_BENCH_SHARE_DEVICE") == "1"
+    device = 0 if share else local_rank
+    torch.cuda.set_device(device)
     dist = None
     comm_id = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         from dslabs_amd import _lib
         lib = _lib.load()
         import ctypes
@@ -233,7 +240,7 @@ def main():
     wl = WORKLOADS[args.workload]
     depth = args.depth if args.depth is not None else wl["depth"]
     proto, settings, oracle_args = build_search(args.workload, depth)
-    eng = Engine(proto, device=local_rank, rank=rank, world_size=world, comm_id=comm_id)
+    eng = Engine(proto, device=device, rank=rank, world_size=world, comm_id=comm_id)
     state = proto.initial_state()
 
     def barrier():
@@ -253,7 +260,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if share else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = eng.kernel_stats()
