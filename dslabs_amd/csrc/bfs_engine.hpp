@@ -108,7 +108,6 @@ struct BfsEngine : EngineBase {
     TerminalRec* terms = nullptr;
     unsigned char* find_ctr = nullptr;  // scratch counter sets of a find-mode k_level
     RouteCounters* rc = nullptr;
-    int32_t* seed = nullptr;
     FpRec* out_fp = nullptr;
     uint64_t out_fp_cap = 0;
     FpRec* in_fp = nullptr;
@@ -211,7 +210,7 @@ struct BfsEngine : EngineBase {
 
   ~BfsEngine() override {
     for (auto& s : sh) {
-      void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,     s.seed,
+      void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,
                       s.out_fp,    s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
                       s.find_ctr};
       for (void* q : ptrs) (void)hipFree(q);
@@ -543,10 +542,9 @@ struct BfsEngine : EngineBase {
         S.table = nullptr;
         DSL_HIP(hipMalloc(&S.table, buckets * 64));
       }
-      DSL_HIP(hipMemsetAsync(S.table, 0, buckets * 64, stream));
+      // the table, counter sets and route counters are zeroed by k_setup (below)
       if (!S.ctrbuf) DSL_HIP(hipMalloc(&S.ctrbuf, 2 * kCtrSet));
       if (!S.hctr) DSL_HIP(hipHostMalloc(&S.hctr, kCtrSet + sizeof(RouteCounters)));
-      DSL_HIP(hipMemsetAsync(S.ctrbuf, 0, 2 * kCtrSet, stream));
       S.cset = 0;
       S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf);
       S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + kCtrSegOff);
@@ -556,10 +554,8 @@ struct BfsEngine : EngineBase {
         DSL_HIP(hipMalloc(&S.terms, sizeof(TerminalRec) * term_cap));
       }
       if (!S.rc) DSL_HIP(hipMalloc(&S.rc, sizeof(RouteCounters)));
-      if (!S.seed) DSL_HIP(hipMalloc(&S.seed, 4 * sizeof(int32_t)));
       S.seg_base.clear();
       S.seg_cnt.clear();
-      DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
       DSL_TRY(grow_rows(&S.cur, &S.cur_cap, 1024, false, 0));
       DSL_TRY(grow_rows(&S.next, &S.next_cap, 1024, false, 0));
       DSL_TRY(grow(&S.cur_fp, &S.curfp_cap, 1024, false, 0));
@@ -601,7 +597,7 @@ struct BfsEngine : EngineBase {
     bool rep_active = W > 1 && rep_threshold() > 0;
     bool first_sharded = W > 1 && !rep_active;
     // checkState of the initial state: the same judge, on the host (no round trip before the
-    // first level); k_seed only inserts its fingerprint
+    // first level); k_setup only inserts its fingerprint
     {
       int pi = -1;
       const NodeView v0{init.w, P::kNodeWords, -1, nullptr};
@@ -609,16 +605,28 @@ struct BfsEngine : EngineBase {
       init_enc = ((uint64_t)v << 32) | (uint32_t)(pi + 1);
     }
     for (auto& S : sh) {
-      if (S.gid != init_owner && !rep_active) continue;
-      // staged through the pinned counter buffer: a pageable source would make the copies synchronous
-      static_assert(sizeof(init) + sizeof(Fp) <= (size_t)kCtrSet, "initial state larger than the staging buffer");
-      std::memcpy(S.hctr, init.w, NW * 4);
-      std::memcpy(S.hctr + NW * 4, &init_fp, sizeof(Fp));
-      DSL_HIP(hipMemcpyAsync(S.cur, S.hctr, NW * 4, hipMemcpyHostToDevice, stream));
-      DSL_HIP(hipMemcpyAsync(S.cur_fp, S.hctr + NW * 4, sizeof(Fp), hipMemcpyHostToDevice, stream));
-      Table t = tbl_proto;
-      t.slots = S.table;
-      hipLaunchKernelGGL(k_seed<P>, dim3(1), dim3(64), 0, stream, S.cur, S.cur_fp, prm, dset, t, init_depth, S.seed);
+      // one k_setup per shard: zeroes its table and counters; seeds the initial state's owner (or
+      // every shard while small levels are replicated)
+      const bool seed = S.gid == init_owner || rep_active;
+      SetupArgs<P> sa{};
+      sa.table = reinterpret_cast<uint4*>(S.table);
+      sa.n_table = buckets * 4;
+      sa.ctr = reinterpret_cast<uint4*>(S.ctrbuf);
+      sa.n_ctr = 2 * kCtrSet / 16;
+      sa.rc = reinterpret_cast<uint4*>(S.rc);
+      sa.n_rc = (int32_t)((sizeof(RouteCounters) + 15) / 16);
+      static_assert(sizeof(RouteCounters) % 16 == 0, "RouteCounters is zeroed in 16-byte units");
+      sa.seed = seed ? 1 : 0;
+      sa.home = ((init_fp.lo & (buckets - 1)) << 3) | ((init_fp.lo >> 28) & 7);  // table_home
+      sa.key = (unsigned long long)(init_fp.hi | 1ull);
+      sa.cur = S.cur;
+      sa.cur_fp = S.cur_fp;
+      sa.fp = init_fp;
+      std::memcpy(sa.init, init.w, NW * 4);
+      const int sgrid = (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, sa.n_table / kBlock));
+      hipLaunchKernelGGL(k_setup<P>, dim3(sgrid), dim3(kBlock), 0, stream, sa);
+      DSL_HIP(hipGetLastError());
+      if (!seed) continue;
       S.F = 1;
       S.seg_base.assign(1, 0);
       S.seg_cnt.assign(1, 1);

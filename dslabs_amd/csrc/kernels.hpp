@@ -766,17 +766,48 @@ __global__ void __launch_bounds__(kBlock) k_unspill(const uint64_t* items, uint6
   block_flush(s_red, &ctr->next_work, c_next_work);
 }
 
-// Inserts the initial state's fingerprint and judges it (BFS.initSearch + exploreNode's
-// initial-state check, Search.java:434-440, :470-480).
+// Search setup in one launch (it replaces three memsets, two copies and k_seed): zeroes the
+// visited table, the level counter sets and the route counters, and -- on the shard that holds the
+// initial state -- writes the initial row and fingerprint to frontier row 0 and its key into its
+// home slot (BFS.initSearch's discovered.add, Search.java:434-440: in an empty table the first
+// probe is the home slot). The initial state is judged on the host (bfs_engine.hpp).
 template <class P>
-__global__ void k_seed(const uint32_t* init, const Fp* fp, typename P::Params prm, DevSettings set, Table table,
-                       int depth, int32_t* out /* [verdict, pred_index, insert_rc] */) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    out[2] = table_insert(table, *fp);
-    int pi = -1;
-    const NodeView v{init, P::kNodeWords, -1, nullptr};
-    out[0] = judge_view<P>(v, prm, set, depth, &pi);
-    out[1] = pi;
+struct SetupArgs {
+  uint4* table;       // n_table 16-byte units (two slots each)
+  uint64_t n_table;
+  uint4* ctr;         // n_ctr 16-byte units
+  int32_t n_ctr;
+  uint4* rc;
+  int32_t n_rc;
+  int32_t seed;       // this shard holds the initial state
+  uint64_t home;      // its home slot
+  unsigned long long key;
+  uint32_t* cur;
+  Fp* cur_fp;
+  Fp fp;
+  uint32_t init[Layout<P>::kWords];
+};
+
+template <class P>
+__global__ void __launch_bounds__(kBlock) k_setup(SetupArgs<P> a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t hu = a.seed ? a.home >> 1 : ~0ull;
+  for (uint64_t u = tid; u < a.n_table; u += stride) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (u == hu) {
+      if (a.home & 1) v = make_uint4(0, 0, (uint32_t)a.key, (uint32_t)(a.key >> 32));
+      else v = make_uint4((uint32_t)a.key, (uint32_t)(a.key >> 32), 0, 0);
+    }
+    a.table[u] = v;
+  }
+  if (blockIdx.x == 0) {
+    for (int i = threadIdx.x; i < a.n_ctr; i += blockDim.x) a.ctr[i] = make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < a.n_rc; i += blockDim.x) a.rc[i] = make_uint4(0, 0, 0, 0);
+    if (a.seed) {
+      for (int i = threadIdx.x; i < Layout<P>::kWords; i += blockDim.x) a.cur[i] = a.init[i];
+      if (threadIdx.x == 0) *a.cur_fp = a.fp;
+    }
   }
 }
 
