@@ -361,6 +361,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
   __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kLevelBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[NWAVE];
+  __shared__ unsigned long long s_red5[NWAVE * 5];
   __shared__ int s_wsum[NWAVE];
   __shared__ int s_cbase[kWin / 64][NC];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
@@ -498,6 +499,32 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 #endif
       // 3b. class counts per 64-item group (ballots), bases in class-major order
       const int ng = (wn + 63) >> 6;
+      if (ng == 1) {
+        // one group (every small level): wave 0 sorts it alone, in registers, with one barrier
+        if (wid == 0) {
+          const int c = lane < wn ? (int)s_cls[lane] : -1;
+          int mine = 0, rank = 0;
+#pragma unroll
+          for (int q = 0; q < NC; q++) {
+            const unsigned long long mq = __ballot(c == q);
+            if (lane == q) mine = __popcll(mq);
+            if (c == q) rank = __popcll(mq & ((1ull << lane) - 1ull));
+          }
+          int inc = mine;
+          for (int o = 1; o < 16; o <<= 1) {
+            const int y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+          }
+          const int run = inc - mine;  // lane q < NC: the first position of class q
+          if (lane == NC - 1) {        // the skipped events: counted, never run
+            s_weff = run;
+            c_succ += (uint32_t)mine;
+          }
+          const int b = __shfl(run, c < 0 ? 0 : c);
+          if (lane < wn) s_perm[b + rank] = (uint16_t)lane;
+        }
+        __syncthreads();
+      } else {
       for (int gr = wid; gr < ng; gr += NWAVE) {
         const int t = gr * 64 + lane;
         const int c = t < wn ? (int)s_cls[t] : -1;
@@ -545,6 +572,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         if (t < wn) s_perm[s_cbase[gr][c] + rank] = (uint16_t)t;
       }
       __syncthreads();
+      }
       PH_MARK(7);  // classify + sort
       const int wrun = s_weff;  // the window's events whose handler runs (a prefix of s_perm)
       for (int base = 0; base < wrun; base += kLevelBlock) {
@@ -722,11 +750,24 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   }
   PH_FLUSH(s_red, a.ctr);
   PH_CLS_FLUSH(a.ctr);
-  block_flush<kLevelBlock>(s_red, &a.ctr->successors, c_succ);
-  block_flush<kLevelBlock>(s_red, &a.ctr->new_states, c_new);
-  block_flush<kLevelBlock>(s_red, &a.ctr->next_work, c_next_work);
-  block_flush<kLevelBlock>(s_red, &a.ctr->work_items, c_work);
-  block_flush<kLevelBlock>(s_red, &a.ctr->probes, c_probe);
+  {  // the five statistics in one workgroup reduction (one barrier pair, five atomics)
+    unsigned long long v[5] = {c_succ, c_new, c_next_work, c_work, c_probe};
+#pragma unroll
+    for (int i = 0; i < 5; i++)
+      for (int o = 32; o > 0; o >>= 1) v[i] += __shfl_xor(v[i], o);
+    __syncthreads();
+    if (lane == 0)
+#pragma unroll
+      for (int i = 0; i < 5; i++) s_red5[wid * 5 + i] = v[i];
+    __syncthreads();
+    if (tid < 5) {
+      unsigned long long t = 0;
+      for (int w = 0; w < NWAVE; w++) t += s_red5[w * 5 + tid];
+      unsigned long long* dst = tid == 0 ? &a.ctr->successors : tid == 1 ? &a.ctr->new_states
+                                : tid == 2 ? &a.ctr->next_work : tid == 3 ? &a.ctr->work_items : &a.ctr->probes;
+      if (t) atomicAdd(dst, t);
+    }
+  }
 }
 
 // Materializes spilled VALID states (already inserted, counted and judged) at next_size.
