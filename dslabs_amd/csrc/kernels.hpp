@@ -435,7 +435,24 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 #endif
     // 2. enabled events per parent (SearchState.events), workgroup exclusive scan (wave scans)
     int total;
-    {
+    if (pb <= 64) {  // one wave's worth of parents: wave 0 scans them alone, one barrier
+      if (wid == 0) {
+        int x = 0;
+        if (lane < pb)
+          x = (ROUTE && a.owner_filter && owner_of(fps[lane], a.W) != a.me) ? 0
+                                                                           : count_events<P>(rows + lane * NW, prm, set);
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(x, o);
+          if (lane >= o) x += y;
+        }
+        if (lane < pb) off[lane + 1] = x;
+        if (lane == 0) off[0] = 0;
+        if (lane == 63) s_wsum[0] = x;
+      }
+      __syncthreads();
+      total = s_wsum[0];
+      if (tid == 0) c_work += (uint32_t)total;
+    } else {
       int x = 0;
       if (tid < pb)
         x = (ROUTE && a.owner_filter && owner_of(fps[tid], a.W) != a.me) ? 0
@@ -744,7 +761,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
         }
       }
-      __syncthreads();  // the window's LDS arrays are reused by the next window
+      if (w0 + kWin < total) __syncthreads();  // the window's LDS arrays are reused by the next window
     }
     __syncthreads();  // LDS is reused by the next chunk
   }
