@@ -35,6 +35,9 @@ constexpr int kMaxShards = 16;
 #define DSL_KWIN 1024
 #endif
 constexpr int kWin = DSL_KWIN;  // work items per class-sorted window of k_level
+// Levels of at most this many chunks (one round of the 1,024 resident workgroups) spread each
+// pass over all of a workgroup's waves (k_level step 4).
+constexpr int kSpreadChunks = 1024;
 // The next frontier is written into up to kSegs segments, one reservation counter each (a
 // workgroup appends to segment blockIdx % nseg), so every wavefront reserves its rows with one
 // returning atomic and no workgroup barrier, and no counter word carries more than 1/kSegs of
@@ -411,6 +414,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     for (int i = tid; i < kCtrSet / 16; i += blockDim.x) a.zero_next[i] = make_uint4(0, 0, 0, 0);
   const int PB = s_segs.pb;
   const uint64_t nchunks = s_segs.chunk0[s_segs.n];
+  const bool spread = nchunks <= (uint64_t)kSpreadChunks;
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
   int g = 0;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
@@ -593,7 +597,15 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
       PH_MARK(7);  // classify + sort
       const int wrun = s_weff;  // the window's events whose handler runs (a prefix of s_perm)
       for (int base = 0; base < wrun; base += kLevelBlock) {
-        const int t = base + tid;
+        // a pass of r <= 256 items. In a level of at most one round of chunks (latency-bound:
+        // every chunk runs at once) each wave takes an equal contiguous share of the class-sorted
+        // items -- a short pass spread over all four waves has fewer handler classes, probes and
+        // emitted rows per wave, so a shorter critical path; in a larger level (throughput-bound)
+        // the waves are filled in order, which issues fewer half-empty wave instructions
+        const int r = min(kLevelBlock, wrun - base);
+        const int per = spread ? (r + NWAVE - 1) / NWAVE : 64;
+        const int t = base + wid * per + lane;
+        const bool live = lane < per && t < base + r;
         bool is_valid = false, route = false;
         int dest = 0, j = 0, k = 0, tv = 0, tpi = -1;
         uint64_t tkey = ~0ull;  // terminal candidate
@@ -601,7 +613,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         Delta<P> d;  // the successor as a canonical delta of its parent
         d.node = 0;
         d.out.n = 0;
-        if (t < wrun) {
+        if (live) {
           const int u = s_perm[t];
           j = s_par[u];
           k = w0 + u - off[j];
