@@ -181,9 +181,9 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 
 // Wave-cooperative row emission: every lane with `active` has a successor (its parent row
 // `base + pidx * NW`, its canonical delta `d`) to be written to `dst`. The rows are written one
-// after another by the whole wavefront, lane L producing words L, L+64, ... of the row
-// (nodestate.hpp: emit_word), so each store instruction covers 256 contiguous bytes and the
-// destination is never read back. The source lane's delta is read with v_readlane into scalar
+// after another by the whole wavefront, lane L producing words 4L .. 4L+3 (+256 t) of the row
+// (nodestate.hpp: emit_word) as one 16-byte store, so each store instruction covers up to 1 KiB
+// of contiguous bytes and the destination is never read back. The source lane's delta is read with v_readlane into scalar
 // registers (no LDS round trip per field), every send's merge position is an independent ballot
 // over the parent's records (one per lane), and the parent words are read from `base` (LDS in
 // k_level) with uniform row addresses. Must be called by all lanes of the wave.
@@ -197,7 +197,10 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
                                           uint32_t* dst) {
   using L = Layout<P>;
   using Rec = typename P::Rec;
-  constexpr int NW = L::kWords, T = (NW + 63) / 64;
+  // lane L writes words 4 (L + 64 t) .. +3 of the row as one 16-byte store (kWords is a multiple
+  // of 4): one store instruction per 1 KiB of row
+  constexpr int NW = L::kWords, NQ = NW / 4, T = (NQ + 63) / 64;
+  static_assert(NW % 4 == 0, "rows are whole 16-byte units");
   constexpr int TR = (P::kNetCap + 63) / 64;  // parent records per lane (kNetCap <= 64 * TR)
   unsigned long long mask = __ballot(active);
   const int lane = __lane_id();
@@ -220,9 +223,9 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
       const int q = lane + 64 * t;
       pr[t] = q < n ? Net<P>::at(pw, q) : ~(Rec)0;
     }
-    EmitAcc acc[T];
+    EmitAcc acc[4 * T];
 #pragma unroll
-    for (int t = 0; t < T; t++) acc[t] = EmitAcc{0u, 0, 0};
+    for (int t = 0; t < 4 * T; t++) acc[t] = EmitAcc{0u, 0, 0};
 #pragma unroll
     for (int i = 0; i < P::kMaxSends; i++) {  // constant indices: the send list stays in VGPRs
       if (i < m) {
@@ -234,13 +237,21 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
         for (int t = 0; t < TR; t++) lb += __popcll(__ballot(pr[t] < r));
         const int pos = lb + i;
 #pragma unroll
-        for (int t = 0; t < T; t++) emit_acc_send<P>(acc[t], lane + 64 * t, r, pos);
+        for (int t = 0; t < 4 * T; t++) emit_acc_send<P>(acc[t], 4 * (lane + 64 * (t >> 2)) + (t & 3), r, pos);
       }
     }
 #pragma unroll
     for (int t = 0; t < T; t++) {
-      const int o = lane + 64 * t;
-      if (o < NW) ow[o] = emit_word<P>(pw, n, m, node, nw, o, acc[t]);
+      const int q = lane + 64 * t;
+      if (q < NQ) {
+        const int o = 4 * q;
+        uint4 v;
+        v.x = emit_word<P>(pw, n, m, node, nw, o, acc[4 * t]);
+        v.y = emit_word<P>(pw, n, m, node, nw, o + 1, acc[4 * t + 1]);
+        v.z = emit_word<P>(pw, n, m, node, nw, o + 2, acc[4 * t + 2]);
+        v.w = emit_word<P>(pw, n, m, node, nw, o + 3, acc[4 * t + 3]);
+        reinterpret_cast<uint4*>(ow)[q] = v;
+      }
     }
   }
 }

@@ -70,7 +70,9 @@ def test_time_limit_ends_queued_search(secs):
         for run in range(2):  # the first run also allocates the table; the second has a queue time
             r = e.bfs(proto.initial_state(), s)
             assert r.endCondition().name == "TIME_EXHAUSTED"
-            assert r.elapsed_s < secs + 0.25
+            # the first run also grows every buffer (hipMalloc of up to GiBs on a fresh device,
+            # slow and variable); the second one reuses them and must stop right after the limit
+            assert r.elapsed_s < secs + (2.0 if run == 0 else 0.25), (run, r.elapsed_s)
             n = min(len(r.per_depth), len(case["per_depth"]))
             assert r.per_depth[:n] == case["per_depth"][:n]
             if run:
