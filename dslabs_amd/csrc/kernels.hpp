@@ -296,7 +296,11 @@ struct LevelArgs {
 // Parents per chunk of a level of F parents: at most pbmax, and the chunks come in whole rounds
 // of `slots` (the workgroups resident at once) -- R = ceil(F / (slots pbmax)) rounds of equal
 // chunks, so the level has no partly filled last round (a round lasts as long as its chunks).
+// The frontier is up to kMaxSegs row ranges, each rounded up to whole chunks, so the rounds are
+// sized for slots - kMaxSegs chunks: a one-round level never spills a few chunks into a second
+// round (measured: C5 level 8, 4,050 parents in 32 segments, took 45 or 80 us by that rounding).
 __host__ __device__ inline int balanced_chunk(uint64_t F, int pbmax, int slots) {
+  if (slots > 2 * kMaxSegs) slots -= kMaxSegs;
   const uint64_t per_round = (uint64_t)slots * (uint64_t)(pbmax > 0 ? pbmax : 1);
   const uint64_t R = F ? (F + per_round - 1) / per_round : 1;
   const uint64_t pb = (F + (uint64_t)slots * R - 1) / ((uint64_t)slots * R);
