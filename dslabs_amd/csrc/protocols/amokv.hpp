@@ -141,6 +141,24 @@ struct AmoKV {
   // ClientTimers are all (100, 100): only the head of the queue is deliverable
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params&) { return i > 0 && ntim(w) > 0; }
 
+  // Deliveries that surely change nothing (nodestate.hpp NoopFilter), read off on_message below:
+  // a superseded Request at the server (seq below the client's last: no reply, no state), and a
+  // Reply the client neither takes (handleReply) nor lets the worker loop act on. The server's
+  // cached re-reply (seq == last) is not claimed: its Reply may or may not be in the network.
+  static DSL_HD bool surely_noop(int i, const uint32_t* row, Rec m, const Params& p) {
+    const uint32_t* w = row + i * kNodeWords;
+    if (i == 0) {
+      if (m_type(m) != M_REQUEST) return false;
+      const int c = rec_from(m) - 1, seq = m_seq(m);
+      if (c < 0 || c >= p.clients || seq < 1 || seq > p.ncmds) return false;  // throws
+      return seq < (int)(sel_word<kNodeWords>(w, 3 + c) & 3);
+    }
+    if (m_type(m) != M_REPLY) return false;
+    const int n = nres(w), s = seq_of(w);
+    if (n < s && !has_result(w) && m_seq(m) == s) return false;  // handleReply takes it
+    return !(n < s && has_result(w)) && !(n == s && s < p.ncmds);  // worker_continue idle
+  }
+
   template <class O>
   static DSL_HD int on_message(int i, uint32_t* w, Rec m, O& out, const Params& p) {
     if (i == 0) {
