@@ -287,7 +287,7 @@ struct LevelArgs {
   const LevelCounters* qprev;        // null: the table is `segs`
   const unsigned long long* qprev_seg;
   uint64_t qflimit, qwlimit;         // the queue stops above these frontier / work sizes
-  int32_t qspread;                   // parents per chunk = ceil(F / qspread), at most PB
+  int32_t qspread;                   // resident workgroups: parents per chunk = balanced_chunk(F, PB, qspread)
   uint32_t term_cap;                 // TerminalRec entries of `terms`
   int32_t find;                      // find mode (no table, no rows): the successor whose terminal
   uint64_t find_key;                 // key equals find_key is recorded in terms[0]
@@ -378,7 +378,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
   __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kLevelBlock * P::kMaxSends : 1];
-  __shared__ unsigned long long s_red[NWAVE];
+#ifdef DSL_PHASES
+  __shared__ unsigned long long s_red[NWAVE];  // PH_FLUSH (instrumented builds)
+#endif
   __shared__ unsigned long long s_red5[NWAVE * 5];
   __shared__ int s_wsum[NWAVE];
   __shared__ int s_cbase[kWin / 64][NC];
