@@ -39,7 +39,7 @@ EXPORTED = [
     "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
     "dsl_run_dfs", "dsl_replay", "dsl_human_readable_trace", "dsl_set_dropped",
 ]
-DSL_ABI_VERSION = 2  # include/dslabs_hip.h; load() refuses a library of another layout
+DSL_ABI_VERSION = 3  # include/dslabs_hip.h; load() refuses a library of another layout
 
 
 class dsl_protocol_desc(ctypes.Structure):
@@ -73,7 +73,11 @@ class dsl_settings(ctypes.Structure):
 class dsl_engine_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("rank", ctypes.c_int32), ("world_size", ctypes.c_int32),
                 ("virtual_shards", ctypes.c_int32), ("comm_id", ctypes.c_uint8 * 128),
-                ("replicate_below", ctypes.c_int64)]
+                ("replicate_below", ctypes.c_int64), ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+DSL_CFG_RCCL_AT_WORLD_1 = 1           # dsl_engine_config.flags
+DSL_HOST_COMM_DEVICE_COLLECTIVES = 1  # dsl_host_comm.flags
 
 
 class dsl_dfs_config(ctypes.Structure):

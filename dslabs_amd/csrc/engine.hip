@@ -140,6 +140,23 @@ struct HostComm : Comm {
   int bcast_u64(uint64_t* v, int n, int root, hipStream_t) override {
     return h.bcast_u64(h.ctx, v, n, root) ? DSL_ERR_COMM : DSL_OK;
   }
+  // DSL_HOST_COMM_DEVICE_COLLECTIVES: the engine runs its RCCL branches (device gathers enqueued on
+  // its stream); each device gather is emulated here by a copy of the rank's words to the host, the
+  // caller's allgather and a copy of the gathered words back, all before returning. This is test
+  // plumbing for the bookkeeping of those branches, not a fast path.
+  std::vector<uint64_t> gin, gout;
+  bool device_collectives() const override { return (h.flags & DSL_HOST_COMM_DEVICE_COLLECTIVES) != 0; }
+  int allgather_dev(const uint64_t* d_in, int k, uint64_t* d_out, hipStream_t st) override {
+    if (!device_collectives()) return DSL_ERR_COMM;
+    gin.resize(k);
+    gout.resize((size_t)k * h.size);
+    DSL_HIP(hipMemcpyAsync(gin.data(), d_in, (size_t)k * 8, hipMemcpyDeviceToHost, st));
+    DSL_HIP(hipStreamSynchronize(st));
+    if (h.allgather_u64(h.ctx, gin.data(), k, gout.data())) return DSL_ERR_COMM;
+    DSL_HIP(hipMemcpyAsync(d_out, gout.data(), gout.size() * 8, hipMemcpyHostToDevice, st));
+    DSL_HIP(hipStreamSynchronize(st));  // gout is pageable host memory: the copy completes here
+    return DSL_OK;
+  }
   int alltoallv(const uint8_t* send, const uint64_t* so, const uint64_t* sb, uint8_t* recv, const uint64_t* ro,
                 const uint64_t* rb, hipStream_t st) override {
     const int n = h.size;
@@ -184,7 +201,7 @@ static int make_engine(const dsl_protocol_desc& d, const dsl_engine_config& cfg,
     set_error("invalid protocol parameters");
     return DSL_ERR_ARG;
   }
-  if (cfg.world_size > 1) {
+  if (cfg.world_size > 1 || (cfg.flags & DSL_CFG_RCCL_AT_WORLD_1)) {
     if (cfg.world_size > kMaxShards || cfg.rank < 0 || cfg.rank >= cfg.world_size) return DSL_ERR_ARG;
     Comm* cm = nullptr;
     if (g_pending_host_comm) {

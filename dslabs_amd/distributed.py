@@ -27,7 +27,7 @@ ALLTOALLV = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, _U8P, _U64P, _U64P, 
 class dsl_host_comm(ctypes.Structure):
     _fields_ = [("ctx", ctypes.c_void_p), ("rank", ctypes.c_int32), ("size", ctypes.c_int32),
                 ("allgather_u64", ALLGATHER), ("allreduce_u64", ALLREDUCE), ("bcast_u64", BCAST),
-                ("alltoallv", ALLTOALLV)]
+                ("alltoallv", ALLTOALLV), ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 _SIGN = np.uint64(1 << 63)
@@ -40,7 +40,9 @@ def _u64(ptr, n) -> np.ndarray:
 class TorchHostComm:
     """dsl_host_comm over a torch.distributed process group (CPU tensors, e.g. gloo)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, device_collectives: bool = False):
+        """device_collectives: DSL_HOST_COMM_DEVICE_COLLECTIVES -- the engine takes its RCCL code
+        path (device-side gathers), each gather emulated through allgather (tests)."""
         import torch.distributed as dist
         self.dist = dist
         self.group = group
@@ -49,7 +51,8 @@ class TorchHostComm:
         self.errors = []
         self._cbs = (ALLGATHER(self._wrap(self.allgather)), ALLREDUCE(self._wrap(self.allreduce)),
                      BCAST(self._wrap(self.bcast)), ALLTOALLV(self._wrap(self.alltoallv)))
-        self.struct = dsl_host_comm(None, self.rank, self.size, *self._cbs)
+        self.struct = dsl_host_comm(None, self.rank, self.size, *self._cbs,
+                                    _lib.DSL_HOST_COMM_DEVICE_COLLECTIVES if device_collectives else 0, 0)
 
     def _wrap(self, fn):
         def cb(*args):

@@ -450,7 +450,9 @@ class Engine:
 
     def __init__(self, protocol, device: int = -1, rank: int = 0, world_size: int = 1,
                  virtual_shards: int = 0, comm_id: Optional[bytes] = None, host_comm=None,
-                 replicate_below: int = -1):
+                 replicate_below: int = -1, rccl_at_world_1: bool = False):
+        """rccl_at_world_1: build the RCCL communicator (comm_id) even at world_size 1
+        (DSL_CFG_RCCL_AT_WORLD_1), so the collectives run on a one-GPU box."""
         lib = _lib.load()
         self.lib = lib
         self.protocol = protocol
@@ -461,6 +463,7 @@ class Engine:
         cfg.world_size = world_size
         cfg.virtual_shards = virtual_shards
         cfg.replicate_below = replicate_below
+        cfg.flags = _lib.DSL_CFG_RCCL_AT_WORLD_1 if rccl_at_world_1 else 0
         if comm_id is not None:
             ctypes.memmove(cfg.comm_id, comm_id, 128)
         handle = ctypes.c_void_p()

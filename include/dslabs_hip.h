@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define DSL_ABI_VERSION 2 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version */
+#define DSL_ABI_VERSION 3 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version;
+                            3: dsl_engine_config.flags, dsl_host_comm.flags */
 #define DSL_MAX_NODES 32
 #define DSL_MAX_PREDICATES 16
 #define DSL_MAX_POOL 48          /* operands of combinator predicates (dsl_settings.pool) */
@@ -160,8 +161,15 @@ typedef struct {
   int32_t virtual_shards;   /* >1: emulate that many hash shards on this one device (tests) */
   uint8_t comm_id[128];     /* RCCL ncclUniqueId when world_size > 1 */
   int64_t replicate_below;  /* multi-shard: a level whose frontier is smaller runs replicated on every
-                               shard (no exchange); -1 = default (65536), 0 = always hash-sharded */
+                               shard (no exchange); -1 = automatic (a per-level cost decision),
+                               0 = always hash-sharded, n > 0 = below n states */
+  int32_t flags;            /* DSL_CFG_* */
+  int32_t reserved;
 } dsl_engine_config;
+
+/* dsl_engine_config.flags */
+#define DSL_CFG_RCCL_AT_WORLD_1 1 /* build the RCCL communicator (comm_id) also at world_size 1, so the
+                                     collectives' code runs on a one-GPU box (tests) */
 
 /* A decoded event (MessageEnvelope / TimerEnvelope, T/MessageEnvelope.java, T/TimerEnvelope.java). */
 typedef struct {
@@ -309,7 +317,15 @@ typedef struct {
   int (*bcast_u64)(void* ctx, uint64_t* v, int32_t n, int32_t root);
   int (*alltoallv)(void* ctx, const uint8_t* send, const uint64_t* send_off, const uint64_t* send_bytes,
                    uint8_t* recv, const uint64_t* recv_off, const uint64_t* recv_bytes);
+  int32_t flags;            /* DSL_HOST_COMM_* */
+  int32_t reserved;
 } dsl_host_comm;
+
+/* dsl_host_comm.flags */
+#define DSL_HOST_COMM_DEVICE_COLLECTIVES 1 /* the engine takes its RCCL code path (device-side gathers of
+                                              the route counts and the level records, enqueued on its
+                                              stream); the transport emulates each device gather as a
+                                              copy to the host, allgather_u64 and a copy back (tests) */
 
 int dsl_create_with_host_comm(const dsl_protocol_desc* proto, const dsl_engine_config* cfg,
                               const dsl_host_comm* comm, dsl_engine** out);

@@ -31,8 +31,8 @@ public final class Dsl {
       OFF_MAX_FRONTIER = 2312, OFF_MEMORY_BUDGET = 2320, OFF_POOL = 2328;
   public static final int MAX_NODES = 32, MAX_PREDICATES = 16, MAX_POOL = 48;
   // dsl_engine_config
-  public static final long SIZE_ENGINE_CONFIG = 152, OFF_CFG_DEVICE = 0, OFF_CFG_RANK = 4, OFF_CFG_WORLD = 8,
-      OFF_CFG_VSHARDS = 12, OFF_CFG_COMM_ID = 16, OFF_CFG_REPLICATE_BELOW = 144;
+  public static final long SIZE_ENGINE_CONFIG = 160, OFF_CFG_DEVICE = 0, OFF_CFG_RANK = 4, OFF_CFG_WORLD = 8,
+      OFF_CFG_VSHARDS = 12, OFF_CFG_COMM_ID = 16, OFF_CFG_REPLICATE_BELOW = 144, OFF_CFG_FLAGS = 152;
   // dsl_event
   public static final long SIZE_EVENT = 96, OFF_EV_IS_TIMER = 0, OFF_EV_FROM = 4, OFF_EV_TO = 8, OFF_EV_TYPE = 12,
       OFF_EV_N_FIELDS = 16, OFF_EV_TIMER_MIN = 20, OFF_EV_TIMER_MAX = 24, OFF_EV_FIELDS = 32;
@@ -43,7 +43,7 @@ public final class Dsl {
       OFF_RES_INITIAL_DEPTH = 60, OFF_RES_ELAPSED = 64;
 
   // DSL_ABI_VERSION: the struct layout above; a library of another version is refused
-  public static final int ABI_VERSION = 2;
+  public static final int ABI_VERSION = 3;
   public static final int MAX_EVENT_FIELDS = 8;
 
   // dsl_protocol_id (include/dslabs_hip.h)

@@ -20,7 +20,9 @@ def main():
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     from dslabs_amd.distributed import TorchHostComm
-    hc = TorchHostComm()
+    # DSL_TEST_DEVICE_COLLECTIVES=1: the engine runs its RCCL branches (device-side gathers), the
+    # gathers emulated over gloo (DSL_HOST_COMM_DEVICE_COLLECTIVES)
+    hc = TorchHostComm(device_collectives=os.environ.get("DSL_TEST_DEVICE_COLLECTIVES") == "1")
     res = {"rank": rank}
     if mode == "collectives":
         U = ctypes.POINTER(ctypes.c_uint64)
@@ -70,9 +72,12 @@ def main():
         s.table_log2_slots = 23 if mode == "mp_c5" else 22
         rb = int(os.environ.get("DSL_TEST_REPLICATE_BELOW", "0"))
         eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=rb)
+        if mode == "mp_c5":  # warm-up: buffers grow in the first search (each growth is a host sync)
+            eng.bfs(proto.initial_state(), s)
         r = eng.bfs(proto.initial_state(), s)
-        res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states,
-                   exchanged=eng.kernel_stats()["exchanged"])
+        st = eng.kernel_stats()
+        res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states, exchanged=st["exchanged"],
+                   host_syncs=st["host_syncs"], sharded_levels=st["sharded_levels"])
         t = r.invariantViolatingState() or r.goalMatchingState()
         if t is not None:
             res["trace"] = t.trace()

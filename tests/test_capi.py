@@ -66,7 +66,8 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
     the ctypes mirrors in dslabs_amd/_lib.py."""
     import subprocess
     from dslabs_amd import _lib
-    structs = {"dsl_protocol_desc": ["protocol", "params"], "dsl_engine_config": ["comm_id", "replicate_below"],
+    structs = {"dsl_protocol_desc": ["protocol", "params"], "dsl_engine_config": ["comm_id", "replicate_below", "flags"],
+               "dsl_host_comm": ["allgather_u64", "alltoallv", "flags"],
                "dsl_settings": ["table_log2_slots", "max_frontier_states"], "dsl_event": ["fields"],
                "dsl_result": ["per_depth", "trace", "terminal_state"], "dsl_stats": ["table_slots", "probes", "host_syncs", "rccl_version"],
                "dsl_dfs_config": ["max_probes", "max_trace", "no_minimize"], "dsl_predicate": ["arg1"]}
@@ -82,8 +83,9 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(c)], check=True)
     got = dict(line.split() for line in subprocess.run([str(exe)], check=True, capture_output=True,
                                                        text=True).stdout.splitlines())
+    from dslabs_amd import distributed
     for st, fields in structs.items():
-        cls = getattr(_lib, st)
+        cls = getattr(_lib, st, None) or getattr(distributed, st)
         assert ctypes.sizeof(cls) == int(got[st]), st
         for f in fields:
             assert getattr(cls, f).offset == int(got[f"{st}.{f}"]), (st, f)

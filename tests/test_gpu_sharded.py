@@ -78,6 +78,48 @@ def test_multiprocess_shards_one_gpu(mode, world, rep):
         assert sum(r["exchanged"] for r in res) > 0
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_multiprocess_device_collectives_c5(world):
+    """The RCCL engine's bookkeeping on gloo: with DSL_HOST_COMM_DEVICE_COLLECTIVES the engine takes
+    its device-collective branches (the route-count matrix and the level records gathered on the
+    device, bfs_engine.hpp dev_gather), each gather emulated by the transport. C5 d12 with every
+    level hash-sharded, then with the default threshold: per-depth counts equal the golden vector,
+    states are routed, and a sharded level costs at most two host round trips."""
+    want = MPX["mp_c5_d12"]["per_depth"]
+    for rep in (0, -1):
+        res = run_workers("mp_c5", world, replicate_below=rep, device_collectives=True)
+        for r in res:
+            assert r["errors"] == []
+            assert r["per_depth"] == want
+            assert r["sharded_levels"] > 0
+            assert r["host_syncs"] <= 2 * r["sharded_levels"] + 2 * (12 - r["sharded_levels"]) + 2, r
+        assert sum(r["exchanged"] for r in res) > 0
+        if rep == 0:
+            for r in res:
+                assert r["sharded_levels"] == 12
+                assert r["host_syncs"] <= 2 * r["sharded_levels"] + 1, r
+
+
+def test_rccl_engine_at_world_1():
+    """make_comm / ncclCommInitRank / ncclGetVersion and the RcclComm collectives run once on a
+    one-GPU box: a world-size-1 engine with its RCCL communicator (DSL_CFG_RCCL_AT_WORLD_1) runs
+    C5 to depth 8; the counts equal the golden prefix and the engine reports the RCCL it bound."""
+    import argmap
+    from dslabs_amd.distributed import comm_unique_id
+    case = MPX["mp_c5_d12"]
+    proto = argmap.protocol(case["args"])
+    eng = Engine(proto, device=0, rank=0, world_size=1, comm_id=comm_unique_id(), rccl_at_world_1=True)
+    try:
+        s = argmap.settings(case["args"], proto, table_log2=20)
+        s.maxDepth(8)
+        r = eng.bfs(proto.initial_state(), s)
+        st = eng.kernel_stats()
+    finally:
+        eng.close()
+    assert r.per_depth == case["per_depth"][:9]
+    assert st["rccl_version"] > 0, st
+
+
 @pytest.mark.parametrize("shards", [2, 4, 8])
 def test_virtual_shards_c5_default_settings(shards):
     """BASELINE C5 (d12) with the default replicate_below: the levels above it are hash-sharded

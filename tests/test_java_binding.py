@@ -37,7 +37,7 @@ FIELDS = {
                      "MEMORY_BUDGET": "memory_budget_bytes", "POOL": "pool"},
     "dsl_engine_config": {"ENGINE_CONFIG": None, "CFG_DEVICE": "device", "CFG_RANK": "rank",
                           "CFG_WORLD": "world_size", "CFG_VSHARDS": "virtual_shards", "CFG_COMM_ID": "comm_id",
-                          "CFG_REPLICATE_BELOW": "replicate_below"},
+                          "CFG_REPLICATE_BELOW": "replicate_below", "CFG_FLAGS": "flags"},
     "dsl_event": {"EVENT": None, "EV_IS_TIMER": "is_timer", "EV_FROM": "from_", "EV_TO": "to", "EV_TYPE": "type",
                   "EV_N_FIELDS": "n_fields", "EV_TIMER_MIN": "timer_min", "EV_TIMER_MAX": "timer_max",
                   "EV_FIELDS": "fields"},
@@ -60,7 +60,7 @@ def test_java_struct_offsets_match_the_c_abi():
             else:
                 assert c["OFF_" + jname] == getattr(S, field).offset, (struct, jname)
             checked += 1
-    assert checked == 59
+    assert checked == 60
 
 
 def test_java_end_conditions_and_predicate_ids_match_the_header():
