@@ -162,6 +162,13 @@ struct BfsEngine : EngineBase {
   // k_level_record), on the device and pinned on the host
   static constexpr int kXWords = kMaxShards * kMaxShards + (kMaxShards + 1) * kRecWords;
   uint64_t* xdev = nullptr;
+  // the device-side deadline of a time-limited search (LevelArgs::budget_rt): the device clock at
+  // the search's start (k_clock) and the budget in its ticks; not used in a replicated level of a
+  // multi-rank search (every rank runs the level on its own clock: the host check, agreed by a
+  // collective, ends those)
+  uint64_t* t0_rt = nullptr;
+  uint64_t budget_rt = 0;
+  uint64_t level_budget(bool rep) const { return comm && rep ? 0 : budget_rt; }
   uint64_t* xhost = nullptr;
   uint64_t* segs_dev = nullptr;   // virtual shards: the segment tables of the two exchange rounds
   uint64_t* segs_host = nullptr;
@@ -208,13 +215,18 @@ struct BfsEngine : EngineBase {
   uint64_t queue_span(uint64_t F) const {
     if (q_rows_forced) return q_rows_forced;  // tests: small queues that spill and stop early
     uint64_t s = kQueueRowsMin;
-    while ((s < 32 * F || s < q_span_hint) && s < queue_span_max()) s <<= 1;
+    while ((s < 32 * F || s < q_span_hint || s < q_span_want) && s < queue_span_max()) s <<= 1;
     return s;
   }
+  // The span a repeated search of this engine wants: 4x the largest frontier the last search
+  // produced, so that one queue covers every level that fits (no host round trip between them);
+  // DSL_QSPAN_FIXED keeps the span at 32x the frontier the queue starts from.
+  uint64_t q_span_want = 0;
+  const bool q_span_adapt = getenv("DSL_QSPAN_FIXED") == nullptr;
   uint64_t q_rows_forced = 0;  // DSL_QUEUE_ROWS (a multiple of 32)
   uint64_t q_span_hint = 0;  // the largest span an earlier queue of this engine used (buffers exist)
   uint64_t queue_flimit(uint64_t span) const {
-    return W > 1 ? std::min<uint64_t>(span / 4, rep_threshold() - 1) : span / 4;
+    return W > 1 && !auto_rep() ? std::min<uint64_t>(span / 4, rep_threshold() - 1) : span / 4;
   }
   double q_ms_per_level = 0;       // the last queue's device time per level
   unsigned char* qctr = nullptr;   // kQueue + 1 counter sets
@@ -266,6 +278,7 @@ struct BfsEngine : EngineBase {
     (void)hipFree(segs_dev);
     if (segs_host) (void)hipHostFree(segs_host);
     (void)hipFree(rehash_err);
+    (void)hipFree(t0_rt);
     if (xhost) (void)hipHostFree(xhost);
     if (hq) (void)hipHostFree(hq);
     for (auto e : qev) (void)hipEventDestroy(e);
@@ -424,9 +437,29 @@ struct BfsEngine : EngineBase {
 #define DSL_SLOTS 1024
 #endif
   static constexpr int kSlots = DSL_SLOTS;
-  // Frontier size below which a multi-shard search runs the level replicated (see run()):
-  // dsl_engine_config.replicate_below, -1 = default, 0 = never.
-  uint64_t rep_threshold() const { return cfg.replicate_below < 0 ? (1ull << 16) : (uint64_t)cfg.replicate_below; }
+  // Replicated or hash-sharded (multi-shard searches, see run()). dsl_engine_config.replicate_below
+  // n > 0: a level whose frontier holds fewer than n states runs replicated; 0: every level is
+  // sharded; -1 (automatic): a level is sharded once sharding it pays, by the cost model
+  //     replicated  T(work)          sharded  T(work / W) + X,   T(w) = max(Tf, c w)
+  // i.e. from work = shard_work_min on, with c = k_level ns per work item (the whole GPU), Tf the
+  // latency floor of a small level and X =
+  // the non-kernel time of a sharded level (exchange rounds, owner probes, materialization, the two
+  // host round trips). Both are measured (c: the smallest per-item time of a level of >= 64K items,
+  // X: the mean of the sharded levels), kept across searches and agreed by every rank at the start
+  // of a search (the maximum, in the collective that judges the initial state), so every rank
+  // takes the same decision; before any measurement c = 0.05 ns, X = 100 us. The switch happens
+  // once per search: a sharded level's tables no longer hold every state.
+  static constexpr double kLevelFloorUs = 20.0;  // a small level's k_level time (profiles/r03_level_times*)
+  bool auto_rep() const { return cfg.replicate_below < 0; }
+  uint64_t rep_threshold() const { return auto_rep() ? ~0ull : (uint64_t)cfg.replicate_below; }
+  double cost_c_ns = 0, cost_x_us = 0;  // this rank's measurements (0: none yet)
+  uint64_t shard_work_min = ~0ull;      // agreed for the current search (auto mode)
+  bool level_replicated(uint64_t F, uint64_t work) const {
+    return auto_rep() ? work <= shard_work_min : F < rep_threshold();
+  }
+  uint64_t queue_wlimit(uint64_t span) const {
+    return W > 1 && auto_rep() ? std::min<uint64_t>(8 * span, shard_work_min) : 8 * span;
+  }
   int chunk_parents(uint64_t F) const {
     const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
     int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / per);
@@ -460,7 +493,7 @@ struct BfsEngine : EngineBase {
     int nq = hset.max_depth >= 0 ? std::max(1, std::min(kQueue, hset.max_depth - depth)) : kQueue;
     if (hset.max_time_ms > 0 && q_ms_per_level > 0)
       nq = std::max(1, std::min(nq, (int)((hset.max_time_ms - elapsed_ms) / q_ms_per_level)));
-    const uint64_t flimit = queue_flimit(span), wlimit = 8 * span;
+    const uint64_t flimit = queue_flimit(span), wlimit = queue_wlimit(span);
     const uint64_t room = table_room();
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
@@ -501,6 +534,8 @@ struct BfsEngine : EngineBase {
       a.qwlimit = wlimit;
       a.qroom = room;
       a.qspread = spread;
+      a.t0_rt = t0_rt;
+      a.budget_rt = level_budget(W > 1);
       a.PB = pb_max;
       a.depth = depth + 1 + j;
       a.incremental = depth + j > init_depth ? 1 : 0;
@@ -577,20 +612,55 @@ struct BfsEngine : EngineBase {
     if (hset.memory_budget_bytes) lim = std::min<uint64_t>(lim, std::max<uint64_t>(16, hset.memory_budget_bytes / 64));
     return lim;
   }
+  // The key layout (fingerprint.hpp) pins 60 + b0 fingerprint bits, b0 = log2 of the search's
+  // first table: a table of 2^b buckets (at most 2^(b+2) states, half full) keeps the chance of a
+  // false merge n^2 / 2^(61 + b0) below 2^-20 while 2b - b0 <= kKeyRisk. A growth past that does
+  // not rehash: the search restarts from a first table of the size needed (DSL_RESTART_REKEY), so
+  // its keys pin more bits. Every input is identical on every rank, so all ranks restart together.
+  static constexpr int kKeyRisk = 37;
+  static constexpr int DSL_RESTART_REKEY = 1;
+  uint64_t rekey_buckets = 0;
   int ensure_table(uint64_t need_states) {
     const uint64_t have = tbl.bucket_mask + 1;
     uint64_t nb = have;
     while (nb * 4 < need_states && nb < table_limit_buckets()) nb <<= 1;  // 8 slots per bucket, half full
     if (nb == have) return DSL_OK;  // large enough, or at the budget (the probes then report a full table)
+    {
+      int b = 0;
+      while ((2ull << b) <= nb) b++;
+      const char* kr = getenv("DSL_KEY_RISK");  // tests: a smaller bound forces the restart
+      if (2 * b - tbl.b0 > (kr ? atoi(kr) : kKeyRisk)) {
+        rekey_buckets = nb;
+        if (getenv("DSL_LEVEL_TRACE"))
+          fprintf(stderr, "[table] %llu slots would pin too few key bits (b0 %d): restart\n",
+                  (unsigned long long)nb * 8, tbl.b0);
+        return DSL_RESTART_REKEY;
+      }
+    }
     if (!rehash_err) DSL_HIP(hipMalloc(&rehash_err, 8));
     DSL_HIP(hipMemsetAsync(rehash_err, 0, 8, stream));
     Table to = tbl;
     to.bucket_mask = nb - 1;
+    // every shard allocates first; with several ranks the outcome is agreed (one sum over the
+    // ranks) before anything changes, so a failed allocation on one rank ends the search on all
+    std::vector<unsigned long long*> fresh(sh.size(), nullptr);
+    uint64_t fail = 0;
+    for (size_t l = 0; l < sh.size(); l++)
+      if (hipMalloc(&fresh[l], nb * 64) != hipSuccess) fail = 1;
+    (void)hipGetLastError();
+    if (comm) {
+      stats.host_syncs++;
+      DSL_TRY(comm->allreduce_u64(&fail, 1, false, stream));
+    }
+    if (fail) {
+      for (auto* q : fresh) (void)hipFree(q);
+      set_error("visited table growth: device allocation of " + std::to_string(nb * 64) + " bytes failed");
+      return DSL_ERR_TABLE_FULL;
+    }
     std::vector<unsigned long long*> old(sh.size());
     for (size_t l = 0; l < sh.size(); l++) {
       Shard& S = sh[l];
-      unsigned long long* nt = nullptr;
-      DSL_HIP(hipMalloc(&nt, nb * 64));
+      unsigned long long* nt = fresh[l];
       DSL_HIP(hipMemsetAsync(nt, 0, nb * 64, stream));
       Table from = tbl;
       from.slots = S.table;
@@ -604,6 +674,12 @@ struct BfsEngine : EngineBase {
     unsigned long long bad = 0;
     DSL_HIP(hipMemcpyAsync(&bad, rehash_err, 8, hipMemcpyDeviceToHost, stream));
     DSL_TRY(hsync());
+    if (comm) {  // a rehash that found no free slot on one rank ends the search on every rank
+      uint64_t b = bad;
+      stats.host_syncs++;
+      DSL_TRY(comm->allreduce_u64(&b, 1, false, stream));
+      bad = b;
+    }
     for (auto* q : old) (void)hipFree(q);
     tbl.bucket_mask = nb - 1;
     table_buckets = nb;
@@ -685,11 +761,24 @@ struct BfsEngine : EngineBase {
   // Search.run for BFS. A search whose visited table ran out of room (est_new_states far off:
   // more new states in one level than twice the estimate) is run again from a first table twice
   // the size it reached -- the table grows instead of failing, up to the memory budget.
+  // A search restarted for its key width (ensure_table) starts from the table size it needed.
+  // SearchSettings.maxTimeSecs bounds the whole call: a restart gets the time that is left
+  // (t_run0 is the first attempt's start).
   uint64_t restart_buckets = 0;
+  std::chrono::steady_clock::time_point t_run0;
   int run(dsl_result** out) override {
     restart_buckets = 0;
+    t_run0 = std::chrono::steady_clock::now();
     for (int attempt = 0;; attempt++) {
       const int rc = run_once(out);
+      if (rc == DSL_RESTART_REKEY && attempt < 8) {
+        restart_buckets = rekey_buckets;
+        continue;
+      }
+      if (rc == DSL_RESTART_REKEY) {
+        set_error("visited table: no key layout reached the required width");
+        return DSL_ERR_TABLE_FULL;
+      }
       if (rc != DSL_ERR_TABLE_FULL || table_buckets * 2 > table_limit_buckets() || attempt >= 8) return rc;
       restart_buckets = table_buckets * 2;
       if (getenv("DSL_LEVEL_TRACE")) fprintf(stderr, "[table] full: search restarts with %llu slots\n",
@@ -698,7 +787,7 @@ struct BfsEngine : EngineBase {
   }
 
   int run_once(dsl_result** out) {
-    auto t_start = std::chrono::steady_clock::now();
+    const auto t_start = t_run0;
     (void)hipGetLastError();  // the per-thread sticky error must not blame this search for an older call
     if (!stream) {
       if (cfg.device >= 0) DSL_HIP(hipSetDevice(cfg.device));
@@ -764,6 +853,15 @@ struct BfsEngine : EngineBase {
     }
     table_buckets = buckets;
     terms_alloc = term_cap;
+    budget_rt = 0;
+    if (hset.max_time_ms > 0) {
+      if (!t0_rt) DSL_HIP(hipMalloc(&t0_rt, 8));
+      hipLaunchKernelGGL(k_clock, dim3(1), dim3(64), 0, stream, t0_rt);
+      DSL_HIP(hipGetLastError());
+      const double left = hset.max_time_ms -
+                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+      budget_rt = (uint64_t)std::max(1.0, left * 1e5);  // s_memrealtime: 100 MHz
+    }
     stats.table_slots = buckets * 8 * (uint64_t)W;
     q_left = 0;
     q_pos = 0;
@@ -826,7 +924,25 @@ struct BfsEngine : EngineBase {
       S.work = (uint64_t)count_events<P>(init.w, prm, dset);
       S.level_size[0] = 1;
     }
-    if (comm) DSL_TRY(comm->allreduce_u64(&init_enc, 1, true, stream));
+    if (comm) {  // the initial state's verdict and the cost model, agreed by every rank (one collective)
+      uint64_t v[3] = {init_enc, ~(uint64_t)(cost_c_ns * 1e6), ~(uint64_t)(cost_x_us * 1e3)};
+      DSL_TRY(comm->allreduce_u64(v, 3, true, stream));
+      init_enc = v[0];
+      stats.cost_c_ns = (double)~v[1] / 1e6;
+      stats.cost_x_us = (double)~v[2] / 1e3;
+    } else {
+      stats.cost_c_ns = cost_c_ns;
+      stats.cost_x_us = cost_x_us;
+    }
+    {
+      // a level of w work items takes T(w) = max(Tf, c w) (Tf: the latency floor of a small level);
+      // shard iff T(w) - T(w / W) > X, i.e. from the smallest such w
+      const double c = stats.cost_c_ns > 0 ? stats.cost_c_ns : 0.05, x = (stats.cost_x_us > 0 ? stats.cost_x_us : 100.0) * 1e3;
+      const double tf = kLevelFloorUs * 1e3;
+      const double w = x <= (W - 1) * tf ? (x + tf) / c : x / (c * (1.0 - 1.0 / W));
+      shard_work_min = W > 1 ? (uint64_t)std::min(w, 1.8e19) : ~0ull;
+      stats.shard_work_min = W > 1 ? shard_work_min : 0;
+    }
     const int init_verdict = (int)(init_enc >> 32);
     if (trace_levels)
       fprintf(stderr, "[setup] %.4f ms\n",
@@ -842,7 +958,8 @@ struct BfsEngine : EngineBase {
     bool have_g = false;
     std::vector<uint64_t> g_next(3, 0);
     std::vector<uint64_t> per_depth{1};
-    uint64_t total_states = 1, successors = 0, exchanged = 0;
+    uint64_t total_states = 1, successors = 0, exchanged = 0, max_front = 1, x_levels = 0;
+    double x_sum_us = 0;
     int end = DSL_SPACE_EXHAUSTED, pred_index = -1, term_depth = -1;
     int depth = init_depth;
     double level_ms_max = 0;
@@ -855,8 +972,9 @@ struct BfsEngine : EngineBase {
     } else {
       while (true) {
         const auto lt0 = std::chrono::steady_clock::now();
+        const uint64_t reallocs0 = n_reallocs + stats.table_rehashes;
         // every shard holds the same frontier in a replicated level: the decision is identical
-        const bool rep = rep_active && sh[0].F < rep_threshold();
+        const bool rep = rep_active && level_replicated(sh[0].F, sh[0].work);
         if (rep_active && !rep) {
           rep_active = false;
           first_sharded = true;
@@ -905,7 +1023,12 @@ struct BfsEngine : EngineBase {
           q_pos = 0;
         }
         const bool queued = q_left > 0;
-        if (!queued) DSL_TRY(ensure_table(inserted + est_new_states(g[2], prev_new, prev_work)));
+        if (!queued) {
+          // a sharded level inserts about 1/W of its new states into each shard's table (+25 % for
+          // the hash's imbalance); a replicated or single-shard level all of them
+          const uint64_t est = est_new_states(g[2], prev_new, prev_work);
+          DSL_TRY(ensure_table(inserted + (route ? est / W + est / (4 * W) + 1024 : est)));
+        }
 
         // Capacity: the level has exactly S.work work items, an upper bound on its new states.
         // The next frontier gets min(work, 4F) rows (typical growth is ~3 new states per
@@ -983,6 +1106,8 @@ struct BfsEngine : EngineBase {
           a.qprev = nullptr;
           a.qprev_seg = nullptr;
           a.segs.pb = PB;
+          a.t0_rt = t0_rt;
+          a.budget_rt = level_budget(rep);
           const uint64_t nchunks = a.segs.chunk0[a.segs.n];
           const int blocks = (int)std::min<uint64_t>(nchunks, kLevelGrid);
           if (route)
@@ -1216,8 +1341,8 @@ struct BfsEngine : EngineBase {
           nbase[l].push_back(mat_keep[l]);
           ncnt[l].push_back(c);
         }
+        float kms = 0;
         if (!queued || q_pos == 0) {  // a queue is timed as a whole (its dispatches counted there)
-          float kms = 0;
           if (queued) kms = (float)q_ms_total;
           else (void)hipEventElapsedTime(&kms, ev0, ev1);
           stats.expand_ms += kms;
@@ -1253,9 +1378,13 @@ struct BfsEngine : EngineBase {
         std::vector<uint64_t> gsum(8, 0);
         uint64_t enc = ~0ull;
         std::vector<TerminalRec> local_best(L);
+        uint64_t max_new = 0;  // the most states one shard's table took this level
+        bool level_tup = false;  // the level stopped at the deadline: partial
         for (int l = 0; l < (rep ? 1 : L); l++) {  // replicated: every shard has the same counts
           Shard& S = sh[l];
           gsum[0] += S.lc.new_states;
+          max_new = std::max<uint64_t>(max_new, S.lc.new_states);
+          level_tup |= S.lc.time_up != 0;
           uint64_t fn = 0;
           for (uint64_t c : ncnt[l]) fn += c;
           gsum[1] += fn;
@@ -1279,9 +1408,12 @@ struct BfsEngine : EngineBase {
         if (!recs.empty()) {  // the gathered records: global sums, the best terminal, the next level's g
           std::fill(gsum.begin(), gsum.end(), 0);
           std::fill(g_next.begin(), g_next.end(), 0);
+          max_new = 0;
           for (int x = 0; x < W; x++) {
             const uint64_t* r = recs.data() + (size_t)x * kRecWords;
             gsum[0] += r[kRecNew];
+            max_new = std::max<uint64_t>(max_new, r[kRecNew]);
+            level_tup |= r[kRecLevelTimeUp] != 0;
             gsum[1] += r[kRecRows];
             gsum[2] += r[kRecSucc];
             gsum[3] += r[kRecErrOverflow];
@@ -1324,13 +1456,23 @@ struct BfsEngine : EngineBase {
           return DSL_ERR_FRONTIER_FULL;
         }
         if (gsum[7]) avg_events_x16 = std::max<uint64_t>(16, (gsum[6] * 16 + gsum[7] - 1) / gsum[7]);
+        if (level_tup && enc == ~0ull) {
+          // the deadline passed inside the level (Search.java:313-318): its states count, but it is
+          // not a completed depth; a terminal it found is still reported (below)
+          successors += gsum[2];
+          total_states += gsum[0];
+          progress_states = total_states;
+          end = DSL_TIME_EXHAUSTED;
+          break;
+        }
         depth++;
         successors += gsum[2];
         total_states += gsum[0];
-        inserted += gsum[0];
+        inserted += route ? max_new : gsum[0];  // per shard (an upper bound)
         prev_new = gsum[0];
         prev_work = gsum[6];
         if (gsum[0]) per_depth.push_back(gsum[0]);
+        max_front = std::max(max_front, gsum[1]);
         progress_states = total_states;
         progress_depth = depth;
         for (int l = 0; l < L; l++) {
@@ -1339,6 +1481,20 @@ struct BfsEngine : EngineBase {
         }
         const double lms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count();
         level_ms_max = std::max(level_ms_max, lms);
+        // the cost model (auto replicate_below): c from levels in the throughput regime, X from the
+        // sharded levels that allocated nothing (a first search grows its buffers)
+        if (!queued && kms > 0) {
+          uint64_t lw = 0;
+          for (auto& S : sh) lw += S.lc.work_items;
+          if (lw >= 65536) {
+            const double c = (double)kms * 1e6 / (double)lw;
+            cost_c_ns = cost_c_ns > 0 ? std::min(cost_c_ns, c) : c;
+          }
+          if (route && n_reallocs + stats.table_rehashes == reallocs0) {
+            x_sum_us += std::max(0.0, (lms - (double)kms) * 1000.0);
+            x_levels++;
+          }
+        }
         if (trace_levels)
           fprintf(stderr, "[level] depth %d F=%llu new=%llu queued=%d wall_ms=%.4f reallocs=%llu\n", depth,
                   (unsigned long long)gsum[7], (unsigned long long)gsum[0], queued ? 1 : 0, lms,
@@ -1419,6 +1575,12 @@ struct BfsEngine : EngineBase {
         DSL_HIP(hipMemsetAsync(qctr, 0, (size_t)(kQueue + 1) * kCtrSet, stream));
         qctr_clean = true;
       }
+    }
+    if (x_levels) cost_x_us = x_sum_us / (double)x_levels;
+    if (q_span_adapt && L == 1) {
+      uint64_t want = kQueueRowsMin;
+      while (want < 4 * max_front && want < queue_span_max()) want <<= 1;
+      q_span_want = std::max(q_span_want, want);
     }
     stats.exchanged = exchanged;
     const double elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();

@@ -75,6 +75,7 @@ struct LevelCounters {
   unsigned long long n_term_rec;    // TerminalRec entries written (improvements of term_best)
   unsigned long long probes;        // visited-table probes (successors that are not no-ops)
   unsigned long long cum_before;    // queued levels: new states of the queue's earlier levels
+  unsigned long long time_up;       // the search's deadline passed during this level (it is partial)
   unsigned long long phase[12];     // DSL_PHASES builds only: shader cycles per k_level phase
   unsigned long long phcls[32];     // DSL_PHASES: handler cycles per class [0, 16), wave-passes [16, 32)
 };
@@ -378,7 +379,18 @@ struct LevelArgs {
   uint32_t term_cap;                 // TerminalRec entries of `terms`
   int32_t find;                      // find mode (no table, no rows): the successor whose terminal
   uint64_t find_key;                 // key equals find_key is recorded in terms[0]
+  // SearchSettings.maxTimeSecs inside a level (Search.java:127-133: the workers check the deadline
+  // continuously): budget_rt > 0 = the search's deadline in s_memrealtime ticks (100 MHz) after
+  // *t0_rt, the clock when the search started (k_clock); a workgroup checks it before every chunk
+  // and a level past it stops, marked LevelCounters::time_up
+  const uint64_t* t0_rt;
+  uint64_t budget_rt;
 };
+
+// The device clock at the start of a time-limited search (the reference point of the deadline).
+__global__ void k_clock(uint64_t* t0) {
+  if (threadIdx.x == 0) *t0 = __builtin_amdgcn_s_memrealtime();
+}
 
 // Parents per chunk of a level of F parents: at most pbmax, and the chunks come in whole rounds
 // of `slots` (the workgroups resident at once) -- R = ceil(F / (slots pbmax)) rounds of equal
@@ -407,7 +419,8 @@ __host__ __device__ inline uint64_t est_new_states(uint64_t work, uint64_t prev_
 // if the queue's inserted states so far plus its estimate fit (the host grows the table first).
 __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
                                                 uint64_t wlimit, uint64_t room) {
-  return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier) && F > 0 && F <= flimit &&
+  return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier | c.time_up) && F > 0 &&
+         F <= flimit &&
          c.next_work <= wlimit &&
          c.cum_before + c.new_states + est_new_states(c.next_work, c.new_states, c.work_items) <= room;
 }
@@ -492,7 +505,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ int s_cbase[kWin / 64][NC];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
-  __shared__ int s_stop, s_weff, s_gnext;
+  __shared__ int s_stop, s_weff, s_gnext, s_tup;
+  __shared__ uint64_t s_t0;
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
   const bool find = a.find != 0;
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
@@ -542,6 +556,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     for (int i = tid; i < (int)(sizeof(SegTable) / 4); i += blockDim.x) dst[i] = src[i];
     if (tid == 0) s_stop = 0;
   }
+  if (a.budget_rt && tid == 0) s_t0 = *a.t0_rt;
   __syncthreads();
   if (s_stop) return;  // an earlier queued level stopped the queue
   PH_MARK(8);  // prologue: the frontier's segment table (+ the queue rule)
@@ -555,6 +570,14 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
   int g = 0;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+    if (a.budget_rt) {  // the deadline, before every chunk (one workgroup-uniform decision)
+      if (tid == 0) s_tup = __builtin_amdgcn_s_memrealtime() - s_t0 > a.budget_rt ? 1 : 0;
+      __syncthreads();
+      if (s_tup) {
+        if (tid == 0) atomicOr(&a.ctr->time_up, 1ull);
+        break;
+      }
+    }
     while (chunk >= s_segs.chunk0[g + 1]) g++;  // chunks ascend: the segment index only grows
     const uint64_t p0 = s_segs.base[g] + (chunk - s_segs.chunk0[g]) * (uint64_t)PB;
     const int pb = (int)min<uint64_t>((uint64_t)PB, s_segs.base[g] + s_segs.cnt[g] - p0);
@@ -1019,7 +1042,7 @@ __global__ void __launch_bounds__(kBlock) k_copy_segments(const uint64_t* seg, i
 // BfsEngine::run): what the next level and the level's bookkeeping need from every shard.
 enum : int {
   kRecNew = 0, kRecRows, kRecSucc, kRecErrOverflow, kRecErrTable, kRecErrFrontier, kRecWork, kRecParents,
-  kRecNextWork, kRecTerm, kRecTimeUp, kRecProbes, kRecWords
+  kRecNextWork, kRecTerm, kRecTimeUp, kRecProbes, kRecLevelTimeUp, kRecWords
 };
 __global__ void k_level_record(const LevelCounters* c, uint64_t base_rows, uint64_t mat_total, uint64_t parents,
                                uint64_t time_up, int gid, uint64_t* out) {
@@ -1037,6 +1060,7 @@ __global__ void k_level_record(const LevelCounters* c, uint64_t base_rows, uint6
   out[kRecTerm] = c->term_best ? ((~(uint64_t)c->term_best) & ~(uint64_t)0xff) | (uint64_t)gid : ~0ull;
   out[kRecTimeUp] = time_up;
   out[kRecProbes] = c->probes;
+  out[kRecLevelTimeUp] = c->time_up;  // the level itself stopped at the deadline (partial)
 }
 
 // A sharded level keeps every new state at the shard that generated it; only the visited set is

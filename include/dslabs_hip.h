@@ -300,6 +300,12 @@ typedef struct {
   uint64_t table_rehashes;   /* visited-table growths (rehashed into a table twice the size) */
   int32_t rccl_version;      /* ncclGetVersion() of the RCCL the engine bound (multi-GPU), 0 otherwise */
   int32_t reserved;
+  /* multi-shard cost model (replicate_below = -1), as agreed by the ranks for this search: k_level ns
+     per work item, the non-kernel time of a sharded level (us; 0 = not measured yet, defaults used),
+     and the resulting work threshold above which a level is sharded */
+  double cost_c_ns;
+  double cost_x_us;
+  uint64_t shard_work_min;
 } dsl_stats;
 
 int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);

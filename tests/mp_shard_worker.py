@@ -72,12 +72,17 @@ def main():
         s.table_log2_slots = 23 if mode == "mp_c5" else 22
         rb = int(os.environ.get("DSL_TEST_REPLICATE_BELOW", "0"))
         eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=rb)
+        first = None
         if mode == "mp_c5":  # warm-up: buffers grow in the first search (each growth is a host sync)
-            eng.bfs(proto.initial_state(), s)
+            r0 = eng.bfs(proto.initial_state(), s)
+            st0 = eng.kernel_stats()
+            first = dict(per_depth=r0.per_depth, exchanged=st0["exchanged"], sharded_levels=st0["sharded_levels"],
+                         shard_work_min=st0["shard_work_min"])
         r = eng.bfs(proto.initial_state(), s)
         st = eng.kernel_stats()
         res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states, exchanged=st["exchanged"],
-                   host_syncs=st["host_syncs"], sharded_levels=st["sharded_levels"])
+                   host_syncs=st["host_syncs"], sharded_levels=st["sharded_levels"], first=first,
+                   cost_c_ns=st["cost_c_ns"], cost_x_us=st["cost_x_us"], shard_work_min=st["shard_work_min"])
         t = r.invariantViolatingState() or r.goalMatchingState()
         if t is not None:
             res["trace"] = t.trace()

@@ -69,7 +69,7 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
     structs = {"dsl_protocol_desc": ["protocol", "params"], "dsl_engine_config": ["comm_id", "replicate_below", "flags"],
                "dsl_host_comm": ["allgather_u64", "alltoallv", "flags"],
                "dsl_settings": ["table_log2_slots", "max_frontier_states"], "dsl_event": ["fields"],
-               "dsl_result": ["per_depth", "trace", "terminal_state"], "dsl_stats": ["table_slots", "probes", "host_syncs", "rccl_version"],
+               "dsl_result": ["per_depth", "trace", "terminal_state"], "dsl_stats": ["table_slots", "probes", "host_syncs", "rccl_version", "cost_x_us", "shard_work_min"],
                "dsl_dfs_config": ["max_probes", "max_trace", "no_minimize"], "dsl_predicate": ["arg1"]}
     src = ['#include <stdio.h>', '#include <stddef.h>', '#include "dslabs_hip.h"', "int main(void) {"]
     for st, fields in structs.items():

@@ -53,12 +53,28 @@ def test_repeated_search_starts_at_the_size_reached():
     assert s2["table_slots"] == s1["table_slots"]
 
 
-@pytest.mark.parametrize("shards", [2, 3])
+@pytest.mark.parametrize("shards", [3, 4])
 def test_table_grows_on_virtual_shards(shards):
+    """Every level hash-sharded: each shard's table is sized for the states IT holds (about 1/W of
+    them), not for the global count."""
     case = MP["mp_c5_d12"]
     (r, st), = _search(case, 10, shards=shards)
     assert r.per_depth == case["per_depth"]
     assert st["table_rehashes"] >= 1
+    per_shard = st["table_slots"] // shards
+    assert per_shard >= 2 * r.states // shards  # at most half full
+    assert per_shard <= 2 ** 21 < 2 * r.states  # a global-count sizing would need 2^22
+
+
+def test_key_width_restart(monkeypatch):
+    """A table grown far past its first size would pin too few fingerprint bits (fingerprint.hpp:
+    60 + b0): the search restarts from a first table of the size it needs. DSL_KEY_RISK lowers the
+    bound so that C5 d12 from 2^10 slots restarts; the counts are unchanged."""
+    monkeypatch.setenv("DSL_KEY_RISK", "25")
+    case = MP["mp_c5_d12"]
+    (r, st), = _search(case, 10)
+    assert r.per_depth == case["per_depth"]
+    assert st["table_slots"] >= 2 * r.states
 
 
 def test_memory_budget_caps_the_table():

@@ -42,6 +42,7 @@ for shards in (2, 4, 8):
         lv = st["sharded_levels"]
         print(json.dumps({"shards": shards, "replicate_below": rep, "ms": round(dt * 1e3, 3),
                           "sharded_levels": lv, "exchanged": st["exchanged"],
-                          "exchange_ms": round(st["exchange_ms"], 3),
+                          "exchange_ms": round(st["exchange_ms"], 3), "cost_c_ns": round(st["cost_c_ns"], 2),
+                          "cost_x_us": round(st["cost_x_us"], 1), "shard_work_min": st["shard_work_min"],
                           "added_ms_per_sharded_level": round((dt - base_dt) * 1e3 / lv, 4) if lv else None}),
               flush=True)
