@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355X"
 CPU_SAMPLE_S = 10.0  # seconds of timed CPU-baseline searches (a bounded sample)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+LLC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 
 WORKLOADS = {
     # BASELINE config C5: lab3 Multi-Paxos (builder-authored), 3 servers, 2 clients
@@ -203,9 +204,16 @@ def roofline(stats: dict, workload: str, depth: int) -> dict:
     # visited-set atomics (north_star): one 64-bit CAS per inserted state (live, HIP events), the
     # probes (bucket lookups) behind them, the table's size, and the PMC count of every atomic at
     # the L2 (TCC_ATOMIC, the committed profile of the same workload) per search
+    out["level_slots"] = stats["level_slots"]  # k_level workgroups resident at once (the grid)
     out["atomics_per_s"] = round(stats["new_states"] / t, 1) if t > 0 else 0.0
     out["probes_per_s"] = round(stats["probes"] / t, 1) if t > 0 else 0.0
+    # where the visited table lives: a table within the 256 MiB Infinity Cache (MALL) keeps the
+    # probes' lines on chip, so that regime is bound by latency, not by HBM bandwidth (the 8 TB/s
+    # denominator above then states how far the kernel is from the HBM roofline, not its bound)
     out["table_bytes"] = int(stats["table_slots"] * 8)
+    out["llc_bytes"] = LLC_BYTES
+    out["llc_resident"] = out["table_bytes"] <= LLC_BYTES
+    out["regime"] = "latency (table in the Infinity Cache)" if out["llc_resident"] else "hbm random access"
     prof = pmc_profile(workload, depth)
     if prof and prof.get("atomics_per_step") is not None:
         out["pmc_atomics_per_search"] = int(prof["atomics_per_step"])

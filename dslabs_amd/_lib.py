@@ -114,7 +114,7 @@ class dsl_stats(ctypes.Structure):
                 ("table_slots", ctypes.c_uint64), ("terminal_finds", ctypes.c_uint64),
                 ("sharded_levels", ctypes.c_uint64), ("probes", ctypes.c_uint64),
                 ("host_syncs", ctypes.c_uint64), ("table_rehashes", ctypes.c_uint64),
-                ("rccl_version", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("rccl_version", ctypes.c_int32), ("level_slots", ctypes.c_int32),
                 ("cost_c_ns", ctypes.c_double), ("cost_x_us", ctypes.c_double), ("shard_work_min", ctypes.c_uint64)]
 
 

@@ -30,9 +30,6 @@
 
 // LDS budget for a k_level chunk's parent rows: with the kernel's ~11 KB of static LDS, 4
 // resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
-#ifndef DSL_QGRID_MIN
-#define DSL_QGRID_MIN 1024  // fewest workgroups of a queued k_level launch
-#endif
 #ifndef DSL_ROWS_LDS_KB
 #define DSL_ROWS_LDS_KB 24
 #endif
@@ -423,20 +420,6 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
-  // Parents per workgroup chunk: about three passes of 256 lanes at the observed branching,
-  // within the LDS budget of 4 resident workgroups per CU; a small level is spread over at least
-  // ~1024 workgroups instead (one short pass each), since its time is the serial latency chain
-  // of one chunk, not throughput; a large level gets equal chunks in whole rounds of the
-  // resident workgroups (balanced_chunk).
-#ifndef DSL_LEVEL_GRID
-#define DSL_LEVEL_GRID 1024
-#endif
-  static constexpr uint64_t kLevelGrid = DSL_LEVEL_GRID;
-  // k_level workgroups resident at once: 4 per CU (4 waves/SIMD, 256 CUs)
-#ifndef DSL_SLOTS
-#define DSL_SLOTS 1024
-#endif
-  static constexpr int kSlots = DSL_SLOTS;
   // Replicated or hash-sharded (multi-shard searches, see run()). dsl_engine_config.replicate_below
   // n > 0: a level whose frontier holds fewer than n states runs replicated; 0: every level is
   // sharded; -1 (automatic): a level is sharded once sharding it pays, by the cost model
@@ -460,11 +443,42 @@ struct BfsEngine : EngineBase {
   uint64_t queue_wlimit(uint64_t span) const {
     return W > 1 && auto_rep() ? std::min<uint64_t>(8 * span, shard_work_min) : 8 * span;
   }
-  int chunk_parents(uint64_t F) const {
-    const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
-    int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / per);
-    int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
-    return balanced_chunk(F, std::max(1, std::min({want, lds_max, kLevelBlock})), kSlots);
+  // Parents per chunk at most: about three passes of 256 lanes at the observed branching, within
+  // the LDS budget of the staged rows.
+  static constexpr size_t kRowLds = (size_t)NW * 4 + sizeof(Fp) + 4;  // LDS per staged parent
+  int pb_max() const {
+    const int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / kRowLds);
+    const int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
+    return std::max(1, std::min({want, lds_max, kLevelBlock}));
+  }
+  // k_level workgroups resident at once on the device with `lds` bytes of dynamic LDS: the
+  // occupancy of the protocol's instantiation (registers, LDS) x the CUs -- 1,024 for C5's
+  // Multi-Paxos (128 VGPRs: 4 per CU), more for a protocol with small rows and few registers (the
+  // synthetic C3: 48 VGPRs). The grids and the chunk rounds are sized for it. DSL_SLOTS_RT forces it.
+  std::vector<std::pair<uint64_t, int>> slot_cache;
+  int level_slots(size_t lds, bool route = false) {
+    if (const char* e = getenv("DSL_SLOTS_RT")) return stats.level_slots = std::max(64, atoi(e));
+    const uint64_t key = lds * 2 + (route ? 1 : 0);
+    for (auto& kv : slot_cache)
+      if (kv.first == key) {
+        stats.level_slots = std::max(stats.level_slots, kv.second);
+        return kv.second;
+      }
+    int occ = 0, cus = 0, dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const hipError_t e = route ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_level<P, true>, kLevelBlock, lds)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_level<P, false>, kLevelBlock, lds);
+    if (e != hipSuccess || occ <= 0) occ = 4;
+    (void)hipGetLastError();
+    const int slots = std::min(8192, std::max(256, occ * cus));
+    slot_cache.push_back({key, slots});
+    stats.level_slots = std::max(stats.level_slots, slots);
+    return slots;
+  }
+  int chunk_parents(uint64_t F, bool route = false) {
+    const int pb = pb_max();
+    return balanced_chunk(F, pb, level_slots((size_t)pb * kRowLds + 16, route));
   }
 
   // Enqueues up to kQueue levels of shard 0 (see the members above); returns how many ran.
@@ -504,11 +518,9 @@ struct BfsEngine : EngineBase {
     const size_t lev0 = S.level_size.size();  // the history level of the first queued level's rows
     for (int j = 0; j < nq; j++) DSL_TRY(hist_grow(S, lev0 + j, span, 0));
     DSL_TRY(grow(&S.spill, &S.spill_cap, wlimit, false, 0));
-    const size_t per = (size_t)NW * 4 + sizeof(Fp) + 4;
-    const int pb_max = std::max(1, std::min({(int)((DSL_ROWS_LDS_KB * 1024) / per), kLevelBlock,
-                                             (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) /
-                                                   std::max<uint64_t>(avg_events_x16, 1))}));
-    const int spread = kSlots;
+    const size_t per = kRowLds;
+    const int pb_max = this->pb_max();
+    const int spread = level_slots((size_t)pb_max * per + 16);
     SegTable t0{};
     t0.n = (int32_t)S.seg_cnt.size();
     t0.pb = balanced_chunk(S.F, pb_max, spread);
@@ -560,7 +572,8 @@ struct BfsEngine : EngineBase {
       if (j == 0 && q_events) DSL_HIP(hipEventRecord(qev[0], stream));
       // grid: one chunk per workgroup at the predicted frontier size (the kernel loops over more)
       const double fpred = (double)S.F * std::pow(growth, (double)j);
-      const int grid = (int)std::min<double>(kLevelGrid, std::max<double>(DSL_QGRID_MIN, std::ceil(1.5 * fpred / pb_max)));
+      (void)fpred;
+      const int grid = spread;
       hipLaunchKernelGGL((k_level<P, false>), dim3(grid), dim3(kLevelBlock), lds, stream, a, prm, dset);
       DSL_HIP(hipGetLastError());
     }
@@ -620,6 +633,12 @@ struct BfsEngine : EngineBase {
   static constexpr int kKeyRisk = 37;
   static constexpr int DSL_RESTART_REKEY = 1;
   uint64_t rekey_buckets = 0;
+  // Probe mode (fingerprint.hpp table_insert): load first when the tables are well beyond the
+  // Infinity Cache (256 MiB); DSL_PROBE_LOAD=0 / 1 forces it.
+  int probe_load_first(uint64_t buckets) const {
+    if (const char* e = getenv("DSL_PROBE_LOAD")) return atoi(e) ? 1 : 0;
+    return buckets * 64 * (uint64_t)sh.size() > (1ull << 30) ? 1 : 0;
+  }
   int ensure_table(uint64_t need_states) {
     const uint64_t have = tbl.bucket_mask + 1;
     uint64_t nb = have;
@@ -682,6 +701,7 @@ struct BfsEngine : EngineBase {
     }
     for (auto* q : old) (void)hipFree(q);
     tbl.bucket_mask = nb - 1;
+    tbl.load_first = probe_load_first(nb);
     table_buckets = nb;
     stats.table_rehashes++;
     stats.table_slots = nb * 8 * (uint64_t)W;
@@ -716,6 +736,7 @@ struct BfsEngine : EngineBase {
     uint64_t F = 0;
     for (uint64_t c : S.seg_cnt) F += c;
     const int PB = chunk_parents(F);
+    const int slots = level_slots((size_t)pb_max() * kRowLds + 16);
     LevelArgs<P> a{};
     a.cur = S.cur;
     a.cur_fp = S.cur_fp;
@@ -744,8 +765,9 @@ struct BfsEngine : EngineBase {
     a.me = S.gid;
     a.find = 1;
     a.find_key = key;
+    a.qspread = slots;
     const uint64_t nchunks = a.segs.chunk0[a.segs.n];
-    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, kLevelGrid));
+    const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)slots));
     const size_t lds = (size_t)PB * (NW * 4 + sizeof(Fp) + 4) + 16;
     hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
     DSL_HIP(hipGetLastError());
@@ -869,6 +891,7 @@ struct BfsEngine : EngineBase {
     if (const char* qr = getenv("DSL_QUEUE_ROWS")) q_rows_forced = std::max<uint64_t>(kSegs, strtoull(qr, nullptr, 10) / kSegs * kSegs);
     const bool trace_levels = getenv("DSL_LEVEL_TRACE") != nullptr;
     tbl = Table{nullptr, buckets - 1, 0, 0};
+    tbl.load_first = probe_load_first(buckets);
     while ((2ull << tbl.b0) <= buckets) tbl.b0++;  // log2(buckets): the key layout of this search
     inserted = 1;
     uint64_t prev_new = 0, prev_work = 0;  // the last level's new states and work items (est_new_states)
@@ -1037,7 +1060,8 @@ struct BfsEngine : EngineBase {
         // kernel, so the estimate never fails and never reserves the worst case.
         uint64_t Fmax = 0;
         for (auto& S : sh) Fmax = std::max(Fmax, S.F);
-        const int PB = chunk_parents(Fmax);
+        const int PB = chunk_parents(Fmax, route);
+        const int lslots = level_slots((size_t)pb_max() * kRowLds + 16, route);
         if (queued) {
           sh[0].nseg = kSegs;
           sh[0].segcap = q_segcap;
@@ -1045,7 +1069,7 @@ struct BfsEngine : EngineBase {
         for (auto& S : sh) {
           uint64_t nchunks = 0;
           for (size_t q = 0; q < S.seg_cnt.size(); q++) nchunks += (S.seg_cnt[q] + PB - 1) / PB;
-          const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(nchunks, kLevelGrid));
+          const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)lslots));
           S.nseg = (int)std::min<uint64_t>(kSegs, blocks);
           const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 8192)) + 1;
           S.segcap = (want + S.nseg - 1) / S.nseg + 1;
@@ -1106,10 +1130,11 @@ struct BfsEngine : EngineBase {
           a.qprev = nullptr;
           a.qprev_seg = nullptr;
           a.segs.pb = PB;
+          a.qspread = lslots;
           a.t0_rt = t0_rt;
           a.budget_rt = level_budget(rep);
           const uint64_t nchunks = a.segs.chunk0[a.segs.n];
-          const int blocks = (int)std::min<uint64_t>(nchunks, kLevelGrid);
+          const int blocks = (int)std::min<uint64_t>(nchunks, (uint64_t)lslots);
           if (route)
             hipLaunchKernelGGL((k_level<P, true>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
           else

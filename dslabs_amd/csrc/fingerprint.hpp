@@ -86,7 +86,7 @@ struct Table {
   unsigned long long* slots;  // nbuckets * 8
   uint64_t bucket_mask;       // nbuckets - 1 (power of two)
   int32_t b0;                 // log2(buckets) of the search's first table: the key layout
-  int32_t pad;
+  int32_t load_first;         // probe by a load first, CAS only an empty slot (table_insert)
 };
 
 DSL_HD uint64_t table_key0(const Table& t, const Fp& f) {
@@ -104,6 +104,11 @@ DSL_HD uint64_t table_home(const Table& t, const Fp& f) { return ((f.lo & t.buck
 // the memory side (coherent across the 8 XCD L2s), so a probe is ONE memory round trip whether the
 // state is new or not (a bucket load followed by a CAS was two for every new state: +18 % at d12,
 // +26 % at d14 on C5, profiles/r02_*).
+//
+// load_first (a table far beyond the Infinity Cache, where probes are bound by the memory-side
+// atomic rate rather than latency): each slot is read with a plain load first and only an empty
+// one is CAS'd. A load can only be stale towards 0 (slots are write-once), which the CAS then
+// corrects, so the answer is the same; a state already present costs a read instead of an atomic.
 __device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
   const uint64_t k0 = table_key0(t, f), home = table_home(t, f), nmask = t.bucket_mask * 8 + 7;
   uint64_t i = home;
@@ -111,8 +116,12 @@ __device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
     const uint64_t d = ((i >> 3) - (home >> 3)) & t.bucket_mask;
     if (d > (uint64_t)kMaxDisp) break;
     const unsigned long long key = (unsigned long long)(k0 | (d << 1));
-    const unsigned long long old = atomicCAS(t.slots + i, 0ull, key);
-    if (old == 0ull) return INS_NEW;
+    unsigned long long old = 0ull;
+    if (t.load_first) old = __hip_atomic_load(t.slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == 0ull) {
+      old = atomicCAS(t.slots + i, 0ull, key);
+      if (old == 0ull) return INS_NEW;
+    }
     if (old == key) return INS_EXISTS;
     i = (i + 1) & nmask;
   }

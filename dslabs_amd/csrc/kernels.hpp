@@ -35,12 +35,6 @@ constexpr int kMaxShards = 16;
 #define DSL_KWIN 1024
 #endif
 constexpr int kWin = DSL_KWIN;  // work items per class-sorted window of k_level
-// Levels of at most this many chunks (one round of the 1,024 resident workgroups) spread each
-// pass over all of a workgroup's waves (k_level step 4).
-#ifndef DSL_SLOTS
-#define DSL_SLOTS 1024
-#endif
-constexpr int kSpreadChunks = DSL_SLOTS;
 // The next frontier is written into up to kSegs segments, one reservation counter each (a
 // workgroup appends to segment blockIdx % nseg), so every wavefront reserves its rows with one
 // returning atomic and no workgroup barrier, and no counter word carries more than 1/kSegs of
@@ -375,7 +369,8 @@ struct LevelArgs {
   uint64_t qflimit, qwlimit;         // the queue stops above these frontier / work sizes
   uint64_t qroom;                    // ... and before a level whose estimated new states would
                                      // take the visited table past half full (table_room)
-  int32_t qspread;                   // resident workgroups: parents per chunk = balanced_chunk(F, PB, qspread)
+  int32_t qspread;                   // resident workgroups (BfsEngine::level_slots): a level of at most
+                                     // this many chunks is one round; queued: pb = balanced_chunk(F, PB, qspread)
   uint32_t term_cap;                 // TerminalRec entries of `terms`
   int32_t find;                      // find mode (no table, no rows): the successor whose terminal
   uint64_t find_key;                 // key equals find_key is recorded in terms[0]
@@ -479,8 +474,15 @@ __device__ __forceinline__ void fold_terminals(bool term, uint64_t key, int v, i
 
 // Occupancy floor of 4 waves/SIMD (<= 128 VGPRs): a latency-bound kernel (r01 on C5 Multi-Paxos:
 // 2 waves/SIMD 1.5x slower, 3 waves/SIMD 7-11 % slower at d12/d14, 5 waves/SIMD 1.5-1.65x slower).
+// A protocol with small states and short handlers (P::kLevelWaves, e.g. the synthetic C3) asks for
+// more waves per SIMD: its instantiation then fits in fewer registers and more workgroups are
+// resident (BfsEngine::level_slots sizes the grid from the occupancy).
+template <class P, class = void>
+struct LevelWaves : std::integral_constant<int, 4> {};
+template <class P>
+struct LevelWaves<P, std::void_t<decltype(P::kLevelWaves)>> : std::integral_constant<int, P::kLevelWaves> {};
 #ifndef DSL_KLEVEL_ATTR
-#define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#define DSL_KLEVEL_ATTR __attribute__((amdgpu_waves_per_eu(LevelWaves<P>::value)))
 #endif
 template <class P, bool ROUTE>
 __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
@@ -566,7 +568,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   }
   const int PB = s_segs.pb;
   const uint64_t nchunks = s_segs.chunk0[s_segs.n];
-  const bool spread = nchunks <= (uint64_t)kSpreadChunks;
+  const bool spread = nchunks <= (uint64_t)a.qspread;  // at most one round of resident workgroups
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
   int g = 0;
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {

@@ -18,9 +18,14 @@
 
 namespace dsl {
 
+#ifndef DSL_SYNTH_WAVES
+#define DSL_SYNTH_WAVES 8
+#endif
+
 struct Synthetic {
   static constexpr int kMaxNodes = 5;
   static constexpr int kNodes = kMaxNodes, kNodeWords = 2, kNetCap = kMaxNodes, kMaxSends = 1;
+  static constexpr int kLevelWaves = DSL_SYNTH_WAVES;  // k_level waves per SIMD (kernels.hpp LevelWaves)
   static constexpr int kMsgClasses = 1;  // handler classes of messages (Poke); timers: class 1
   static constexpr int kTimerMin = 1, kTimerMax = 100;
   using Rec = uint32_t;

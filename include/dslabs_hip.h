@@ -299,7 +299,7 @@ typedef struct {
   uint64_t host_syncs;       /* host round trips of the search: stream synchronizations and collectives */
   uint64_t table_rehashes;   /* visited-table growths (rehashed into a table twice the size) */
   int32_t rccl_version;      /* ncclGetVersion() of the RCCL the engine bound (multi-GPU), 0 otherwise */
-  int32_t reserved;
+  int32_t level_slots;       /* k_level workgroups resident at once (occupancy x CUs): the grid of a level */
   /* multi-shard cost model (replicate_below = -1), as agreed by the ranks for this search: k_level ns
      per work item, the non-kernel time of a sharded level (us; 0 = not measured yet, defaults used),
      and the resulting work threshold above which a level is sharded */

@@ -248,6 +248,8 @@ DEEP = {
                                         "--max-depth", "14", "--finish-level"], pinned={}, timeout=7200),
     # BASELINE C3 through depth 7
     "synth_c3_d7": dict(args=SY + ["--inv", "NOT_ALL_MAX", "--max-depth", "7"], pinned={}, timeout=7200),
+    # ... and through depth 8: 30,341,487 states (19 min on the oracle), the deepest C3 pin
+    "synth_c3_d8": dict(args=SY + ["--inv", "NOT_ALL_MAX", "--max-depth", "8"], pinned={}, timeout=7200),
 }
 
 

@@ -45,3 +45,32 @@ def test_synthetic_sharded(shards, rep):
         case = GOLD[name]
         r = _run(case, virtual_shards=shards, replicate_below=rep)
         assert r.per_depth == case["per_depth"], (name, shards)
+
+
+def test_synthetic_c3_bench_config_depth10(monkeypatch):
+    """The C3 bench configuration itself (bench.py --workload synthetic: maxDepth 10, 780,909,037
+    states, a 2^31-slot table far beyond the Infinity Cache): its depth-0..8 counts equal the
+    oracle's deepest pin (tests/golden/deep.json synth_c3_d8), depth 9 equals the multithreaded host
+    BFS over the same transition functions (tools/cpu_bfs.cpp: another engine, not the kernels),
+    and both probe modes (load-first, the default at this table size; CAS-only) give the same
+    vector at full size."""
+    import sys
+    deep = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "deep.json")))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from tools import cpu_baseline
+    proto, s, _ = bench.build_search("synthetic", 10)
+    e = Engine(proto)
+    try:
+        r = e.bfs(proto.initial_state(), s)
+        monkeypatch.setenv("DSL_PROBE_LOAD", "0")
+        r0 = e.bfs(proto.initial_state(), s)
+    finally:
+        e.close()
+    assert r.per_depth == r0.per_depth
+    assert r.states == sum(r.per_depth) == 780909037
+    assert r.per_depth[:9] == deep["synth_c3_d8"]["per_depth"]
+    s9 = s.clone()
+    s9.maxDepth(9)
+    c = cpu_baseline.run(proto, s9, table_log2=29)
+    assert c["per_depth"] == r.per_depth[:10], c["per_depth"]
