@@ -22,8 +22,12 @@ import java.util.Set;
  * replaying the device trace with stepEvent(e, settings, false) (TraceReplaySearch.java:76-101
  * semantics), so trace printing and SerializableTrace work unchanged. A mid-search start state is
  * packed by replaying its own trace on the engine (dsl_replay, then dsl_set_initial). A protocol,
- * predicate or event with no device form (GpuProtocols / GpuPredicates return null), a start state
- * with a dropped network, or no visible GPU runs the JVM search.
+ * predicate or event with no device form (GpuProtocols / GpuPredicates return null), or no visible
+ * GPU runs the JVM search. A start state with a dropped network (PaxosTest's narrowed searches:
+ * dropPendingMessages, then undropMessagesFrom / To, PaxosTest.java:1065-1132) is packed the same
+ * way on the engine (dsl_drop_pending_messages, dsl_undrop_messages) and its dropped set handed to
+ * the search (dsl_set_dropped); a dropped network no sequence of those calls produces keeps the JVM
+ * search.
  * This file is part of the integration layer (INTEGRATION.md); it is not compiled in this build,
  * whose image has no JDK.
  */
@@ -36,17 +40,71 @@ public final class GpuBFS {
     List<SearchState> chain = new ArrayList<>();
     init.trace().forEach(chain::add);
     GpuProtocols.Desc desc = GpuProtocols.describe(chain.get(0));
-    if (desc == null || hasDroppedNetwork(init)) return Search.bfs(init, settings);
+    if (desc == null) return Search.bfs(init, settings);
+    Undrop undrop = undrop(init, desc);
+    if (undrop == null) return Search.bfs(init, settings);
     try (Dsl.Engine eng = new Dsl.Engine(desc.protocol())) {
       MemorySegment enc = GpuPredicates.encode(settings, desc.addresses(), desc.leaf(), eng.arena());
       byte[] packed = enc == null ? null : start(eng, desc, chain);
       if (packed == null) return Search.bfs(init, settings);
       eng.setSettings(enc);
+      if (undrop.dropped()) {
+        if (packed.length == 0) return Search.bfs(init, settings);  // an initial state has nothing to drop
+        eng.setDropped(eng.dropPending(packed, undrop.from(), undrop.to()));
+      }
       if (packed.length > 0) eng.setInitial(packed, init.depth());
       Dsl.Result r = eng.run();
       return results(init, settings, desc, r);
     }
   }
+
+  /**
+   * How a start state's live network follows from its dropped one: every message was dropped
+   * (dropPendingMessages), then those from the nodes `from` and to the nodes `to` were undropped.
+   * dropped() is false for a state that never dropped anything; null when the live network is not
+   * such a union (the JVM search then runs).
+   */
+  record Undrop(boolean dropped, int[] from, int[] to) {}
+
+  @SuppressWarnings("unchecked")
+  private static Undrop undrop(SearchState s, GpuProtocols.Desc desc) {
+    // the two sets of SearchState (SearchState.java:71-77): network() is their union
+    Set<MessageEnvelope> dropped, live;
+    try {
+      java.lang.reflect.Field d = SearchState.class.getDeclaredField("droppedNetwork");
+      java.lang.reflect.Field n = SearchState.class.getDeclaredField("network");
+      d.setAccessible(true);
+      n.setAccessible(true);
+      dropped = (Set<MessageEnvelope>) d.get(s);
+      live = (Set<MessageEnvelope>) n.get(s);
+    } catch (ReflectiveOperationException e) {
+      return null;
+    }
+    if (dropped.isEmpty()) return new Undrop(false, new int[0], new int[0]);
+    if (!dropped.containsAll(live)) return null;  // sent after the drop: not an undrop
+    List<Integer> from = new ArrayList<>(), to = new ArrayList<>();
+    Set<MessageEnvelope> union = new HashSet<>();
+    for (int i = 0; i < desc.addresses().size(); i++) {
+      var a = desc.addresses().get(i);
+      Set<MessageEnvelope> sent = new HashSet<>(), got = new HashSet<>();
+      for (MessageEnvelope m : dropped) {
+        if (m.from().rootAddress().equals(a)) sent.add(m);
+        if (m.to().rootAddress().equals(a)) got.add(m);
+      }
+      if (!sent.isEmpty() && live.containsAll(sent)) {
+        from.add(i);
+        union.addAll(sent);
+      }
+      if (!got.isEmpty() && live.containsAll(got)) {
+        to.add(i);
+        union.addAll(got);
+      }
+    }
+    if (!union.equals(live)) return null;
+    return new Undrop(true, from.stream().mapToInt(Integer::intValue).toArray(),
+        to.stream().mapToInt(Integer::intValue).toArray());
+  }
+
 
   /**
    * BaseJUnitTest.traceReplay (BaseJUnitTest.java:279-284, TraceReplaySearch.java:76-101) on the
@@ -61,7 +119,7 @@ public final class GpuBFS {
     List<SearchState> chain = new ArrayList<>();
     init.trace().forEach(chain::add);
     GpuProtocols.Desc desc = GpuProtocols.describe(chain.get(0));
-    if (desc == null || hasDroppedNetwork(init)) return null;
+    if (desc == null || undrop(init, desc) == null || undrop(init, desc).dropped()) return null;
     Dsl.Event[] evs = new Dsl.Event[trace.size()];
     for (int i = 0; i < evs.length; i++)
       if ((evs[i] = desc.encoder().encode(trace.get(i))) == null) return null;
@@ -91,17 +149,6 @@ public final class GpuBFS {
     if (r.endCondition() != Dsl.END_SPACE_EXHAUSTED || r.trace().length != evs.length || r.terminalState() == null)
       return null;  // a step threw, or the engine could not deliver an event the JVM did
     return r.terminalState();
-  }
-
-  // SearchState.dropPendingMessages (SearchState.java:538-541) leaves messages in network() that
-  // events() no longer offers; such a start state keeps the JVM search.
-  private static boolean hasDroppedNetwork(SearchState s) {
-    Set<MessageEnvelope> live = new HashSet<>();
-    for (Event e : s.events(new SearchSettings()))
-      if (e instanceof MessageEnvelope m) live.add(m);
-    for (MessageEnvelope m : s.network())
-      if (!live.contains(m)) return true;
-    return false;
   }
 
   private static SearchResults results(SearchState init, SearchSettings settings, GpuProtocols.Desc desc,

@@ -47,7 +47,7 @@ public final class Dsl {
   public static final int MAX_EVENT_FIELDS = 8;
 
   // dsl_protocol_id (include/dslabs_hip.h)
-  public static final int PROTO_PINGPONG = 1, PROTO_SIPAXOS = 2, PROTO_MULTIPAXOS = 5;
+  public static final int PROTO_PINGPONG = 1, PROTO_SIPAXOS = 2, PROTO_AMOKV = 4, PROTO_MULTIPAXOS = 5, PROTO_PB = 6;
 
   // dsl_end_condition (include/dslabs_hip.h)
   public static final int END_EXCEPTION_THROWN = 0, END_INVARIANT_VIOLATED = 1, END_GOAL_FOUND = 2,
@@ -75,6 +75,10 @@ public final class Dsl {
   static final MethodHandle ABI = fn("dsl_abi_version", FunctionDescriptor.of(I));
   static final MethodHandle REPLAY = fn("dsl_replay", FunctionDescriptor.of(I, A, A, I, I, A));
   static final MethodHandle SET_DROPPED = fn("dsl_set_dropped", FunctionDescriptor.of(I, A, A, I));
+  static final MethodHandle DROP_PENDING =
+      fn("dsl_drop_pending_messages", FunctionDescriptor.of(I, A, A, ValueLayout.JAVA_LONG, A, I, A));
+  static final MethodHandle UNDROP =
+      fn("dsl_undrop_messages", FunctionDescriptor.of(I, A, A, ValueLayout.JAVA_LONG, A, I, I, I));
 
   private Dsl() {}
 
@@ -110,9 +114,10 @@ public final class Dsl {
   public static final class Engine implements AutoCloseable {
     private final Arena arena = Arena.ofConfined();
     private final MemorySegment handle;
+    private final MemorySegment desc;
 
     public Engine(Protocol p) {
-      MemorySegment desc = arena.allocate(SIZE_PROTOCOL_DESC, 8);
+      desc = arena.allocate(SIZE_PROTOCOL_DESC, 8);
       desc.set(ValueLayout.JAVA_INT, OFF_DESC_PROTOCOL, p.id());
       desc.set(ValueLayout.JAVA_INT, OFF_DESC_N_PARAMS, p.params().length);
       for (int i = 0; i < p.params().length; i++)
@@ -163,6 +168,38 @@ public final class Dsl {
       for (int i = 0; i < records.length; i++) buf.set(ValueLayout.JAVA_LONG, 8L * i, records[i]);
       try {
         check((int) SET_DROPPED.invokeExact(handle, buf, records.length), "dsl_set_dropped");
+      } catch (RuntimeException e) {
+        throw e;
+      } catch (Throwable t) {
+        throw new IllegalStateException(t);
+      }
+    }
+
+    /**
+     * SearchState.dropPendingMessages then undropMessagesFrom / undropMessagesTo
+     * (SearchState.java:538-561) on a packed state (dsl_drop_pending_messages, dsl_undrop_messages):
+     * every record of its network moves into the returned dropped set (sorted, distinct), then the
+     * dropped records sent by each node of `undropFrom` and addressed to each node of `undropTo`
+     * (node indices) are live again. `packed` is updated in place.
+     */
+    public long[] dropPending(byte[] packed, int[] undropFrom, int[] undropTo) {
+      final int cap = 4096;
+      MemorySegment st = arena.allocate(packed.length, 8);
+      MemorySegment.copy(MemorySegment.ofArray(packed), 0, st, 0, packed.length);
+      MemorySegment dr = arena.allocate(8L * cap, 8);
+      MemorySegment n = arena.allocate(I);
+      n.set(I, 0, 0);
+      try {
+        check((int) DROP_PENDING.invokeExact(desc, st, (long) packed.length, dr, cap, n), "dsl_drop_pending_messages");
+        int nd = n.get(I, 0);
+        for (int a : undropFrom)
+          check((int) UNDROP.invokeExact(desc, st, (long) packed.length, dr, nd, a, -1), "dsl_undrop_messages");
+        for (int b : undropTo)
+          check((int) UNDROP.invokeExact(desc, st, (long) packed.length, dr, nd, -1, b), "dsl_undrop_messages");
+        MemorySegment.copy(st, 0, MemorySegment.ofArray(packed), 0, packed.length);
+        long[] out = new long[nd];
+        for (int i = 0; i < nd; i++) out[i] = dr.get(ValueLayout.JAVA_LONG, 8L * i);
+        return out;
       } catch (RuntimeException e) {
         throw e;
       } catch (Throwable t) {

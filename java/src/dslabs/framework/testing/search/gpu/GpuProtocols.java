@@ -34,8 +34,10 @@ import org.apache.commons.lang3.tuple.Pair;
  * dsl_set_initial), and replaying a saved trace (GpuBFS.traceReplay).
  *
  * <p>Covered: lab0 PingPong (labs/lab0-pingpong), the reference's single-instance Paxos
- * (T/visualization/examples/paxosmadesimple) and lab3 Multi-Paxos (java/src/dslabs/paxos, the
- * solution of DESIGN.md §9). Lab classes are read by reflection (class simple names and field
+ * (T/visualization/examples/paxosmadesimple), lab1 AMO KV (java/src/dslabs/clientserver, the
+ * solution of DESIGN.md §11: BASELINE C2), lab2 primary-backup + ViewServer
+ * (java/src/dslabs/primarybackup, DESIGN.md §12: C4) and lab3 Multi-Paxos (java/src/dslabs/paxos,
+ * DESIGN.md §9: C5). Lab classes are read by reflection (class simple names and field
  * names), since this file is compiled with every lab and each lab has only its own classes.
  * Anything else returns null (GpuBFS then runs the JVM search).
  */
@@ -74,6 +76,8 @@ public final class GpuProtocols {
       if (first.equals("PingServer")) return pingPong(addrs, nodes);
       if (first.endsWith("Proposer")) return sipaxos(addrs, nodes);
       if (first.equals("PaxosServer")) return multiPaxos(addrs, nodes);
+      if (first.equals("SimpleServer")) return amoKV(addrs, nodes);
+      if (first.equals("ViewServer")) return primaryBackup(addrs, nodes);
     } catch (ReflectiveOperationException | ClassCastException e) {
       return null;  // a class of that name with another shape: not the protocol the engine has
     }
@@ -82,8 +86,8 @@ public final class GpuProtocols {
 
   private static int rank(Node n) {
     String c = simpleName(n);
-    return c.equals("PingServer") || c.endsWith("Proposer") || c.equals("PaxosServer") ? 0
-        : c.equals("Acceptor") ? 1 : 2;
+    return c.equals("PingServer") || c.endsWith("Proposer") || c.equals("PaxosServer") || c.equals("SimpleServer")
+        || c.equals("ViewServer") ? 0 : c.equals("Acceptor") || c.equals("PBServer") ? 1 : 2;
   }
 
   // ---- lab0 PingPong: "pingserver", then ClientWorkers around PingClients (PingTest.java:44-51) ----
@@ -204,6 +208,86 @@ public final class GpuProtocols {
     MultiPaxosCodec codec = MultiPaxosCodec.of(addrs, n, work);
     if (codec == null) return null;
     return new Desc(new Dsl.Protocol(Dsl.PROTO_MULTIPAXOS, codec.params()), addrs, multiPaxosLeaf(addrs, n, codec), codec::encode);
+  }
+
+  // ---- lab1 AMO KV: "server", then ClientWorkers around SimpleClients (DESIGN.md §11) ----
+  private static Desc amoKV(List<Address> addrs, List<Node> nodes) throws ReflectiveOperationException {
+    if (!addrs.get(0).toString().equals("server")) return null;
+    List<List<Pair<Command, Result>>> work = new ArrayList<>();
+    for (int i = 1; i < nodes.size(); i++) {
+      if (!(nodes.get(i) instanceof ClientWorker cw) || !simpleName(field(cw, "client")).equals("SimpleClient"))
+        return null;
+      List<Pair<Command, Result>> w = commands(cw, addrs.get(i));
+      if (w == null) return null;
+      work.add(w);
+    }
+    AmoKVCodec codec = AmoKVCodec.of(addrs, work);
+    if (codec == null) return null;
+    Function<String, GpuPredicates.Leaf> leaf = name -> {
+      Integer id = STANDARD.get(name);
+      if (id != null) return new GpuPredicates.Leaf(id, 0, 0);
+      return name.equals("Sequence of appends to the same key is linearizable") ? new GpuPredicates.Leaf(300, 0, 0)
+          : null;
+    };
+    return new Desc(new Dsl.Protocol(Dsl.PROTO_AMOKV, codec.params()), addrs, leaf, codec::encode);
+  }
+
+  // ---- lab2 primary-backup: "viewserver", PBServers, ClientWorkers around PBClients (DESIGN.md §12) ----
+  private static Desc primaryBackup(List<Address> addrs, List<Node> nodes) throws ReflectiveOperationException {
+    int n = 0;
+    while (1 + n < nodes.size() && simpleName(nodes.get(1 + n)).equals("PBServer")) n++;
+    List<List<Pair<Command, Result>>> work = new ArrayList<>();
+    for (int i = 1 + n; i < nodes.size(); i++) {
+      if (!(nodes.get(i) instanceof ClientWorker cw) || !simpleName(field(cw, "client")).equals("PBClient"))
+        return null;
+      List<Pair<Command, Result>> w = commands(cw, addrs.get(i));
+      if (w == null) return null;
+      work.add(w);
+    }
+    PBCodec codec = PBCodec.of(addrs, n, work);
+    if (codec == null) return null;
+    return new Desc(new Dsl.Protocol(Dsl.PROTO_PB, codec.params()), addrs, pbLeaf(addrs, n), codec::encode);
+  }
+
+  // PrimaryBackupTest's predicates (PrimaryBackupTest.java:104-117, initView's goal :136-156)
+  private static final String VIEW = "View\\(viewNum=(\\d+), primary=([^,]+), backup=([^)]+)\\)";
+  private static final Pattern HAS_VIEW_REPLY = Pattern.compile("ViewReply with viewNum: (\\d+)");
+  private static final Pattern HAS_VIEW_REPLY_EXACT = Pattern.compile("ViewReply with " + VIEW);
+  private static final Pattern VIEW_REPLIES_SENT =
+      Pattern.compile("ViewReply for " + VIEW + " sent to nodes \\[(.*)\\], primary ack sent");
+
+  private static Function<String, GpuPredicates.Leaf> pbLeaf(List<Address> addrs, int servers) {
+    return name -> {
+      Integer id = STANDARD.get(name);
+      if (id != null) return new GpuPredicates.Leaf(id, 0, 0);
+      Matcher m = HAS_VIEW_REPLY.matcher(name);
+      if (m.matches()) return new GpuPredicates.Leaf(500, Long.parseLong(m.group(1)), 0);
+      m = HAS_VIEW_REPLY_EXACT.matcher(name);
+      if (m.matches()) {
+        long v = viewBits(addrs, servers, m);
+        return v < 0 ? null : new GpuPredicates.Leaf(501, v, 0);
+      }
+      m = VIEW_REPLIES_SENT.matcher(name);
+      if (m.matches()) {
+        long v = viewBits(addrs, servers, m), mask = 0;
+        for (String a : m.group(4).split(", ")) {
+          int i = nodeIndex(addrs, a);
+          if (i < 0) return null;
+          mask |= 1L << i;
+        }
+        return v < 0 ? null : new GpuPredicates.Leaf(502, v, mask);
+      }
+      return null;
+    };
+  }
+
+  // A View's toString groups (viewNum, primary, backup) as num | primary id << 4 | backup id << 6
+  private static long viewBits(List<Address> addrs, int servers, Matcher m) {
+    long n = Long.parseLong(m.group(1));
+    int p = m.group(2).equals("null") ? 0 : nodeIndex(addrs, m.group(2));
+    int b = m.group(3).equals("null") ? 0 : nodeIndex(addrs, m.group(3));
+    if (n > 15 || p < 0 || p > servers || b < 0 || b > servers) return -1;
+    return n | (long) p << 4 | (long) b << 6;
   }
 
   // PaxosTest's predicates (PaxosTest.java:113-346) and KVStoreWorkload.APPENDS_LINEARIZABLE

@@ -84,7 +84,8 @@ def test_java_abi_version_and_protocol_ids_match_the_header():
     assert c["ABI_VERSION"] == int(re.search(r"#define DSL_ABI_VERSION (\d+)", HEADER).group(1)) == _lib.DSL_ABI_VERSION
     assert c["MAX_EVENT_FIELDS"] == int(re.search(r"#define DSL_MAX_EVENT_FIELDS (\d+)", HEADER).group(1))
     assert c["MAX_POOL"] == int(re.search(r"#define DSL_MAX_POOL (\d+)", HEADER).group(1))
-    for j, h in (("PINGPONG", "PINGPONG"), ("SIPAXOS", "SIPAXOS"), ("MULTIPAXOS", "MULTIPAXOS")):
+    for j, h in (("PINGPONG", "PINGPONG"), ("SIPAXOS", "SIPAXOS"), ("MULTIPAXOS", "MULTIPAXOS"), ("AMOKV", "AMOKV"),
+                 ("PB", "PB")):
         assert c["PROTO_" + j] == int(re.search(r"DSL_PROTO_%s = (\d+)" % h, HEADER).group(1))
     assert "dsl_abi_version" in DSL and "abi != ABI_VERSION" in DSL
 
@@ -113,8 +114,9 @@ def test_java_downcalls_match_the_c_prototypes():
         assert ret == ("void" if f.restype is None else _kind(f.restype)), sym
         assert java == [_kind(a) for a in (f.argtypes or [])], sym
         found += 1
-    assert found == 11  # create / set_settings / set_initial / run / result_free / destroy / last_error /
-    #                      device_count / abi_version / replay / set_dropped
+    assert found == 13  # create / set_settings / set_initial / run / result_free / destroy / last_error /
+    #                      device_count / abi_version / replay / set_dropped / drop_pending_messages /
+    #                      undrop_messages
 
 
 MPC = open(os.path.join(JAVA, "gpu", "MultiPaxosCodec.java")).read()
@@ -230,3 +232,104 @@ def test_java_multipaxos_predicate_leaves():
     m = re.fullmatch(kv, "KVStore.Append(key=foo, value=X)")
     assert m and m.groups() == ("Append", "foo", "X")
     assert (MultiPaxos.OPS["APPEND"] << 2 | 1) == mp.kv_code("APPEND:foo:X")
+
+
+AKC = open(os.path.join(JAVA, "gpu", "AmoKVCodec.java")).read()
+AKH = open(os.path.join(ROOT, "dslabs_amd", "csrc", "protocols", "amokv.hpp")).read()
+PBC = open(os.path.join(JAVA, "gpu", "PBCodec.java")).read()
+PBH = open(os.path.join(ROOT, "dslabs_amd", "csrc", "protocols", "pb.hpp")).read()
+
+
+def _hpp(text, name):
+    return int(re.search(r"\b%s = (\d+)" % name, text).group(1))
+
+
+def test_java_amokv_codec_matches_the_device_layout_and_protocols_py():
+    """lab1 (C2): AmoKVCodec's bounds, op / result / message codes, value and result bit layouts are
+    amokv.hpp's and protocols.py AmoKV's; its parameter rule (keys and value tokens numbered by first
+    use, client-major) builds AmoKV.params() for every workload."""
+    from dslabs_amd.protocols import AmoKV
+    c = consts(AKC)
+    assert (c["MAX_CLIENTS"], c["MAX_CMDS"], c["MAX_KEYS"], c["MAX_LEN"]) == tuple(
+        _hpp(AKH, k) for k in ("kMaxClients", "kMaxCmds", "kMaxKeys", "kMaxLen"))
+    for op, v in AmoKV.OPS.items():
+        assert c["OP_" + op] == v == _hpp(AKH, "OP_" + op)
+    for i, n in enumerate(AmoKV.RTYPES):
+        key = {"AppendResult": "R_APPEND", "GetResult": "R_GET", "KeyNotFound": "R_NOTFOUND", "PutOk": "R_PUTOK"}[n]
+        assert c[key] == i == _hpp(AKH, key)
+    for n in ("M_REQUEST", "M_REPLY", "T_CLIENT"):
+        assert c[n] == _hpp(AKH, n)
+    assert c["RETRY_MILLIS"] == _hpp(AKH, "kRetry")
+    assert "r |= (long) t << (4 + 2 * i)" in AKC and "v |= t << (4 + 2 * j)" in open(
+        os.path.join(ROOT, "dslabs_amd", "protocols.py")).read()
+    assert "R_APPEND | v << 2" in AKC and "R_GET | v << 2" in AKC
+    assert "int b = 2 + 4 * (c * MAX_CMDS + k);" in AKC and "const int b = 2 + 4 * (c * kMaxCmds + k);" in AKH
+    # the Java rule (first-use numbering of keys and tokens, client-major) restated: AmoKV.params()
+    for wl in AmoKV.WORKLOADS:
+        for clients in (1, 2, 3):
+            kv = AmoKV(clients, wl)
+            keys, syms = [], []
+            for cl in kv.cmds:
+                for op, key, val in cl:
+                    keys += [key] if key not in keys else []
+                    syms += [val] if val is not None and val not in syms else []
+            assert keys == kv.keys and syms == kv.syms, wl
+    # Java timers / messages carry the device's fields
+    tim = open(os.path.join(ROOT, "java", "src", "dslabs", "clientserver", "Timers.java")).read()
+    assert "CLIENT_RETRY_MILLIS = 100" in tim and "private final int sequenceNum;" in tim
+    assert 'Dsl.Event.message(from, to, M_REQUEST, seq, 0)' in AKC and 'e->n_fields = 2;' in AKH
+
+
+def test_java_pb_codec_matches_the_device_layout_and_protocols_py():
+    """lab2 (C4): PBCodec's bounds, message / timer codes, view, value, result and state-transfer
+    bit layouts are pb.hpp's; timer periods are the device's; the predicate patterns parse the
+    reference's predicate names (PrimaryBackupTest.java:104-156)."""
+    from dslabs_amd.protocols import PB
+    c = consts(PBC)
+    assert (c["MAX_SERVERS"], c["MAX_CLIENTS"], c["MAX_CMDS"], c["MAX_KEYS"]) == tuple(
+        _hpp(PBH, k) for k in ("kMaxServers", "kMaxClients", "kMaxCmds", "kMaxKeys"))
+    enum = re.search(r"enum \{ M_PING = 0, ([^}]*)\}", PBH).group(1)
+    names = ["M_PING"] + [e.split("=")[0].strip() for e in enum.split(",")]
+    for i, n in enumerate(names[:9]):
+        assert c[n] == i, n
+    for n in ("T_PINGCHECK", "T_PING", "T_CLIENT"):
+        assert c[n] == _hpp(PBH, n)
+    for op, v in (("GET", 0), ("PUT", 1), ("APPEND", 2)):
+        assert c["OP_" + op] == v == _hpp(PBH, "OP_" + op)
+    assert "n | p << 4 | b << 6" in PBC and "return n | (p << 4) | (b << 6); }" in PBH
+    assert PB._view_bits(3, 1, 2) == 3 | 1 << 4 | 2 << 6
+    assert "r |= (long) t << (2 + 2 * i)" in PBC and "v |= t << (2 + 2 * j)" in open(
+        os.path.join(ROOT, "dslabs_amd", "protocols.py")).read()
+    assert "bits |= v << (8 * k)" in PBC and "const int vb = 32 + 8 * key;" in PBH  # keys in w1
+    assert "(seq | r << 2) << (16 + 12 * c)" in PBC and "put(w, 48, 12, na); else put(w, 64, 12, na)" in PBH
+    assert "v | app << 8" in PBC and "(uint64_t)v | (app << 8)" in PBH
+    assert "| (long) ca << 4" in PBC and "((uint64_t)from << 4) | ((uint64_t)seq << 7)" in PBH
+    assert "int b = 3 + 4 * (c * MAX_CMDS + k);" in PBC and "const int b = 3 + 4 * (c * kMaxCmds + k);" in PBH
+    tim = open(os.path.join(ROOT, "java", "src", "dslabs", "primarybackup", "Timers.java")).read()
+    assert "PING_CHECK_MILLIS = 100" in tim and "PING_MILLIS = 25" in tim and "CLIENT_RETRY_MILLIS = 100" in tim
+    assert "e->timer_min = e->timer_max = 25;" in PBH
+    reg = open(os.path.join(JAVA, "gpu", "GpuProtocols.java")).read()
+    view = re.search(r'String VIEW = "([^"]*)";', reg).group(1).replace("\\\\", "\\")
+    pats = {k: re.search(r'%s =\s*Pattern.compile\(([^;]*)\);' % k, reg).group(1) for k in
+            ("HAS_VIEW_REPLY", "HAS_VIEW_REPLY_EXACT", "VIEW_REPLIES_SENT")}
+    java = {k: "".join(view if part.strip() == "VIEW" else part.strip().strip('"') for part in v.split("+"))
+            .replace("\\\\", "\\") for k, v in pats.items()}
+    assert re.fullmatch(java["HAS_VIEW_REPLY"], "ViewReply with viewNum: 4")
+    m = re.fullmatch(java["HAS_VIEW_REPLY_EXACT"], "ViewReply with View(viewNum=2, primary=server1, backup=null)")
+    assert m and m.groups() == ("2", "server1", "null")
+    m = re.fullmatch(java["VIEW_REPLIES_SENT"], "ViewReply for View(viewNum=2, primary=server1, backup=server2) "
+                     "sent to nodes [server1, server2, client1], primary ack sent")
+    assert m and m.groups() == ("2", "server1", "server2", "server1, server2, client1")
+    ids = {n: int(v) for n, v in re.findall(r"DSL_PRED_([A-Z_]+) = (\d+)", HEADER)}
+    assert "Leaf(500," in reg and ids["PB_HAS_VIEW_REPLY"] == 500
+    assert "Leaf(501," in reg and ids["PB_VIEW_REPLY_EXACT"] == 501
+    assert "Leaf(502," in reg and ids["PB_VIEW_REPLIES_SENT"] == 502
+
+
+def test_java_dropped_network_uses_the_engine():
+    """A dropped-network start state is packed on the engine (drop, then undrop from / to), not sent
+    to the JVM search as round 3's GpuBFS did."""
+    bfs = open(os.path.join(JAVA, "GpuBFS.java")).read()
+    assert "hasDroppedNetwork" not in bfs
+    assert "eng.setDropped(eng.dropPending(packed, undrop.from(), undrop.to()))" in bfs
+    assert 'getDeclaredField("droppedNetwork")' in bfs and 'getDeclaredField("network")' in bfs
