@@ -445,7 +445,8 @@ struct BfsEngine : EngineBase {
   }
   // Parents per chunk at most: about three passes of 256 lanes at the observed branching, within
   // the LDS budget of the staged rows.
-  static constexpr size_t kRowLds = (size_t)NW * 4 + sizeof(Fp) + 4;  // LDS per staged parent
+  // LDS per staged parent: its row, fingerprint, node hashes (kernels.hpp k_level step 2) and offset
+  static constexpr size_t kRowLds = (size_t)NW * 4 + sizeof(Fp) * (1 + P::kNodes) + 4;
   int pb_max() const {
     const int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / kRowLds);
     const int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
@@ -768,7 +769,7 @@ struct BfsEngine : EngineBase {
     a.qspread = slots;
     const uint64_t nchunks = a.segs.chunk0[a.segs.n];
     const int blocks = (int)std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)slots));
-    const size_t lds = (size_t)PB * (NW * 4 + sizeof(Fp) + 4) + 16;
+    const size_t lds = (size_t)PB * kRowLds + 16;
     hipLaunchKernelGGL((k_level<P, false>), dim3(blocks), dim3(kLevelBlock), lds, stream, a, prm, dset);
     DSL_HIP(hipGetLastError());
     DSL_HIP(hipMemcpyAsync(out, S.terms, sizeof(TerminalRec), hipMemcpyDeviceToHost, stream));
@@ -1088,7 +1089,7 @@ struct BfsEngine : EngineBase {
           }
         }
         }  // !queued (capacity)
-        const size_t lds = (size_t)PB * (NW * 4 + sizeof(Fp) + 4) + 16;
+        const size_t lds = (size_t)PB * kRowLds + 16;
         if (!queued) {
         DSL_HIP(hipEventRecord(ev0, stream));
         for (auto& S : sh) {

@@ -494,7 +494,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // a.PB (max) * NW
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
-  int* off = reinterpret_cast<int*>(fps + a.PB);           // a.PB + 1
+  Fp* nh = fps + a.PB;                                     // a.PB * kNodes: the parents' node hashes
+  int* off = reinterpret_cast<int*>(nh + a.PB * P::kNodes);  // a.PB + 1
   __shared__ SegTable s_segs;
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
@@ -591,7 +592,14 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     PH_MARK(9);  // staging (LDS-DMA + wait + barrier)
-    // 2. enabled events per parent (SearchState.events), workgroup exclusive scan (wave scans)
+    // 2. every parent's node hashes, once per parent instead of once per successor (the old-node
+    //    term of the incremental fingerprint: fp ^ H(i, old) ^ H(i, new) ^ ...), one lane per
+    //    (parent, node); then the enabled events per parent (SearchState.events) and a workgroup
+    //    exclusive scan (wave scans); the scan's barrier also publishes the hashes
+    for (int x = tid; x < pb * P::kNodes; x += kLevelBlock) {
+      const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
+      nh[x] = node_hash<P>(ii, rows + jj * NW + ii * P::kNodeWords);
+    }
     int total;
     if (pb <= 64) {  // one wave's worth of parents: wave 0 scans them alone, one barrier
       if (wid == 0) {
@@ -782,7 +790,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               dn = delta_new_count<P>(d);
               noop = dn == 0 && same_words<P::kNodeWords>(d.nw, w + dnode * P::kNodeWords);
               if (!noop) {
-                f = delta_fingerprint<P>(w, fps[j], d);
+                f = delta_fingerprint_cached<P>(fp_xor(fps[j], nh[j * P::kNodes + dnode]), d);
                 // the changed node's words go through LDS: a view pointing at the register
                 // array would take its address and push the whole delta into scratch
 #pragma unroll

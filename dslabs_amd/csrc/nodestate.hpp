@@ -395,6 +395,17 @@ DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
   return f;
 }
 
+// The same from the parent's fingerprint with the changed node's old hash already removed
+// (k_level caches the parents' node hashes in LDS).
+template <class P>
+DSL_HD Fp delta_fingerprint_cached(Fp parent_without_node, const Delta<P>& d) {
+  Fp f = fp_xor(parent_without_node, node_hash<P>(d.node, d.nw));
+#pragma unroll
+  for (int j = 0; j < P::kMaxSends; j++)
+    if ((d.keep >> j) & 1u) f = fp_xor(f, msg_hash<P>(d.out.r[j]));
+  return f;
+}
+
 // Enabled events of the successor, from the parent's count and the delta: the changed node's
 // timer events are replaced, records new to the set add their deliverable ones.
 template <class P>

@@ -145,6 +145,11 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
       const Fp f = delta_fingerprint<P>(n.s.w, n.fp, dl);
       const Fp g = full_fingerprint<P>(t.w);
       if (f.hi != g.hi || f.lo != g.lo) fp_mismatch++;
+      {  // k_level's form: the parent's node hash cached per parent (LDS), removed once
+        const Fp c = delta_fingerprint_cached<P>(
+            fp_xor(n.fp, node_hash<P>(dl.node, n.s.w + dl.node * P::kNodeWords)), dl);
+        if (c.hi != g.hi || c.lo != g.lo) fp_mismatch++;
+      }
       if (!seen.insert(key(t)).second) continue;
       if ((int)per.size() <= d) per.resize(d + 1, 0);
       per[d]++;
