@@ -94,11 +94,18 @@ struct LevelCounters {
   unsigned tl_n = 0;                                                                              \
   {                                                                                               \
     const unsigned long long tl_t = __builtin_amdgcn_s_memrealtime();                             \
-    if (threadIdx.x == 0) atomicMax(&a.ctr->phase[0], ~tl_t);                                    \
+    if (threadIdx.x == 0 && (kTlAll || blockIdx.x == 0)) atomicMax(&a.ctr->phase[0], ~tl_t);     \
     if (tl_on) a.ctr->phase[2] = tl_t;                                                            \
   }
 #define PH_MARK(i) do { if (tl_on && tl_n < 32) a.ctr->phcls[tl_n++] = ((unsigned long long)(i) << 56) | (__builtin_amdgcn_s_memrealtime() & ((1ull << 56) - 1)); } while (0)
-#define PH_FLUSH(red, ctr) do { __syncthreads(); if (threadIdx.x == 0) atomicMax(&(ctr)->phase[1], __builtin_amdgcn_s_memrealtime()); } while (0)
+#define PH_FLUSH(red, ctr) do { __syncthreads(); if (threadIdx.x == 0 && (kTlAll || blockIdx.x == 0)) atomicMax(&(ctr)->phase[1], __builtin_amdgcn_s_memrealtime()); } while (0)
+// -DDSL_TIMELINE_WG0: only workgroup 0 touches the entry / exit words (the 1,024 entry atomics of
+// the default on one word serialize and add several microseconds to a small level's prologue)
+#ifdef DSL_TIMELINE_WG0
+constexpr bool kTlAll = false;
+#else
+constexpr bool kTlAll = true;
+#endif
 #define PH_CLS_DECL
 #define PH_CLS_T0
 #define PH_CLS_ADD(cls, active) do { } while (0)
