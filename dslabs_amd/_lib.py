@@ -22,6 +22,7 @@ DSL_MAX_EVENT_FIELDS = 8
 DSL_PROTO_PINGPONG_IR = 8  # protocols generated from the IR (dslabs_amd/ir/specs)
 DSL_PROTO_AMOKV_IR = 9
 DSL_PROTO_MULTIPAXOS_IR = 10
+DSL_PROTO_PB_IR = 11
 
 # dsl_status
 DSL_OK = 0

@@ -236,6 +236,7 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
     case DSL_PROTO_PINGPONG_IR: return make_engine<PingPongIR>(d, cfg, out);
     case DSL_PROTO_AMOKV_IR: return make_engine<AmoKVIR>(d, cfg, out);
     case DSL_PROTO_MULTIPAXOS_IR: return make_engine<MultiPaxosIR>(d, cfg, out);
+    case DSL_PROTO_PB_IR: return make_engine<PBIR>(d, cfg, out);
 #endif
     default:
       set_error("unknown protocol id " + std::to_string(d.protocol));
@@ -324,6 +325,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_PINGPONG_IR: return (int)sizeof(dsl::PingPongIR::State);
     case DSL_PROTO_AMOKV_IR: return (int)sizeof(dsl::AmoKVIR::State);
     case DSL_PROTO_MULTIPAXOS_IR: return (int)sizeof(dsl::MultiPaxosIR::State);
+    case DSL_PROTO_PB_IR: return (int)sizeof(dsl::PBIR::State);
     default: return DSL_ERR_UNKNOWN_PROTOCOL;
   }
 }
@@ -340,6 +342,7 @@ int dsl_state_bytes(const dsl_protocol_desc* proto) {
     case DSL_PROTO_PINGPONG_IR: { using P = dsl::PingPongIR; return call; } \
     case DSL_PROTO_AMOKV_IR: { using P = dsl::AmoKVIR; return call; }       \
     case DSL_PROTO_MULTIPAXOS_IR: { using P = dsl::MultiPaxosIR; return call; } \
+    case DSL_PROTO_PB_IR: { using P = dsl::PBIR; return call; }           \
     default: return DSL_ERR_UNKNOWN_PROTOCOL;                           \
   }
 

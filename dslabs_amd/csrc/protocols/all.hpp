@@ -10,4 +10,5 @@
 #include "gen/pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
 #include "gen/amokv_ir.hpp"
 #include "gen/multipaxos_ir.hpp"
+#include "gen/pb_ir.hpp"
 #define DSL_HAVE_MULTIPAXOS 1

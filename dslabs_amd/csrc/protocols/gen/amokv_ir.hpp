@@ -13,6 +13,7 @@ namespace dsl {
 
 struct AmoKVIR {
   static constexpr int kNodes = 4, kNodeWords = 6, kNetCap = 24, kMaxSends = 1;
+  using Self = AmoKVIR;
   static constexpr int kMsgClasses = 2;
   using Rec = uint32_t;
   using State = StateOf<AmoKVIR>;

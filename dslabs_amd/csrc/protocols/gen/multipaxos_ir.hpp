@@ -21,6 +21,7 @@ namespace dsl {
 struct MultiPaxosIR {
   static constexpr int kNodes = 5, kNodeWords = 6, kNetCap = 64, kMaxSends = 12;
   static constexpr bool kSendsDistinct = true;  // checked by tests/hostcheck (dup_sends)
+  using Self = MultiPaxosIR;
   static constexpr int kMsgClasses = 8;
   using Rec = uint64_t;
   using State = StateOf<MultiPaxosIR>;

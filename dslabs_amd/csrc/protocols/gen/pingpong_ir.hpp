@@ -12,6 +12,7 @@ namespace dsl {
 
 struct PingPongIR {
   static constexpr int kNodes = 5, kNodeWords = 6, kNetCap = 120, kMaxSends = 2;
+  using Self = PingPongIR;
   static constexpr int kMsgClasses = 2;
   using Rec = uint32_t;
   using State = StateOf<PingPongIR>;

@@ -158,12 +158,17 @@ class PredDecl:
     """A protocol state predicate (StatePredicate): `ids` are the engine's DSL_PRED_* ids it
     answers (include/dslabs_hip.h), `names` the oracle CLI names, `full` the reference's
     description; `reads` maps each node kind it reads to the fields it reads (the kernels'
-    incremental judge keeps the parent's value when none of those words changed)."""
+    incremental judge keeps the parent's value when none of those words changed). `nargs`
+    integer arguments (dsl_predicate arg0 / arg1; the oracle CLI name NAME:a0[:a1]) are read with
+    q.arg(i). A predicate that reads the network (q.any_msg) declares network=True: it is
+    re-evaluated for every new state (its read set is everything)."""
     ids: List[int]
     names: List[str]
     full: str
     reads: Dict[str, List[str]]
     fn: Callable
+    nargs: int = 0
+    network: bool = False
 
 
 @dataclass
@@ -285,12 +290,16 @@ class Protocol:
         k.client, k.result_field, k.results_cap, k.timer_cap = True, result_field, results_cap, timer_cap
         return k
 
-    def predicate(self, full: str, ids, names, reads: Dict[str, List[str]]):
-        """reads: node kind name -> the fields the predicate reads."""
+    def predicate(self, full: str, ids, names, reads: Dict[str, List[str]], nargs: int = 0, network: bool = False):
+        """reads: node kind name -> the fields the predicate reads; nargs: integer arguments
+        (q.arg(i)); network: it reads the network (q.any_msg), so it has no node read set."""
         def deco(fn):
-            self.predicates.append(PredDecl(list(ids), list(names), full, dict(reads), fn))
+            self.predicates.append(PredDecl(list(ids), list(names), full, dict(reads), fn, nargs, network))
             return fn
         return deco
+
+    def net_preds(self) -> bool:
+        return any(pd.network for pd in self.predicates)
 
     def kind(self, name: str) -> NodeKind:
         return next(k for k in self.kinds if k.name == name)
@@ -730,6 +739,47 @@ class PredHandler(Handler):
 
     def ret(self, value=True):
         self._emit(RetPV("THREW" if value == "threw" else "TRUE" if value else "FALSE"))
+
+    def arg(self, i: int) -> Expr:
+        """The predicate's integer argument i (dsl_predicate arg0 / arg1; the oracle CLI name's
+        i-th ':' part)."""
+        assert i in (0, 1)
+        return Expr(f"(int)pr.arg{i}", f"a{i}_")
+
+    def any_msg(self, msg: RecordType, cond: Callable) -> Expr:
+        """Whether network() -- the state's messages, the successor's new ones and the dropped
+        ones (SearchState.network(), SearchState.java:153-157; StatePredicate.
+        containsMessageMatching, T/StatePredicate.java:146-149) -- holds a `msg` for which
+        cond(m) is true; m.<field>, m.sender and m.to are the message's."""
+        m = _MsgView(self.p, msg)
+        c = lit(cond(m))
+        dev = (f"view_any_record<Self>(v, [&](Rec r) {{ return rec_type(r) == {msg.index} && ({c.dev}); }})")
+        orc = f"any_net_(s, [&](const Envelope& e) {{ return e.m.type == \"{msg.name}\" && ({c.orc}); }})"
+        return Expr(dev, orc)
+
+
+class _MsgView:
+    """A network message inside q.any_msg: its fields, sender and receiver."""
+
+    def __init__(self, proto: Protocol, msg: RecordType):
+        object.__setattr__(self, "_p", proto)
+        object.__setattr__(self, "_m", msg)
+
+    @property
+    def sender(self) -> Expr:
+        return Expr("rec_from(r)", "e.from")
+
+    @property
+    def to(self) -> Expr:
+        return Expr("rec_to(r)", "e.to")
+
+    def __getattr__(self, name):
+        m = self._m
+        for i, (n, b) in enumerate(m.fields):
+            if n == name:
+                off = sum(bb for _, bb in m.fields[:i])
+                return Expr(f"(int)((r >> {off}) & {(1 << b) - 1}u)", f"std::stoi(e.m.f[{i}])")
+        raise KeyError(f"{m.name} has no field {name}")
 
 
 def record_pred(proto: Protocol, fn: Callable) -> List[Stmt]:

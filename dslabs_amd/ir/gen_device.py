@@ -108,6 +108,9 @@ def generate(p: Protocol, source: str) -> str:
       f"kMaxSends = {p.max_sends};")
     if p.sends_distinct:
         a("  static constexpr bool kSendsDistinct = true;  // checked by tests/hostcheck (dup_sends)")
+    if p.net_preds():
+        a("  static constexpr bool kNetPreds = true;  // a predicate reads the network (view_any_record)")
+    a(f"  using Self = {N};")
     a(f"  static constexpr int kMsgClasses = {len(p.messages)};")
     a(f"  using Rec = {rec_t};")
     a(f"  using State = StateOf<{N}>;")

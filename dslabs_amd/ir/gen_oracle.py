@@ -234,13 +234,32 @@ def generate(p: Protocol, source: str) -> str:
                 a(f"inline const {cls}* n_{k.name}(const State& s, int a) {{ return dynamic_cast<const {cls}*>(s.cw(a)->client.get()); }}")
             else:
                 a(f"inline const {cls}* n_{k.name}(const State& s, int a) {{ return dynamic_cast<const {cls}*>(s.nodes[a].get()); }}")
-        a("// the protocol's state predicates by their oracle CLI names (StatePredicate)")
+        a("// network() = the network and the dropped messages (SearchState.java:153-157)")
+        a("template <class F>")
+        a("inline bool any_net_(const State& s, F f) {")
+        a("  for (auto& e : s.network)")
+        a("    if (f(e)) return true;")
+        a("  for (auto& e : s.dropped)")
+        a("    if (f(e)) return true;")
+        a("  return false;")
+        a("}")
+        a("// the protocol's state predicates by their oracle CLI names (StatePredicate); a predicate with")
+        a("// integer arguments is NAME:a0[:a1]")
         a("inline std::optional<Predicate> predicate(const std::string& name, const Params& prm) {")
+        a("  std::vector<std::string> parts_;")
+        a("  for (size_t i = 0, j; i <= name.size(); i = j + 1) {")
+        a("    j = name.find(':', i);")
+        a("    if (j == std::string::npos) j = name.size();")
+        a("    parts_.push_back(name.substr(i, j - i));")
+        a("  }")
+        a("  const std::string base_ = parts_[0];")
+        a("  const int a0_ = parts_.size() > 1 ? std::stoi(parts_[1]) : 0, a1_ = parts_.size() > 2 ? std::stoi(parts_[2]) : 0;")
+        a("  (void)a0_; (void)a1_;")
         for pd in p.predicates:
-            cond = " || ".join(f"name == \"{n}\"" for n in pd.names)
-            a(f"  if ({cond}) {{")
-            a(f"    return Predicate{{\"{pd.full}\", [prm](const State& s) {{")
-            a("      (void)s;")
+            cond = " || ".join(f"base_ == \"{n}\"" for n in pd.names)
+            a(f"  if (({cond}) && parts_.size() == {1 + pd.nargs}) {{")
+            a(f"    return Predicate{{\"{pd.full}\", [prm, a0_, a1_](const State& s) {{")
+            a("      (void)s; (void)a0_; (void)a1_;")
             a("      PredResult res_;")
             L.extend(_stmts(p, p.kinds[0], record_pred(p, pd.fn), 3))
             a("      return res_;")

@@ -710,6 +710,47 @@ class AmoKVIR(IRProtocol):
                 ",".join(str(x) for x in self.params())]
 
 
+class PBIR(IRProtocol):
+    """lab2 primary-backup + ViewServer (BASELINE C4) generated from the protocol IR
+    (dslabs_amd/ir/specs/pb.py), with PB's workloads (the same command tables and result encodings)
+    and predicates (hasViewReply(n), hasViewReply(n, p, b), initView's viewRepliesSent: network
+    predicates in the IR; the ClientWorker family)."""
+
+    IR_NAMES = {500: "hasViewReply", 501: "hasViewReplyExact", 502: "viewRepliesSent"}
+
+    def __init__(self, servers: int = 2, clients: int = 1, workload: str = "putget"):
+        pb = PB(servers, clients, workload)
+        ps = pb.params()
+        super().__init__("pb", servers=servers, clients=clients, ncmds=ps[2])
+        self.pb = pb
+        self._tables = {n: [[0] * 3 for _ in range(2)] for n in ("op", "key", "sym")}
+        self._tables["expected"] = [[-1] * 3 for _ in range(2)]
+        for c in range(2):
+            for k in range(3):
+                op, key, sym, exp = ps[3 + 4 * (3 * c + k): 3 + 4 * (3 * c + k) + 4]
+                self._tables["op"][c][k], self._tables["key"][c][k], self._tables["sym"][c][k] = op, key, sym
+                self._tables["expected"][c][k] = exp
+
+    def params(self):
+        ps = super().params()
+        for n in ("op", "key", "sym", "expected"):
+            for row in self._tables[n]:
+                ps += row
+        return ps
+
+    def predicate(self, name):
+        return self.pb.predicate(name)
+
+    def oracle_args(self):
+        return ["--proto", "pb_ir", "--ir-params", ",".join(str(x) for x in self.params())]
+
+    def ir_oracle_name(self, name: str) -> str:
+        """A PB predicate name (PB.predicate's forms) as the IR oracle's NAME:arg0[:arg1]."""
+        sp = self.pb.predicate(name)
+        ir = self.IR_NAMES[sp.pred_id]
+        return f"{ir}:{sp.arg0}" + (f":{sp.arg1}" if sp.pred_id == 502 else "")
+
+
 class MultiPaxosIR(IRProtocol):
     """lab3 Multi-Paxos (BASELINE C5) generated from the protocol IR (dslabs_amd/ir/specs/multipaxos.py),
     with MultiPaxos's workloads (the same command tables and result encodings) and predicates

@@ -76,7 +76,8 @@ typedef enum {
   DSL_PROTO_MINITEST = 7,   /* the two-node fixture of SearchAndTraceMinimizerTest (tst-self) */
   DSL_PROTO_PINGPONG_IR = 8, /* lab0 PingPong generated from the protocol IR (dslabs_amd/ir/specs/pingpong.py) */
   DSL_PROTO_AMOKV_IR = 9,    /* lab1 AMO KV generated from the protocol IR (dslabs_amd/ir/specs/amokv.py) */
-  DSL_PROTO_MULTIPAXOS_IR = 10 /* lab3 Multi-Paxos (C5) generated from the protocol IR (dslabs_amd/ir/specs/multipaxos.py) */
+  DSL_PROTO_MULTIPAXOS_IR = 10, /* lab3 Multi-Paxos (C5) generated from the protocol IR (dslabs_amd/ir/specs/multipaxos.py) */
+  DSL_PROTO_PB_IR = 11          /* lab2 primary-backup + ViewServer (C4) generated from the protocol IR (dslabs_amd/ir/specs/pb.py) */
 } dsl_protocol_id;
 
 typedef struct {

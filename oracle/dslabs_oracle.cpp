@@ -28,6 +28,7 @@
 #include "gen/proto_pingpong_ir.hpp"  // generated from the protocol IR (tools/gen_ir.py)
 #include "gen/proto_amokv_ir.hpp"
 #include "gen/proto_multipaxos_ir.hpp"
+#include "gen/proto_pb_ir.hpp"
 
 using namespace oracle;
 
@@ -134,6 +135,17 @@ static Scenario build(const Args& a) {
     sc.pred = [common, prm](const std::string& n) {
       auto p = common(n);
       if (!p) p = multipaxos_ir::predicate(n, prm);
+      if (!p) throw std::runtime_error("unknown predicate " + n);
+      return *p;
+    };
+  } else if (a.proto == "pb_ir") {  // --ir-params: the engine's parameter vector, comma-separated
+    std::vector<long long> v;
+    for (auto& x : split(a.get("ir-params"), ',')) v.push_back(std::stoll(x));
+    const auto prm = pb_ir::from_vector(v);
+    sc.init = pb_ir::initial(prm, sc.names);
+    sc.pred = [common, prm](const std::string& n) {
+      auto p = common(n);
+      if (!p) p = pb_ir::predicate(n, prm);
       if (!p) throw std::runtime_error("unknown predicate " + n);
       return *p;
     };

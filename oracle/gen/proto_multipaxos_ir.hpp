@@ -1270,11 +1270,30 @@ inline std::shared_ptr<State> initial(const Params& prm, Names& names) {
 
 inline const N_server* n_server(const State& s, int a) { return dynamic_cast<const N_server*>(s.nodes[a].get()); }
 inline const N_client* n_client(const State& s, int a) { return dynamic_cast<const N_client*>(s.cw(a)->client.get()); }
-// the protocol's state predicates by their oracle CLI names (StatePredicate)
+// network() = the network and the dropped messages (SearchState.java:153-157)
+template <class F>
+inline bool any_net_(const State& s, F f) {
+  for (auto& e : s.network)
+    if (f(e)) return true;
+  for (auto& e : s.dropped)
+    if (f(e)) return true;
+  return false;
+}
+// the protocol's state predicates by their oracle CLI names (StatePredicate); a predicate with
+// integer arguments is NAME:a0[:a1]
 inline std::optional<Predicate> predicate(const std::string& name, const Params& prm) {
-  if (name == "LOGS_CONSISTENT_ALL_SLOTS" || name == "LOGS_CONSISTENT") {
-    return Predicate{"Non-empty log slots consistent", [prm](const State& s) {
-      (void)s;
+  std::vector<std::string> parts_;
+  for (size_t i = 0, j; i <= name.size(); i = j + 1) {
+    j = name.find(':', i);
+    if (j == std::string::npos) j = name.size();
+    parts_.push_back(name.substr(i, j - i));
+  }
+  const std::string base_ = parts_[0];
+  const int a0_ = parts_.size() > 1 ? std::stoi(parts_[1]) : 0, a1_ = parts_.size() > 2 ? std::stoi(parts_[2]) : 0;
+  (void)a0_; (void)a1_;
+  if ((base_ == "LOGS_CONSISTENT_ALL_SLOTS" || base_ == "LOGS_CONSISTENT") && parts_.size() == 1) {
+    return Predicate{"Non-empty log slots consistent", [prm, a0_, a1_](const State& s) {
+      (void)s; (void)a0_; (void)a1_;
       PredResult res_;
       int l_isch181 = 0;
       int l_confl182 = 0;
@@ -1512,9 +1531,9 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
       return res_;
     }};
   }
-  if (name == "APPENDS_LINEARIZABLE") {
-    return Predicate{"Sequence of appends to the same key is linearizable", [prm](const State& s) {
-      (void)s;
+  if ((base_ == "APPENDS_LINEARIZABLE") && parts_.size() == 1) {
+    return Predicate{"Sequence of appends to the same key is linearizable", [prm, a0_, a1_](const State& s) {
+      (void)s; (void)a0_; (void)a1_;
       PredResult res_;
       const int l_pres233 = ((0 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 0)->results.size()));
       if ((l_pres233 && (prm.op[0][0] != 2))) {

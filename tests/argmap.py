@@ -1,7 +1,7 @@
 """Maps oracle CLI arguments (tests/golden/*.json "args") onto the engine's Python API, so each
 committed oracle fixture is replayed on the GPU with the same meaning."""
 from dslabs_amd import CLIENTS_DONE, NONE_DECIDED, RESULTS_OK, SearchSettings, clientDone
-from dslabs_amd.protocols import PB, AmoKV, AmoKVIR, MiniTest, MultiPaxos, MultiPaxosIR, PingPong, PingPongIR, SIPaxos, Synthetic
+from dslabs_amd.protocols import PB, PBIR, AmoKV, AmoKVIR, MiniTest, MultiPaxos, MultiPaxosIR, PingPong, PingPongIR, SIPaxos, Synthetic
 
 
 def _opt(args, name, default=None):
@@ -28,6 +28,8 @@ def protocol(args):
     if p == "multipaxos":
         return MultiPaxos(int(_opt(args, "--servers", 3)), int(_opt(args, "--clients", 2)),
                           _opt(args, "--workload", "append-xy"))
+    if p == "pb_ir":  # tests give --servers / --clients / --workload (the oracle takes PBIR.oracle_args())
+        return PBIR(int(_opt(args, "--servers", 2)), int(_opt(args, "--clients", 1)), _opt(args, "--workload", "putget"))
     if p == "pb":
         return PB(int(_opt(args, "--servers", 2)), int(_opt(args, "--clients", 1)), _opt(args, "--workload", "putget"))
     if p == "amokv":

@@ -339,6 +339,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, set);
     case DSL_PROTO_AMOKV_IR: return run<AmoKVIR>(d, set);
     case DSL_PROTO_MULTIPAXOS_IR: return run<MultiPaxosIR>(d, set);
+    case DSL_PROTO_PB_IR: return run<PBIR>(d, set);
   }
   return 2;
 }

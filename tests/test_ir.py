@@ -168,3 +168,75 @@ def test_ir_multipaxos_device_form_host_bfs(protocheck, servers, clients, worklo
     assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
     assert got["skip_mismatch"] == 0 and got["skipped"] > 0  # the generated no-op filter is sound and used
     assert got["dup_sends"] == 0  # the spec's sends_distinct (the Sender skips its duplicate check)
+
+
+# ---- lab2 primary-backup + ViewServer (BASELINE C4's protocol) from the IR: dslabs_amd/ir/specs/pb.py ---------
+PBG = json.load(open(os.path.join(HERE, "golden", "pb.json")))
+_PB_LEAF = r"(hasViewReply|viewRepliesSent)(:[^,()]+)"
+
+
+def _pb_ir(args):
+    """The IR protocol for a pb.json fixture's --servers / --clients / --workload, and the rest of its
+    arguments (predicates, settings, network shape)."""
+    from dslabs_amd.protocols import PBIR
+    opt = lambda n, d: args[args.index(n) + 1] if n in args else d  # noqa: E731
+    proto = PBIR(int(opt("--servers", 2)), int(opt("--clients", 1)), opt("--workload", "putget"))
+    rest, i = [], 0
+    while i < len(args):
+        if args[i] in ("--proto", "--servers", "--clients", "--workload"):
+            i += 2
+            continue
+        rest.append(args[i])
+        i += 1
+    return proto, rest
+
+
+def _pb_oracle_args(proto, rest):
+    """The fixture's arguments for the IR oracle: PB's predicate leaves (hasViewReply:n[:p:b],
+    viewRepliesSent:...) spelled as the spec's network predicates (PBIR.ir_oracle_name)."""
+    import re
+    out = []
+    for k, a in enumerate(rest):
+        if k and rest[k - 1] in ("--inv", "--goal", "--prune"):
+            a = re.sub(_PB_LEAF, lambda m: proto.ir_oracle_name(m.group(0)), a)
+        out.append(a)
+    return proto.oracle_args() + out
+
+
+@pytest.mark.parametrize("name", sorted(PBG))
+def test_ir_pb_oracle_matches_golden(name):
+    """The IR's oracle form (argument and network predicates included) against the hand-written
+    protocol's golden vectors -- initView's network-off search with its viewRepliesSent goal among them."""
+    case = PBG[name]
+    proto, rest = _pb_ir(case["args"])
+    r = oracle_util.run("bfs", _pb_oracle_args(proto, rest), timeout=600)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
+    assert r["states"] == case["states"]
+
+
+@pytest.mark.parametrize("name", sorted(PBG))
+def test_ir_pb_device_form_on_cpu(name):
+    """The generated PB device handlers and predicates in the multithreaded CPU BFS."""
+    case = PBG[name]
+    proto, rest = _pb_ir(case["args"])
+    r = cpu_baseline.run(proto, argmap.settings(rest, proto, table_log2=22), threads=4)
+    assert r["end"] == case["end"]
+    assert r["per_depth"] == case["per_depth"]
+
+
+@pytest.mark.parametrize("servers,clients,workload,tail", [
+    (2, 1, "putget", ["--", 1, "/", "/", 2, "500:4", 13]),
+    (3, 1, "putget", ["--", 1, "/", "/", 2, "500:3", 10]),
+    (2, 2, "appendappendget", ["--", 1, "/", "/", 2, "500:3", 9]),
+])
+def test_ir_pb_device_form_host_bfs(protocheck, servers, clients, workload, tail):  # noqa: F811
+    """Exact-equality host BFS over the generated PB against the hand-written PB (tests/hostcheck,
+    protocol 6) on the same predicates: per-depth counts, and the incremental fingerprint, row
+    emission and incremental judge of the generated form on every successor."""
+    from dslabs_amd.protocols import PB, PBIR
+    got = run(protocheck, [11] + PBIR(servers, clients, workload).params() + tail)
+    want = run(protocheck, [6] + PB(servers, clients, workload).params() + tail)
+    assert got["per_depth"] == want["per_depth"]
+    assert got["end"] == want["end"]
+    assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0

@@ -252,6 +252,7 @@ int main(int argc, char** argv) {
     case DSL_PROTO_PINGPONG_IR: return run<PingPongIR>(d, s, threads, log2, repeat, min_s, start, depth0);
     case DSL_PROTO_AMOKV_IR: return run<AmoKVIR>(d, s, threads, log2, repeat, min_s, start, depth0);
     case DSL_PROTO_MULTIPAXOS_IR: return run<MultiPaxosIR>(d, s, threads, log2, repeat, min_s, start, depth0);
+    case DSL_PROTO_PB_IR: return run<PBIR>(d, s, threads, log2, repeat, min_s, start, depth0);
   }
   return fprintf(stderr, "unknown protocol\n"), 2;
 }

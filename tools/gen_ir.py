@@ -9,7 +9,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from dslabs_amd.ir import gen_device, gen_oracle  # noqa: E402
 
-SPECS = ["pingpong", "amokv", "multipaxos"]
+SPECS = ["pingpong", "amokv", "multipaxos", "pb"]
 
 
 def outputs():
