@@ -207,24 +207,47 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
 }
 
 // ViewServerTest (labs/lab2-primarybackup/tst/dslabs/primarybackup/ViewServerTest.java:156-303)
-// against the DEVICE ViewServer handler (PB node 0), the same scenarios the oracle replays.
+// against a DEVICE ViewServer handler (PB node 0), the same scenarios the oracle replays: the
+// hand-written one (csrc/protocols/pb.hpp) or the IR-generated one (csrc/protocols/gen/pb_ir.hpp).
+// Both reply with the view as num | p << 4 | b << 6 in the record's low byte.
+struct VsHand {
+  using P = PB;
+  static PB::Rec ping(int n, int from) { return PB::msg(PB::M_PING, from, 0, (uint64_t)n); }
+  static PB::Rec getview() { return PB::msg(PB::M_GETVIEW, 4, 0, 0); }
+  static void init(uint32_t*, const PB::Params&) {}
+};
+struct VsIR {  // records: type << 60 | from << 57 | to << 54 | fields; Ping = 0 (num: bits 0-3), GetView = 1
+  using P = PBIR;
+  static PBIR::Rec ping(int n, int from) { return ((PBIR::Rec)from << 57) | (PBIR::Rec)(n & 15); }
+  static PBIR::Rec getview() { return ((PBIR::Rec)1 << 60) | ((PBIR::Rec)4 << 57); }
+  static void init(uint32_t* w, const PBIR::Params& p) {  // the ViewServer's init: its PingCheckTimer
+    Sender<PBIR> out;
+    PBIR::init_viewserver(0, w, out, p);
+  }
+};
+
+template <class V>
 static int vstest() {
+  using P = typename V::P;
   struct H {
-    PB::Params p{};
-    uint32_t w[PB::kNodeWords] = {0, 0, 0};
+    typename P::Params p{};
+    uint32_t w[P::kNodeWords] = {};
     bool ok = true;
-    H() { p.servers = 3; p.clients = 1; p.ncmds = 1; }
+    H() {
+      p.servers = 3; p.clients = 1; p.ncmds = 1;
+      V::init(w, p);
+    }
     void ping(int n, int from) {
-      Sender<PB> out;
-      PB::on_message(0, w, PB::msg(PB::M_PING, from, 0, (uint64_t)n), out, p);
+      Sender<P> out;
+      if (P::on_message(0, w, V::ping(n, from), out, p) != STEP_OK) ok = false;
     }
     void timeout() {
-      Sender<PB> out;
-      PB::on_timer(0, w, 0, out, p);
+      Sender<P> out;
+      if (P::on_timer(0, w, 0, out, p) != STEP_OK) ok = false;
     }
     int get() {  // GetView: the ViewReply's view (num | p << 4 | b << 6)
-      Sender<PB> out;
-      PB::on_message(0, w, PB::msg(PB::M_GETVIEW, 4, 0, 0), out, p);
+      Sender<P> out;
+      if (P::on_message(0, w, V::getview(), out, p) != STEP_OK || out.n != 1) ok = false;
       return (int)(out.r[0] & 0xff);
     }
     void check(int pr, int b, int n) {
@@ -286,7 +309,8 @@ static int vstest() {
 }
 
 int main(int argc, char** argv) {
-  if (argc > 1 && strcmp(argv[1], "vstest") == 0) return vstest();
+  if (argc > 1 && strcmp(argv[1], "vstest") == 0) return vstest<VsHand>();
+  if (argc > 1 && strcmp(argv[1], "vstest_ir") == 0) return vstest<VsIR>();
   dsl_protocol_desc d{};
   int i = 1;
   d.protocol = atoi(argv[i++]);

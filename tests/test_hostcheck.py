@@ -139,8 +139,10 @@ def test_encoding_matches_oracle(protocheck, name):
     assert got["skip_mismatch"] == 0  # every event k_level skips (NoopFilter) is a true no-op
 
 
-def test_device_viewserver_passes_reference_unit_tests(protocheck):
-    """The packed ViewServer handler (PB node 0) against ViewServerTest test01-test12."""
-    out = subprocess.run([protocheck, "vstest"], check=True, capture_output=True, text=True, timeout=60)
+@pytest.mark.parametrize("form", ["vstest", "vstest_ir"])
+def test_device_viewserver_passes_reference_unit_tests(protocheck, form):
+    """The device ViewServer handler (PB node 0) against ViewServerTest test01-test12: the
+    hand-written one (csrc/protocols/pb.hpp) and the one generated from dslabs_amd/ir/specs/pb.py."""
+    out = subprocess.run([protocheck, form], check=True, capture_output=True, text=True, timeout=60)
     res = json.loads(out.stdout)["results"]
     assert len(res) == 12 and all(r["ok"] for r in res), res
