@@ -117,8 +117,16 @@ struct Sender {
       overflow = true;
       return;
     }
+#ifdef DSL_SENDER_SHIFT
+    // shift register: the newest record at r[0] (the lanes at this send site move, the others keep
+    // their registers under the exec mask; no compare with n per slot)
+#pragma unroll
+    for (int i = K - 1; i > 0; i--) r[i] = r[i - 1];
+    r[0] = x;
+#else
 #pragma unroll
     for (int i = 0; i < K; i++) r[i] = keep_value(i == n ? x : r[i]);
+#endif
     n++;
   }
 };
