@@ -1661,179 +1661,284 @@ struct MultiPaxosIR {
         return PV_TRUE;
         return PV_TRUE;
       }
+      case 402:  // slotValid
+      {
+        const int l_i = (int)pr.arg0;
+        if ((l_i < 1)) {
+          return PV_FALSE;
+        }
+        if ((l_i > 4)) {
+          return PV_TRUE;
+        }
+        int l_isch = 0;
+        int l_confl = 0;
+        int l_chosen = 0;
+        int l_count = 0;
+        if ((0 < p.servers)) {
+          const int l_e233 = arr_server_log(v.node(first_server(p) + 0), (l_i - 1));
+          if (((l_e233 & 3) == 2)) {
+            const int l_x234 = ((((l_e233 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x234 != l_chosen))) {
+              l_confl = 1;
+            }
+            l_chosen = l_x234;
+            l_isch = 1;
+          }
+        }
+        if ((1 < p.servers)) {
+          const int l_e235 = arr_server_log(v.node(first_server(p) + 1), (l_i - 1));
+          if (((l_e235 & 3) == 2)) {
+            const int l_x236 = ((((l_e235 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x236 != l_chosen))) {
+              l_confl = 1;
+            }
+            l_chosen = l_x236;
+            l_isch = 1;
+          }
+        }
+        if ((2 < p.servers)) {
+          const int l_e237 = arr_server_log(v.node(first_server(p) + 2), (l_i - 1));
+          if (((l_e237 & 3) == 2)) {
+            const int l_x238 = ((((l_e237 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x238 != l_chosen))) {
+              l_confl = 1;
+            }
+            l_chosen = l_x238;
+            l_isch = 1;
+          }
+        }
+        if ((0 < p.servers)) {
+          const int l_e239 = arr_server_log(v.node(first_server(p) + 0), (l_i - 1));
+          if ((((l_e239 & 3) != 0) && (((l_e239 & 3) != 1) || (((((l_e239 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+            l_count = (l_count + 1);
+          }
+        }
+        if ((1 < p.servers)) {
+          const int l_e240 = arr_server_log(v.node(first_server(p) + 1), (l_i - 1));
+          if ((((l_e240 & 3) != 0) && (((l_e240 & 3) != 1) || (((((l_e240 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+            l_count = (l_count + 1);
+          }
+        }
+        if ((2 < p.servers)) {
+          const int l_e241 = arr_server_log(v.node(first_server(p) + 2), (l_i - 1));
+          if ((((l_e241 & 3) != 0) && (((l_e241 & 3) != 1) || (((((l_e241 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+            l_count = (l_count + 1);
+          }
+        }
+        if (((l_isch != 0) && ((l_confl != 0) || ((l_count * 2) <= p.servers)))) {
+          return PV_FALSE;
+        }
+        return PV_TRUE;
+        return PV_TRUE;
+      }
+      case 403:  // hasStatus
+      {
+        const int l_k242 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
+        if (((l_k242 < 0) || (l_k242 >= p.servers))) {
+          return PV_THREW;
+        }
+        const int l_slot243 = ((int)pr.arg1 >> 4);
+        int l_se244 = 0;
+        if (((l_slot243 >= 1) && (l_slot243 <= 4))) {
+          l_se244 = arr_server_log(v.node(first_server(p) + l_k242), (l_slot243 - 1));
+        }
+        if (((l_se244 & 3) == ((int)pr.arg1 & 15))) {
+          return PV_TRUE;
+        }
+        return PV_FALSE;
+        return PV_TRUE;
+      }
+      case 404:  // hasCommand
+      {
+        const int l_k245 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
+        if (((l_k245 < 0) || (l_k245 >= p.servers))) {
+          return PV_THREW;
+        }
+        const int l_slot246 = ((int)pr.arg1 >> 8);
+        int l_se247 = 0;
+        if (((l_slot246 >= 1) && (l_slot246 <= 4))) {
+          l_se247 = arr_server_log(v.node(first_server(p) + l_k245), (l_slot246 - 1));
+        }
+        const int l_cc = (((l_se247 & 3) == 0) ? 0 : ((((l_se247 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0));
+        if ((l_cc == ((int)pr.arg1 & 255))) {
+          return PV_TRUE;
+        }
+        return PV_FALSE;
+        return PV_TRUE;
+      }
       case 300:  // APPENDS_LINEARIZABLE
       {
-        const int l_pres233 = ((0 < p.clients) && (0 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres233 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u) != 2))) {
+        const int l_pres248 = ((0 < p.clients) && (0 < get(v.node(first_client(p) + 0), 26, 2)));
+        if ((l_pres248 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res234 = (l_pres233 ? arr_client__results(v.node(first_client(p) + 0), 0) : 0);
-        const int l_rlen235 = (l_res234 & 7);
-        if ((l_pres233 && (((l_rlen235 == 0) || (l_rlen235 > 4)) || (((l_res234 >> (1 + (l_rlen235 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u))))) {
-          return PV_FALSE;
-        }
-        const int l_pres236 = ((0 < p.clients) && (1 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres236 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u) != 2))) {
-          return PV_THREW;
-        }
-        const int l_res237 = (l_pres236 ? arr_client__results(v.node(first_client(p) + 0), 1) : 0);
-        const int l_rlen238 = (l_res237 & 7);
-        if ((l_pres236 && (((l_rlen238 == 0) || (l_rlen238 > 4)) || (((l_res237 >> (1 + (l_rlen238 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u))))) {
-          return PV_FALSE;
-        }
-        const int l_pres239 = ((0 < p.clients) && (2 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres239 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u) != 2))) {
-          return PV_THREW;
-        }
-        const int l_res240 = (l_pres239 ? arr_client__results(v.node(first_client(p) + 0), 2) : 0);
-        const int l_rlen241 = (l_res240 & 7);
-        if ((l_pres239 && (((l_rlen241 == 0) || (l_rlen241 > 4)) || (((l_res240 >> (1 + (l_rlen241 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u))))) {
-          return PV_FALSE;
-        }
-        const int l_pres242 = ((1 < p.clients) && (0 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres242 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u) != 2))) {
-          return PV_THREW;
-        }
-        const int l_res243 = (l_pres242 ? arr_client__results(v.node(first_client(p) + 1), 0) : 0);
-        const int l_rlen244 = (l_res243 & 7);
-        if ((l_pres242 && (((l_rlen244 == 0) || (l_rlen244 > 4)) || (((l_res243 >> (1 + (l_rlen244 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u))))) {
-          return PV_FALSE;
-        }
-        const int l_pres245 = ((1 < p.clients) && (1 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres245 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u) != 2))) {
-          return PV_THREW;
-        }
-        const int l_res246 = (l_pres245 ? arr_client__results(v.node(first_client(p) + 1), 1) : 0);
-        const int l_rlen247 = (l_res246 & 7);
-        if ((l_pres245 && (((l_rlen247 == 0) || (l_rlen247 > 4)) || (((l_res246 >> (1 + (l_rlen247 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u))))) {
-          return PV_FALSE;
-        }
-        const int l_pres248 = ((1 < p.clients) && (2 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres248 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u) != 2))) {
-          return PV_THREW;
-        }
-        const int l_res249 = (l_pres248 ? arr_client__results(v.node(first_client(p) + 1), 2) : 0);
+        const int l_res249 = (l_pres248 ? arr_client__results(v.node(first_client(p) + 0), 0) : 0);
         const int l_rlen250 = (l_res249 & 7);
-        if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u))))) {
+        if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        if ((l_pres233 && l_pres236)) {
-          if ((l_rlen235 == l_rlen238)) {
+        const int l_pres251 = ((0 < p.clients) && (1 < get(v.node(first_client(p) + 0), 26, 2)));
+        if ((l_pres251 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u) != 2))) {
+          return PV_THREW;
+        }
+        const int l_res252 = (l_pres251 ? arr_client__results(v.node(first_client(p) + 0), 1) : 0);
+        const int l_rlen253 = (l_res252 & 7);
+        if ((l_pres251 && (((l_rlen253 == 0) || (l_rlen253 > 4)) || (((l_res252 >> (1 + (l_rlen253 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u))))) {
+          return PV_FALSE;
+        }
+        const int l_pres254 = ((0 < p.clients) && (2 < get(v.node(first_client(p) + 0), 26, 2)));
+        if ((l_pres254 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u) != 2))) {
+          return PV_THREW;
+        }
+        const int l_res255 = (l_pres254 ? arr_client__results(v.node(first_client(p) + 0), 2) : 0);
+        const int l_rlen256 = (l_res255 & 7);
+        if ((l_pres254 && (((l_rlen256 == 0) || (l_rlen256 > 4)) || (((l_res255 >> (1 + (l_rlen256 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u))))) {
+          return PV_FALSE;
+        }
+        const int l_pres257 = ((1 < p.clients) && (0 < get(v.node(first_client(p) + 1), 26, 2)));
+        if ((l_pres257 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u) != 2))) {
+          return PV_THREW;
+        }
+        const int l_res258 = (l_pres257 ? arr_client__results(v.node(first_client(p) + 1), 0) : 0);
+        const int l_rlen259 = (l_res258 & 7);
+        if ((l_pres257 && (((l_rlen259 == 0) || (l_rlen259 > 4)) || (((l_res258 >> (1 + (l_rlen259 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u))))) {
+          return PV_FALSE;
+        }
+        const int l_pres260 = ((1 < p.clients) && (1 < get(v.node(first_client(p) + 1), 26, 2)));
+        if ((l_pres260 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u) != 2))) {
+          return PV_THREW;
+        }
+        const int l_res261 = (l_pres260 ? arr_client__results(v.node(first_client(p) + 1), 1) : 0);
+        const int l_rlen262 = (l_res261 & 7);
+        if ((l_pres260 && (((l_rlen262 == 0) || (l_rlen262 > 4)) || (((l_res261 >> (1 + (l_rlen262 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u))))) {
+          return PV_FALSE;
+        }
+        const int l_pres263 = ((1 < p.clients) && (2 < get(v.node(first_client(p) + 1), 26, 2)));
+        if ((l_pres263 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u) != 2))) {
+          return PV_THREW;
+        }
+        const int l_res264 = (l_pres263 ? arr_client__results(v.node(first_client(p) + 1), 2) : 0);
+        const int l_rlen265 = (l_res264 & 7);
+        if ((l_pres263 && (((l_rlen265 == 0) || (l_rlen265 > 4)) || (((l_res264 >> (1 + (l_rlen265 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u))))) {
+          return PV_FALSE;
+        }
+        if ((l_pres248 && l_pres251)) {
+          if ((l_rlen250 == l_rlen253)) {
             return PV_FALSE;
           }
-          if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen238) ? l_rlen235 : l_rlen238) * 2)) - 1)) != ((l_res237 >> 3) & ((1 << (((l_rlen235 < l_rlen238) ? l_rlen235 : l_rlen238) * 2)) - 1)))) {
+          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)) != ((l_res252 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres233 && l_pres239)) {
-          if ((l_rlen235 == l_rlen241)) {
+        if ((l_pres248 && l_pres254)) {
+          if ((l_rlen250 == l_rlen256)) {
             return PV_FALSE;
           }
-          if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen241) ? l_rlen235 : l_rlen241) * 2)) - 1)) != ((l_res240 >> 3) & ((1 << (((l_rlen235 < l_rlen241) ? l_rlen235 : l_rlen241) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres233 && l_pres242)) {
-          if ((l_rlen235 == l_rlen244)) {
-            return PV_FALSE;
-          }
-          if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen244) ? l_rlen235 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen235 < l_rlen244) ? l_rlen235 : l_rlen244) * 2)) - 1)))) {
+          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres233 && l_pres245)) {
-          if ((l_rlen235 == l_rlen247)) {
+        if ((l_pres248 && l_pres257)) {
+          if ((l_rlen250 == l_rlen259)) {
             return PV_FALSE;
           }
-          if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen247) ? l_rlen235 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen235 < l_rlen247) ? l_rlen235 : l_rlen247) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres233 && l_pres248)) {
-          if ((l_rlen235 == l_rlen250)) {
-            return PV_FALSE;
-          }
-          if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen250) ? l_rlen235 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen235 < l_rlen250) ? l_rlen235 : l_rlen250) * 2)) - 1)))) {
+          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres236 && l_pres239)) {
-          if ((l_rlen238 == l_rlen241)) {
+        if ((l_pres248 && l_pres260)) {
+          if ((l_rlen250 == l_rlen262)) {
             return PV_FALSE;
           }
-          if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen241) ? l_rlen238 : l_rlen241) * 2)) - 1)) != ((l_res240 >> 3) & ((1 << (((l_rlen238 < l_rlen241) ? l_rlen238 : l_rlen241) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres236 && l_pres242)) {
-          if ((l_rlen238 == l_rlen244)) {
-            return PV_FALSE;
-          }
-          if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen244) ? l_rlen238 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen238 < l_rlen244) ? l_rlen238 : l_rlen244) * 2)) - 1)))) {
+          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres236 && l_pres245)) {
-          if ((l_rlen238 == l_rlen247)) {
+        if ((l_pres248 && l_pres263)) {
+          if ((l_rlen250 == l_rlen265)) {
             return PV_FALSE;
           }
-          if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen247) ? l_rlen238 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen238 < l_rlen247) ? l_rlen238 : l_rlen247) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres236 && l_pres248)) {
-          if ((l_rlen238 == l_rlen250)) {
-            return PV_FALSE;
-          }
-          if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen250) ? l_rlen238 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen238 < l_rlen250) ? l_rlen238 : l_rlen250) * 2)) - 1)))) {
+          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres239 && l_pres242)) {
-          if ((l_rlen241 == l_rlen244)) {
+        if ((l_pres251 && l_pres254)) {
+          if ((l_rlen253 == l_rlen256)) {
             return PV_FALSE;
           }
-          if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen244) ? l_rlen241 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen241 < l_rlen244) ? l_rlen241 : l_rlen244) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres239 && l_pres245)) {
-          if ((l_rlen241 == l_rlen247)) {
-            return PV_FALSE;
-          }
-          if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen247) ? l_rlen241 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen241 < l_rlen247) ? l_rlen241 : l_rlen247) * 2)) - 1)))) {
+          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres239 && l_pres248)) {
-          if ((l_rlen241 == l_rlen250)) {
+        if ((l_pres251 && l_pres257)) {
+          if ((l_rlen253 == l_rlen259)) {
             return PV_FALSE;
           }
-          if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen250) ? l_rlen241 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen241 < l_rlen250) ? l_rlen241 : l_rlen250) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres242 && l_pres245)) {
-          if ((l_rlen244 == l_rlen247)) {
-            return PV_FALSE;
-          }
-          if ((((l_res243 >> 3) & ((1 << (((l_rlen244 < l_rlen247) ? l_rlen244 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen244 < l_rlen247) ? l_rlen244 : l_rlen247) * 2)) - 1)))) {
+          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres242 && l_pres248)) {
-          if ((l_rlen244 == l_rlen250)) {
+        if ((l_pres251 && l_pres260)) {
+          if ((l_rlen253 == l_rlen262)) {
             return PV_FALSE;
           }
-          if ((((l_res243 >> 3) & ((1 << (((l_rlen244 < l_rlen250) ? l_rlen244 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen244 < l_rlen250) ? l_rlen244 : l_rlen250) * 2)) - 1)))) {
+          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres245 && l_pres248)) {
-          if ((l_rlen247 == l_rlen250)) {
+        if ((l_pres251 && l_pres263)) {
+          if ((l_rlen253 == l_rlen265)) {
             return PV_FALSE;
           }
-          if ((((l_res246 >> 3) & ((1 << (((l_rlen247 < l_rlen250) ? l_rlen247 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen247 < l_rlen250) ? l_rlen247 : l_rlen250) * 2)) - 1)))) {
+          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres254 && l_pres257)) {
+          if ((l_rlen256 == l_rlen259)) {
+            return PV_FALSE;
+          }
+          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres254 && l_pres260)) {
+          if ((l_rlen256 == l_rlen262)) {
+            return PV_FALSE;
+          }
+          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres254 && l_pres263)) {
+          if ((l_rlen256 == l_rlen265)) {
+            return PV_FALSE;
+          }
+          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres257 && l_pres260)) {
+          if ((l_rlen259 == l_rlen262)) {
+            return PV_FALSE;
+          }
+          if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres257 && l_pres263)) {
+          if ((l_rlen259 == l_rlen265)) {
+            return PV_FALSE;
+          }
+          if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres260 && l_pres263)) {
+          if ((l_rlen262 == l_rlen265)) {
+            return PV_FALSE;
+          }
+          if ((((l_res261 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
@@ -1847,17 +1952,23 @@ struct MultiPaxosIR {
   static uint32_t pred_reads(const DevPred& pr, const Params& p) {
     (void)pr; (void)p;
     if (pr.id == 400 || pr.id == 401) return (((1u << (p.servers)) - 1u) << first_server(p));
+    if (pr.id == 402) return (((1u << (p.servers)) - 1u) << first_server(p));
+    if (pr.id == 403) return (((1u << (p.servers)) - 1u) << first_server(p));
+    if (pr.id == 404) return (((1u << (p.servers)) - 1u) << first_server(p));
     if (pr.id == 300) return (((1u << (p.clients)) - 1u) << first_client(p));
     const uint32_t clients = (((1u << (p.clients)) - 1u) << first_client(p));
     return (pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) ? clients : kReadsAll;
   }
   static DSL_HD bool pred_same(const DevPred& pr, const uint32_t* a, const uint32_t* b) {
     if (pr.id == 400 || pr.id == 401) return (((a[1] ^ b[1]) & 0x3fffffu) | ((a[2] ^ b[2]) & 0x3fffffu)) == 0;
+    if (pr.id == 402) return (((a[1] ^ b[1]) & 0x3fffffu) | ((a[2] ^ b[2]) & 0x3fffffu)) == 0;
+    if (pr.id == 403) return (((a[1] ^ b[1]) & 0x3fffffu) | ((a[2] ^ b[2]) & 0x3fffffu)) == 0;
+    if (pr.id == 404) return (((a[1] ^ b[1]) & 0x3fffffu) | ((a[2] ^ b[2]) & 0x3fffffu)) == 0;
     if (pr.id == 300) return (((a[0] ^ b[0]) & 0xc000000u) | ((a[1] ^ b[1]) & 0xffffffu) | ((a[2] ^ b[2]) & 0xfffu)) == 0;
     if (pr.id >= DSL_PRED_RESULTS_OK && pr.id <= DSL_PRED_CLIENT_HAS_RESULTS) return (((a[0] ^ b[0]) & 0xc000000u) | ((a[1] ^ b[1]) & 0xffffffu) | ((a[2] ^ b[2]) & 0xfffu)) == 0;
     return same_words<kNodeWords>(a, b);
   }
-  static bool known_predicate(int id) { return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == 400 || id == 401 || id == 300; }
+  static bool known_predicate(int id) { return (id >= DSL_PRED_RESULTS_OK && id <= DSL_PRED_CLIENT_HAS_RESULTS) || id == 400 || id == 401 || id == 402 || id == 403 || id == 404 || id == 300; }
   static DSL_HD bool surely_noop(int i, const uint32_t* row, Rec r, const Params& p) {
     const uint32_t* w = row + i * kNodeWords;
     bool x = false;

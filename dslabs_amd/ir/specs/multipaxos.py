@@ -495,6 +495,69 @@ def _logs_consistent(q):
     q.ret(True)
 
 
+@P.predicate("Logs consistent for slot", ids=[402], names=["slotValid"], reads={"server": ["log"]}, nargs=1)
+def _slot_valid(q):
+    """PaxosTest.slotValid(st, i) (PaxosTest.java:215-279): no garbage collection, so a slot below
+    1 is invalid (not CLEARED below firstNonCleared) and one past the log is EMPTY everywhere."""
+    i = q.let("i", q.arg(0))
+    with q.if_(i < 1):
+        q.ret(False)
+    with q.if_(i > SLOTS):
+        q.ret(True)
+    is_chosen, conflict = q.var("isch", 0), q.var("confl", 0)
+    chosen, count = q.var("chosen", 0), q.var("count", 0)
+    for s in range(3):
+        with q.if_(lit(s) < q.count(server)):
+            e = q.let(_n("e"), q.at_node(server, s, "log", i - 1))
+            with q.if_(st(e) == CHOSEN):
+                x = q.let(_n("x"), _kv_cmd(q, ec(e)))
+                with q.if_((is_chosen != 0) & (x != chosen)):
+                    q.assign("confl", 1)
+                q.assign("chosen", x)
+                q.assign("isch", 1)
+    for s in range(3):
+        with q.if_(lit(s) < q.count(server)):
+            e = q.let(_n("e"), q.at_node(server, s, "log", i - 1))
+            with q.if_((st(e) != EMPTY) & ((st(e) != ACCEPTED) | (_kv_cmd(q, ec(e)) == chosen))):
+                q.assign("count", count + 1)
+    with q.if_((is_chosen != 0) & ((conflict != 0) | (count * 2 <= q.count(server)))):
+        q.ret(False)
+    q.ret(True)
+
+
+def _server_entry(q, code_shift):
+    """The log entry of server arg0 (a node address; a non-server throws: the reference's
+    (PaxosServer) st.server(a) cast) in slot arg1 >> code_shift (EMPTY outside the log)."""
+    k = q.let(_n("k"), q.arg(0) - q.node(server, 1))
+    with q.if_((k < 0) | (k >= q.count(server))):
+        q.ret("threw")
+    slot = q.let(_n("slot"), q.arg(1).shr(code_shift))
+    e = q.var(_n("se"), 0)
+    with q.if_((slot >= 1) & (slot <= SLOTS)):
+        q.assign(e.dev[2:], q.at_node(server, k, "log", slot - 1))
+    return e
+
+
+@P.predicate("Server has status in slot", ids=[403], names=["hasStatus"], reads={"server": ["log"]}, nargs=2)
+def _has_status(q):
+    """PaxosTest.hasStatus(a, i, s) (PaxosTest.java:113-117): arg1 = i << 4 | status."""
+    e = _server_entry(q, 4)
+    with q.if_(st(e) == q.arg(1).band(15)):
+        q.ret(True)
+    q.ret(False)
+
+
+@P.predicate("Server has command in slot", ids=[404], names=["hasCommand"], reads={"server": ["log"]}, nargs=2)
+def _has_command(q):
+    """PaxosTest.hasCommand(a, i, c) (PaxosTest.java:119-123): arg1 = i << 8 | KV command code
+    (op << 2 | value token; 0 = null: an empty slot or a no-op)."""
+    e = _server_entry(q, 8)
+    c = q.let("cc", select(st(e) == EMPTY, 0, _kv_cmd(q, ec(e))))
+    with q.if_(c == q.arg(1).band(255)):
+        q.ret(True)
+    q.ret(False)
+
+
 @P.predicate("Sequence of appends to the same key is linearizable", ids=[300],
              names=["APPENDS_LINEARIZABLE"], reads={"client": ["_results"]})
 def _appends_linearizable(q):

@@ -779,3 +779,14 @@ class MultiPaxosIR(IRProtocol):
 
     def oracle_args(self):
         return ["--proto", "multipaxos_ir", "--ir-params", ",".join(str(x) for x in self.params())]
+
+    IR_NAMES = {402: "slotValid", 403: "hasStatus", 404: "hasCommand"}
+
+    def ir_oracle_name(self, name: str) -> str:
+        """A lab3 argument predicate (MultiPaxos.predicate's slotValid:i / hasStatus:serverK:i:S /
+        hasCommand:serverK:i:C) as the IR oracle's NAME:arg0[:arg1] (the server as its node index)."""
+        sp = self.mp.predicate(name)
+        if sp.pred_id == 402:
+            return f"slotValid:{sp.arg0}"
+        a0 = int(name.split(":")[1][len("server"):]) - 1
+        return f"{self.IR_NAMES[sp.pred_id]}:{a0}:{sp.arg1}"

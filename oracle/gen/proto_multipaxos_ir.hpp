@@ -1531,181 +1531,295 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
       return res_;
     }};
   }
+  if ((base_ == "slotValid") && parts_.size() == 2) {
+    return Predicate{"Logs consistent for slot", [prm, a0_, a1_](const State& s) {
+      (void)s; (void)a0_; (void)a1_;
+      PredResult res_;
+      const int l_i = a0_;
+      if ((l_i < 1)) {
+        { res_.value = false; return res_; }
+      }
+      if ((l_i > 4)) {
+        { res_.value = true; return res_; }
+      }
+      int l_isch = 0;
+      int l_confl = 0;
+      int l_chosen = 0;
+      int l_count = 0;
+      if ((0 < prm.servers)) {
+        const int l_e233 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
+        if (((l_e233 & 3) == 2)) {
+          const int l_x234 = ((((l_e233 >> 8) & 7) != 0) ? ((prm.op[((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x234 != l_chosen))) {
+            l_confl = 1;
+          }
+          l_chosen = l_x234;
+          l_isch = 1;
+        }
+      }
+      if ((1 < prm.servers)) {
+        const int l_e235 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
+        if (((l_e235 & 3) == 2)) {
+          const int l_x236 = ((((l_e235 >> 8) & 7) != 0) ? ((prm.op[((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x236 != l_chosen))) {
+            l_confl = 1;
+          }
+          l_chosen = l_x236;
+          l_isch = 1;
+        }
+      }
+      if ((2 < prm.servers)) {
+        const int l_e237 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
+        if (((l_e237 & 3) == 2)) {
+          const int l_x238 = ((((l_e237 >> 8) & 7) != 0) ? ((prm.op[((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x238 != l_chosen))) {
+            l_confl = 1;
+          }
+          l_chosen = l_x238;
+          l_isch = 1;
+        }
+      }
+      if ((0 < prm.servers)) {
+        const int l_e239 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
+        if ((((l_e239 & 3) != 0) && (((l_e239 & 3) != 1) || (((((l_e239 >> 8) & 7) != 0) ? ((prm.op[((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+          l_count = (l_count + 1);
+        }
+      }
+      if ((1 < prm.servers)) {
+        const int l_e240 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
+        if ((((l_e240 & 3) != 0) && (((l_e240 & 3) != 1) || (((((l_e240 >> 8) & 7) != 0) ? ((prm.op[((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+          l_count = (l_count + 1);
+        }
+      }
+      if ((2 < prm.servers)) {
+        const int l_e241 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
+        if ((((l_e241 & 3) != 0) && (((l_e241 & 3) != 1) || (((((l_e241 >> 8) & 7) != 0) ? ((prm.op[((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+          l_count = (l_count + 1);
+        }
+      }
+      if (((l_isch != 0) && ((l_confl != 0) || ((l_count * 2) <= prm.servers)))) {
+        { res_.value = false; return res_; }
+      }
+      { res_.value = true; return res_; }
+      return res_;
+    }};
+  }
+  if ((base_ == "hasStatus") && parts_.size() == 3) {
+    return Predicate{"Server has status in slot", [prm, a0_, a1_](const State& s) {
+      (void)s; (void)a0_; (void)a1_;
+      PredResult res_;
+      const int l_k242 = (a0_ - (first_server(prm) + 1 - 1));
+      if (((l_k242 < 0) || (l_k242 >= prm.servers))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_slot243 = (a1_ >> 4);
+      int l_se244 = 0;
+      if (((l_slot243 >= 1) && (l_slot243 <= 4))) {
+        l_se244 = n_server(s, first_server(prm) + l_k242)->log[(l_slot243 - 1)];
+      }
+      if (((l_se244 & 3) == (a1_ & 15))) {
+        { res_.value = true; return res_; }
+      }
+      { res_.value = false; return res_; }
+      return res_;
+    }};
+  }
+  if ((base_ == "hasCommand") && parts_.size() == 3) {
+    return Predicate{"Server has command in slot", [prm, a0_, a1_](const State& s) {
+      (void)s; (void)a0_; (void)a1_;
+      PredResult res_;
+      const int l_k245 = (a0_ - (first_server(prm) + 1 - 1));
+      if (((l_k245 < 0) || (l_k245 >= prm.servers))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_slot246 = (a1_ >> 8);
+      int l_se247 = 0;
+      if (((l_slot246 >= 1) && (l_slot246 <= 4))) {
+        l_se247 = n_server(s, first_server(prm) + l_k245)->log[(l_slot246 - 1)];
+      }
+      const int l_cc = (((l_se247 & 3) == 0) ? 0 : ((((l_se247 >> 8) & 7) != 0) ? ((prm.op[((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0));
+      if ((l_cc == (a1_ & 255))) {
+        { res_.value = true; return res_; }
+      }
+      { res_.value = false; return res_; }
+      return res_;
+    }};
+  }
   if ((base_ == "APPENDS_LINEARIZABLE") && parts_.size() == 1) {
     return Predicate{"Sequence of appends to the same key is linearizable", [prm, a0_, a1_](const State& s) {
       (void)s; (void)a0_; (void)a1_;
       PredResult res_;
-      const int l_pres233 = ((0 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres233 && (prm.op[0][0] != 2))) {
+      const int l_pres248 = ((0 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres248 && (prm.op[0][0] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res234 = (l_pres233 ? std::stoi(s.cw(first_client(prm) + 0)->results[0].f[0]) : 0);
-      const int l_rlen235 = (l_res234 & 7);
-      if ((l_pres233 && (((l_rlen235 == 0) || (l_rlen235 > 4)) || (((l_res234 >> (1 + (l_rlen235 * 2))) & 3) != prm.val[0][0])))) {
-        { res_.value = false; return res_; }
-      }
-      const int l_pres236 = ((0 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres236 && (prm.op[0][1] != 2))) {
-        throw std::runtime_error("predicate threw");
-      }
-      const int l_res237 = (l_pres236 ? std::stoi(s.cw(first_client(prm) + 0)->results[1].f[0]) : 0);
-      const int l_rlen238 = (l_res237 & 7);
-      if ((l_pres236 && (((l_rlen238 == 0) || (l_rlen238 > 4)) || (((l_res237 >> (1 + (l_rlen238 * 2))) & 3) != prm.val[0][1])))) {
-        { res_.value = false; return res_; }
-      }
-      const int l_pres239 = ((0 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres239 && (prm.op[0][2] != 2))) {
-        throw std::runtime_error("predicate threw");
-      }
-      const int l_res240 = (l_pres239 ? std::stoi(s.cw(first_client(prm) + 0)->results[2].f[0]) : 0);
-      const int l_rlen241 = (l_res240 & 7);
-      if ((l_pres239 && (((l_rlen241 == 0) || (l_rlen241 > 4)) || (((l_res240 >> (1 + (l_rlen241 * 2))) & 3) != prm.val[0][2])))) {
-        { res_.value = false; return res_; }
-      }
-      const int l_pres242 = ((1 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres242 && (prm.op[1][0] != 2))) {
-        throw std::runtime_error("predicate threw");
-      }
-      const int l_res243 = (l_pres242 ? std::stoi(s.cw(first_client(prm) + 1)->results[0].f[0]) : 0);
-      const int l_rlen244 = (l_res243 & 7);
-      if ((l_pres242 && (((l_rlen244 == 0) || (l_rlen244 > 4)) || (((l_res243 >> (1 + (l_rlen244 * 2))) & 3) != prm.val[1][0])))) {
-        { res_.value = false; return res_; }
-      }
-      const int l_pres245 = ((1 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres245 && (prm.op[1][1] != 2))) {
-        throw std::runtime_error("predicate threw");
-      }
-      const int l_res246 = (l_pres245 ? std::stoi(s.cw(first_client(prm) + 1)->results[1].f[0]) : 0);
-      const int l_rlen247 = (l_res246 & 7);
-      if ((l_pres245 && (((l_rlen247 == 0) || (l_rlen247 > 4)) || (((l_res246 >> (1 + (l_rlen247 * 2))) & 3) != prm.val[1][1])))) {
-        { res_.value = false; return res_; }
-      }
-      const int l_pres248 = ((1 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres248 && (prm.op[1][2] != 2))) {
-        throw std::runtime_error("predicate threw");
-      }
-      const int l_res249 = (l_pres248 ? std::stoi(s.cw(first_client(prm) + 1)->results[2].f[0]) : 0);
+      const int l_res249 = (l_pres248 ? std::stoi(s.cw(first_client(prm) + 0)->results[0].f[0]) : 0);
       const int l_rlen250 = (l_res249 & 7);
-      if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != prm.val[1][2])))) {
+      if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != prm.val[0][0])))) {
         { res_.value = false; return res_; }
       }
-      if ((l_pres233 && l_pres236)) {
-        if ((l_rlen235 == l_rlen238)) {
+      const int l_pres251 = ((0 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres251 && (prm.op[0][1] != 2))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_res252 = (l_pres251 ? std::stoi(s.cw(first_client(prm) + 0)->results[1].f[0]) : 0);
+      const int l_rlen253 = (l_res252 & 7);
+      if ((l_pres251 && (((l_rlen253 == 0) || (l_rlen253 > 4)) || (((l_res252 >> (1 + (l_rlen253 * 2))) & 3) != prm.val[0][1])))) {
+        { res_.value = false; return res_; }
+      }
+      const int l_pres254 = ((0 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres254 && (prm.op[0][2] != 2))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_res255 = (l_pres254 ? std::stoi(s.cw(first_client(prm) + 0)->results[2].f[0]) : 0);
+      const int l_rlen256 = (l_res255 & 7);
+      if ((l_pres254 && (((l_rlen256 == 0) || (l_rlen256 > 4)) || (((l_res255 >> (1 + (l_rlen256 * 2))) & 3) != prm.val[0][2])))) {
+        { res_.value = false; return res_; }
+      }
+      const int l_pres257 = ((1 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres257 && (prm.op[1][0] != 2))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_res258 = (l_pres257 ? std::stoi(s.cw(first_client(prm) + 1)->results[0].f[0]) : 0);
+      const int l_rlen259 = (l_res258 & 7);
+      if ((l_pres257 && (((l_rlen259 == 0) || (l_rlen259 > 4)) || (((l_res258 >> (1 + (l_rlen259 * 2))) & 3) != prm.val[1][0])))) {
+        { res_.value = false; return res_; }
+      }
+      const int l_pres260 = ((1 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres260 && (prm.op[1][1] != 2))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_res261 = (l_pres260 ? std::stoi(s.cw(first_client(prm) + 1)->results[1].f[0]) : 0);
+      const int l_rlen262 = (l_res261 & 7);
+      if ((l_pres260 && (((l_rlen262 == 0) || (l_rlen262 > 4)) || (((l_res261 >> (1 + (l_rlen262 * 2))) & 3) != prm.val[1][1])))) {
+        { res_.value = false; return res_; }
+      }
+      const int l_pres263 = ((1 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres263 && (prm.op[1][2] != 2))) {
+        throw std::runtime_error("predicate threw");
+      }
+      const int l_res264 = (l_pres263 ? std::stoi(s.cw(first_client(prm) + 1)->results[2].f[0]) : 0);
+      const int l_rlen265 = (l_res264 & 7);
+      if ((l_pres263 && (((l_rlen265 == 0) || (l_rlen265 > 4)) || (((l_res264 >> (1 + (l_rlen265 * 2))) & 3) != prm.val[1][2])))) {
+        { res_.value = false; return res_; }
+      }
+      if ((l_pres248 && l_pres251)) {
+        if ((l_rlen250 == l_rlen253)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen238) ? l_rlen235 : l_rlen238) * 2)) - 1)) != ((l_res237 >> 3) & ((1 << (((l_rlen235 < l_rlen238) ? l_rlen235 : l_rlen238) * 2)) - 1)))) {
+        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)) != ((l_res252 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres233 && l_pres239)) {
-        if ((l_rlen235 == l_rlen241)) {
+      if ((l_pres248 && l_pres254)) {
+        if ((l_rlen250 == l_rlen256)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen241) ? l_rlen235 : l_rlen241) * 2)) - 1)) != ((l_res240 >> 3) & ((1 << (((l_rlen235 < l_rlen241) ? l_rlen235 : l_rlen241) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres233 && l_pres242)) {
-        if ((l_rlen235 == l_rlen244)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen244) ? l_rlen235 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen235 < l_rlen244) ? l_rlen235 : l_rlen244) * 2)) - 1)))) {
+        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres233 && l_pres245)) {
-        if ((l_rlen235 == l_rlen247)) {
+      if ((l_pres248 && l_pres257)) {
+        if ((l_rlen250 == l_rlen259)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen247) ? l_rlen235 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen235 < l_rlen247) ? l_rlen235 : l_rlen247) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres233 && l_pres248)) {
-        if ((l_rlen235 == l_rlen250)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res234 >> 3) & ((1 << (((l_rlen235 < l_rlen250) ? l_rlen235 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen235 < l_rlen250) ? l_rlen235 : l_rlen250) * 2)) - 1)))) {
+        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres236 && l_pres239)) {
-        if ((l_rlen238 == l_rlen241)) {
+      if ((l_pres248 && l_pres260)) {
+        if ((l_rlen250 == l_rlen262)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen241) ? l_rlen238 : l_rlen241) * 2)) - 1)) != ((l_res240 >> 3) & ((1 << (((l_rlen238 < l_rlen241) ? l_rlen238 : l_rlen241) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres236 && l_pres242)) {
-        if ((l_rlen238 == l_rlen244)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen244) ? l_rlen238 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen238 < l_rlen244) ? l_rlen238 : l_rlen244) * 2)) - 1)))) {
+        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres236 && l_pres245)) {
-        if ((l_rlen238 == l_rlen247)) {
+      if ((l_pres248 && l_pres263)) {
+        if ((l_rlen250 == l_rlen265)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen247) ? l_rlen238 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen238 < l_rlen247) ? l_rlen238 : l_rlen247) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres236 && l_pres248)) {
-        if ((l_rlen238 == l_rlen250)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res237 >> 3) & ((1 << (((l_rlen238 < l_rlen250) ? l_rlen238 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen238 < l_rlen250) ? l_rlen238 : l_rlen250) * 2)) - 1)))) {
+        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres239 && l_pres242)) {
-        if ((l_rlen241 == l_rlen244)) {
+      if ((l_pres251 && l_pres254)) {
+        if ((l_rlen253 == l_rlen256)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen244) ? l_rlen241 : l_rlen244) * 2)) - 1)) != ((l_res243 >> 3) & ((1 << (((l_rlen241 < l_rlen244) ? l_rlen241 : l_rlen244) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres239 && l_pres245)) {
-        if ((l_rlen241 == l_rlen247)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen247) ? l_rlen241 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen241 < l_rlen247) ? l_rlen241 : l_rlen247) * 2)) - 1)))) {
+        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres239 && l_pres248)) {
-        if ((l_rlen241 == l_rlen250)) {
+      if ((l_pres251 && l_pres257)) {
+        if ((l_rlen253 == l_rlen259)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res240 >> 3) & ((1 << (((l_rlen241 < l_rlen250) ? l_rlen241 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen241 < l_rlen250) ? l_rlen241 : l_rlen250) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres242 && l_pres245)) {
-        if ((l_rlen244 == l_rlen247)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res243 >> 3) & ((1 << (((l_rlen244 < l_rlen247) ? l_rlen244 : l_rlen247) * 2)) - 1)) != ((l_res246 >> 3) & ((1 << (((l_rlen244 < l_rlen247) ? l_rlen244 : l_rlen247) * 2)) - 1)))) {
+        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres242 && l_pres248)) {
-        if ((l_rlen244 == l_rlen250)) {
+      if ((l_pres251 && l_pres260)) {
+        if ((l_rlen253 == l_rlen262)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res243 >> 3) & ((1 << (((l_rlen244 < l_rlen250) ? l_rlen244 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen244 < l_rlen250) ? l_rlen244 : l_rlen250) * 2)) - 1)))) {
+        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres245 && l_pres248)) {
-        if ((l_rlen247 == l_rlen250)) {
+      if ((l_pres251 && l_pres263)) {
+        if ((l_rlen253 == l_rlen265)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res246 >> 3) & ((1 << (((l_rlen247 < l_rlen250) ? l_rlen247 : l_rlen250) * 2)) - 1)) != ((l_res249 >> 3) & ((1 << (((l_rlen247 < l_rlen250) ? l_rlen247 : l_rlen250) * 2)) - 1)))) {
+        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres254 && l_pres257)) {
+        if ((l_rlen256 == l_rlen259)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres254 && l_pres260)) {
+        if ((l_rlen256 == l_rlen262)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres254 && l_pres263)) {
+        if ((l_rlen256 == l_rlen265)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres257 && l_pres260)) {
+        if ((l_rlen259 == l_rlen262)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres257 && l_pres263)) {
+        if ((l_rlen259 == l_rlen265)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres260 && l_pres263)) {
+        if ((l_rlen262 == l_rlen265)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res261 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }

@@ -116,3 +116,27 @@ def test_ir_pb_matches_golden(name, shards):
         rep = oracle_util.replay(_pb_oracle_args(proto, [a for a in rest if a != "--finish-level"]), st.trace())
         assert rep["ok"], rep["error"]
         assert rep["depth"] == st.depth()
+
+
+def _lab3():
+    from test_gpu_multipaxos import LIVE
+    return LIVE
+
+
+@pytest.mark.parametrize("name", sorted(_lab3()))
+def test_ir_multipaxos_lab3_predicates(name):
+    """PaxosTest's argument predicates (slotValid, hasStatus, hasCommand, in combinators) on the
+    IR-generated Multi-Paxos on the MI355X engine: the hand-written protocol's oracle run, per
+    depth; terminal traces replay on the IR oracle."""
+    from test_ir import _mp_ir, _mp_oracle_args
+    args = _lab3()[name]
+    want = oracle_util.run("bfs", args + ["--finish-level"], timeout=300)
+    proto, rest = _mp_ir(args)
+    r = Engine(proto).bfs(proto.initial_state(), argmap.settings(rest, proto, table_log2=20))
+    assert r.endCondition().name == want["end"]
+    assert r.per_depth == want["per_depth"]
+    st = r.invariantViolatingState() or r.goalMatchingState()
+    if st is not None:
+        rep = oracle_util.replay(_mp_oracle_args(proto, rest), st.trace())
+        assert rep["ok"], rep["error"]
+        assert rep["depth"] == st.depth()

@@ -13,7 +13,7 @@ import pytest
 
 import argmap
 import oracle_util
-from test_hostcheck import protocheck, run  # noqa: F401  (fixture)
+from test_hostcheck import _X, protocheck, run  # noqa: F401  (fixture)
 from tools import cpu_baseline
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -239,4 +239,56 @@ def test_ir_pb_device_form_host_bfs(protocheck, servers, clients, workload, tail
     want = run(protocheck, [6] + PB(servers, clients, workload).params() + tail)
     assert got["per_depth"] == want["per_depth"]
     assert got["end"] == want["end"]
+    assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
+
+
+# ---- lab3 argument predicates on the IR Multi-Paxos: slotValid(i), hasStatus(a, i, s), hasCommand(a, i, c) ---------
+_MP_LEAF = r"(slotValid|hasStatus|hasCommand)(:[^,()]+)"
+
+
+def _mp_oracle_args(proto, rest):
+    """The arguments for the IR oracle: PaxosTest's predicate leaves as the spec's NAME:arg0[:arg1]."""
+    import re
+    out = []
+    for k, a in enumerate(rest):
+        if k and rest[k - 1] in ("--inv", "--goal", "--prune"):
+            a = re.sub(_MP_LEAF, lambda m: proto.ir_oracle_name(m.group(0)), a)
+        out.append(a)
+    return proto.oracle_args() + out
+
+
+def _lab3_cases():
+    from test_gpu_multipaxos import LIVE
+    return LIVE
+
+
+@pytest.mark.parametrize("name", sorted(_lab3_cases()))
+def test_ir_multipaxos_lab3_predicates(name):
+    """PaxosTest's predicate flows (the hand-written protocol's lab3 cases, PaxosTest.java:113-346,
+    test27 included): the IR oracle and the generated device form in the CPU BFS against the
+    hand-written protocol on the oracle, per depth."""
+    args = _lab3_cases()[name] + ["--finish-level"]
+    want = oracle_util.run("bfs", args, timeout=300)
+    proto, rest = _mp_ir(args)
+    got = oracle_util.run("bfs", _mp_oracle_args(proto, rest), timeout=300)
+    assert got["end"] == want["end"] and got["per_depth"] == want["per_depth"]
+    r = cpu_baseline.run(proto, argmap.settings(rest, proto, table_log2=20), threads=4)
+    assert r["end"] == want["end"] and r["per_depth"] == want["per_depth"]
+
+
+@pytest.mark.parametrize("tail", [
+    ["--", 1, 401, "/", f"403:1:{(1 << 4) | 2}", "/", 10],
+    ["--", f"403:0:{(1 << 4) | 2},not,404:0:{(1 << 8) | _X},or", "402:1", "/", "/", 10],
+    ["--", 400, "/", f"403:0:{(2 << 4) | 2},403:1:{(2 << 4) | 1},-403:2:{(2 << 4) | 0},or,and", "/", 9],
+    ["--", "402:1,402:2,and", "402:0,not", "/", "/", 8],
+])
+def test_ir_multipaxos_lab3_predicates_host_bfs(protocheck, tail):  # noqa: F811
+    """Exact host BFS: the generated argument predicates against the hand-written ones
+    (tests/hostcheck, protocols 10 and 5), with the incremental judge cross-checked on every
+    successor (their declared read set: the servers' logs)."""
+    from dslabs_amd.protocols import MultiPaxos, MultiPaxosIR
+    got = run(protocheck, [10] + MultiPaxosIR(3, 2, "append-xy").params() + tail)
+    want = run(protocheck, [5] + MultiPaxos(3, 2, "append-xy").params() + tail)
+    assert got["per_depth"] == want["per_depth"] and got["end"] == want["end"]
+    assert got["terminals_at_depth"] == want["terminals_at_depth"]
     assert got["fp_mismatch"] == 0 and got["emit_mismatch"] == 0 and got["judge_mismatch"] == 0
