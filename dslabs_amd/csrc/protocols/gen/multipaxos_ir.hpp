@@ -64,14 +64,6 @@ struct MultiPaxosIR {
     const uint64_t x = (((uint64_t)w[5]) & ~((uint64_t)7u << sh)) | ((uint64_t)((uint32_t)v & 7u) << sh);
     w[5] = (uint32_t)x;
   }
-  static DSL_HD int arr_server__timers(const uint32_t* w, int j) {
-    return (int)((((uint64_t)w[5]) >> (14 + (j) / 2 * 32 + (j) % 2 * 3)) & 7u);
-  }
-  static DSL_HD void arr_put_server__timers(uint32_t* w, int j, int v) {
-    const int sh = 14 + (j) / 2 * 32 + (j) % 2 * 3;
-    const uint64_t x = (((uint64_t)w[5]) & ~((uint64_t)7u << sh)) | ((uint64_t)((uint32_t)v & 7u) << sh);
-    w[5] = (uint32_t)x;
-  }
   static DSL_HD int arr_client__timers(const uint32_t* w, int j) {
     return (int)((((uint64_t)w[0]) >> (17 + (j) / 3 * 32 + (j) % 3 * 3)) & 7u);
   }
@@ -106,41 +98,6 @@ struct MultiPaxosIR {
     if (type == 1) { mn = 100; mx = 100; }
   }
   static DSL_HD int ttype(int e) { return e >> 2; }
-  static DSL_HD bool push_timer_server(uint32_t* w, int e) {
-    const int n = get(w, 172, 2);
-    if (n >= 2) return false;
-    arr_put_server__timers(w, n, e);
-    put(w, 172, 2, n + 1);
-    return true;
-  }
-  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)
-  static DSL_HD int deliverable_server(const uint32_t* w, int j) {
-    const int n = get(w, 172, 2);
-    return j < 0 ? (n > 0 ? 1 : 0) : (j == 0 && n > 0 ? 0 : -1);  // only the head (equal fixed durations)
-  }
-  static DSL_HD int deliverable_general_server(const uint32_t* w, int j) {
-    const int n = get(w, 172, 2);
-    int mm = 0x7fffffff, c = 0;
-    for (int q = 0; q < n; q++) {
-      int mn = 0, mx = 0;
-      tbounds(ttype(arr_server__timers(w, q)), mn, mx);
-      if (q > 0 && mn >= mm) continue;
-      if (c == j) return q;
-      c++;
-      if (mx < mm) mm = mx;
-    }
-    return j < 0 ? c : -1;
-  }
-  static DSL_HD void remove_timer_server(uint32_t* w, int e) {  // the first equal entry
-    const int n = get(w, 172, 2);
-    int q0 = n;
-    for (int q = n - 1; q >= 0; q--)
-      if (arr_server__timers(w, q) == e) q0 = q;
-    if (q0 >= n) return;
-    for (int q = q0; q + 1 < n; q++) arr_put_server__timers(w, q, arr_server__timers(w, q + 1));
-    arr_put_server__timers(w, n - 1, 0);
-    put(w, 172, 2, n - 1);
-  }
   static DSL_HD bool push_timer_client(uint32_t* w, int e) {
     const int n = get(w, 15, 2);
     if (n >= 3) return false;
@@ -182,15 +139,15 @@ struct MultiPaxosIR {
     put(w, 0, 2, cmd);
     put(w, 2, 1, 1);
     put(w, 3, 12, 0);
-    const int l_cid0 = (((i - first_client(p)) * 3) + cmd);
+    const int l_cid179 = (((i - first_client(p)) * 3) + cmd);
     if ((0 < p.servers)) {
-      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_cid0) & 7) << 0));
+      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_cid179) & 7) << 0));
     }
     if ((1 < p.servers)) {
-      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_cid0) & 7) << 0));
+      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_cid179) & 7) << 0));
     }
     if ((2 < p.servers)) {
-      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_cid0) & 7) << 0));
+      out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_cid179) & 7) << 0));
     }
     if (!push_timer_client(w, (((cmd) & 3) << 0) | (1 << 2))) return STEP_OVERFLOW;
     return STEP_OK;
@@ -221,7 +178,7 @@ struct MultiPaxosIR {
     }
   }
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {
-    if (is_server(i, p)) return deliverable_server(w, -1);
+    if (is_server(i, p)) return 1;  // [Tick] in every state
     if (is_client(i, p)) return deliverable_client(w, -1);
     (void)i; (void)w; (void)p;
     return 0;
@@ -234,7 +191,7 @@ struct MultiPaxosIR {
     if (((i - first_server(p)) == 0)) {
       put(w, 6, 1, 1);
     }
-    if (!push_timer_server(w, (0 << 2))) return STEP_OVERFLOW;
+    // set Tick: the queue stays [Tick]
     return STEP_OK;
   }
   template <class O>
@@ -243,162 +200,162 @@ struct MultiPaxosIR {
     const int l_cmd = (int)((r >> 0) & 7u);
     const int l_c = ((l_cmd >= 4) ? 1 : 0);
     const int l_q = (l_cmd - (((l_cmd >= 4) ? 1 : 0) * 3));
-    const int l_upto1 = get(w, 14, 3);
-    int l_kv2 = 0;
-    int l_ls03 = 0;
-    int l_ls14 = 0;
-    int l_r5 = 0;
-    const int l_cmd6 = ((arr_server_log(w, 0) >> 8) & 7);
-    const int l_c7 = ((l_cmd6 >= 4) ? 1 : 0);
-    const int l_q8 = (l_cmd6 - (((l_cmd6 >= 4) ? 1 : 0) * 3));
-    if ((((1 < l_upto1) && (l_cmd6 != 0)) && ((l_c7 ? l_ls14 : l_ls03) < l_q8))) {
-      const int l_c9 = ((l_cmd6 >= 4) ? 1 : 0);
-      const int l_op10 = (int)((p.op_pk >> ((2 * ((l_c9) * 3 + (((l_cmd6 - (((l_cmd6 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v11 = (int)((p.val_pk >> ((2 * ((l_c9) * 3 + (((l_cmd6 - (((l_cmd6 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x12 = 0;
-      if ((l_op10 == 1)) {
-        l_kv2 = (1 | (l_v11 << 3));
-        l_x12 = 7;
+    const int l_upto180 = get(w, 14, 3);
+    int l_kv181 = 0;
+    int l_ls0182 = 0;
+    int l_ls1183 = 0;
+    int l_r184 = 0;
+    const int l_cmd185 = ((arr_server_log(w, 0) >> 8) & 7);
+    const int l_c186 = ((l_cmd185 >= 4) ? 1 : 0);
+    const int l_q187 = (l_cmd185 - (((l_cmd185 >= 4) ? 1 : 0) * 3));
+    if ((((1 < l_upto180) && (l_cmd185 != 0)) && ((l_c186 ? l_ls1183 : l_ls0182) < l_q187))) {
+      const int l_c188 = ((l_cmd185 >= 4) ? 1 : 0);
+      const int l_op189 = (int)((p.op_pk >> ((2 * ((l_c188) * 3 + (((l_cmd185 - (((l_cmd185 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v190 = (int)((p.val_pk >> ((2 * ((l_c188) * 3 + (((l_cmd185 - (((l_cmd185 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x191 = 0;
+      if ((l_op189 == 1)) {
+        l_kv181 = (1 | (l_v190 << 3));
+        l_x191 = 7;
       }
-      if ((l_op10 == 2)) {
-        const int l_len13 = (l_kv2 & 7);
-        l_kv2 = (((l_len13 + 1) | (l_kv2 & -8)) | (l_v11 << (3 + (l_len13 * 2))));
-        l_x12 = l_kv2;
+      if ((l_op189 == 2)) {
+        const int l_len192 = (l_kv181 & 7);
+        l_kv181 = (((l_len192 + 1) | (l_kv181 & -8)) | (l_v190 << (3 + (l_len192 * 2))));
+        l_x191 = l_kv181;
       }
-      if ((l_op10 == 3)) {
-        l_x12 = (((l_kv2 & 7) != 0) ? l_kv2 : 6);
+      if ((l_op189 == 3)) {
+        l_x191 = (((l_kv181 & 7) != 0) ? l_kv181 : 6);
       }
-      if ((l_c7 != 0)) {
-        l_ls14 = l_q8;
+      if ((l_c186 != 0)) {
+        l_ls1183 = l_q187;
       } else {
-        l_ls03 = l_q8;
+        l_ls0182 = l_q187;
       }
-      if (((l_c7 == l_c) && (l_q8 == l_q))) {
-        l_r5 = l_x12;
+      if (((l_c186 == l_c) && (l_q187 == l_q))) {
+        l_r184 = l_x191;
       }
     }
-    const int l_cmd14 = ((arr_server_log(w, 1) >> 8) & 7);
-    const int l_c15 = ((l_cmd14 >= 4) ? 1 : 0);
-    const int l_q16 = (l_cmd14 - (((l_cmd14 >= 4) ? 1 : 0) * 3));
-    if ((((2 < l_upto1) && (l_cmd14 != 0)) && ((l_c15 ? l_ls14 : l_ls03) < l_q16))) {
-      const int l_c17 = ((l_cmd14 >= 4) ? 1 : 0);
-      const int l_op18 = (int)((p.op_pk >> ((2 * ((l_c17) * 3 + (((l_cmd14 - (((l_cmd14 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v19 = (int)((p.val_pk >> ((2 * ((l_c17) * 3 + (((l_cmd14 - (((l_cmd14 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x20 = 0;
-      if ((l_op18 == 1)) {
-        l_kv2 = (1 | (l_v19 << 3));
-        l_x20 = 7;
+    const int l_cmd193 = ((arr_server_log(w, 1) >> 8) & 7);
+    const int l_c194 = ((l_cmd193 >= 4) ? 1 : 0);
+    const int l_q195 = (l_cmd193 - (((l_cmd193 >= 4) ? 1 : 0) * 3));
+    if ((((2 < l_upto180) && (l_cmd193 != 0)) && ((l_c194 ? l_ls1183 : l_ls0182) < l_q195))) {
+      const int l_c196 = ((l_cmd193 >= 4) ? 1 : 0);
+      const int l_op197 = (int)((p.op_pk >> ((2 * ((l_c196) * 3 + (((l_cmd193 - (((l_cmd193 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v198 = (int)((p.val_pk >> ((2 * ((l_c196) * 3 + (((l_cmd193 - (((l_cmd193 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x199 = 0;
+      if ((l_op197 == 1)) {
+        l_kv181 = (1 | (l_v198 << 3));
+        l_x199 = 7;
       }
-      if ((l_op18 == 2)) {
-        const int l_len21 = (l_kv2 & 7);
-        l_kv2 = (((l_len21 + 1) | (l_kv2 & -8)) | (l_v19 << (3 + (l_len21 * 2))));
-        l_x20 = l_kv2;
+      if ((l_op197 == 2)) {
+        const int l_len200 = (l_kv181 & 7);
+        l_kv181 = (((l_len200 + 1) | (l_kv181 & -8)) | (l_v198 << (3 + (l_len200 * 2))));
+        l_x199 = l_kv181;
       }
-      if ((l_op18 == 3)) {
-        l_x20 = (((l_kv2 & 7) != 0) ? l_kv2 : 6);
+      if ((l_op197 == 3)) {
+        l_x199 = (((l_kv181 & 7) != 0) ? l_kv181 : 6);
       }
-      if ((l_c15 != 0)) {
-        l_ls14 = l_q16;
+      if ((l_c194 != 0)) {
+        l_ls1183 = l_q195;
       } else {
-        l_ls03 = l_q16;
+        l_ls0182 = l_q195;
       }
-      if (((l_c15 == l_c) && (l_q16 == l_q))) {
-        l_r5 = l_x20;
+      if (((l_c194 == l_c) && (l_q195 == l_q))) {
+        l_r184 = l_x199;
       }
     }
-    const int l_cmd22 = ((arr_server_log(w, 2) >> 8) & 7);
-    const int l_c23 = ((l_cmd22 >= 4) ? 1 : 0);
-    const int l_q24 = (l_cmd22 - (((l_cmd22 >= 4) ? 1 : 0) * 3));
-    if ((((3 < l_upto1) && (l_cmd22 != 0)) && ((l_c23 ? l_ls14 : l_ls03) < l_q24))) {
-      const int l_c25 = ((l_cmd22 >= 4) ? 1 : 0);
-      const int l_op26 = (int)((p.op_pk >> ((2 * ((l_c25) * 3 + (((l_cmd22 - (((l_cmd22 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v27 = (int)((p.val_pk >> ((2 * ((l_c25) * 3 + (((l_cmd22 - (((l_cmd22 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x28 = 0;
-      if ((l_op26 == 1)) {
-        l_kv2 = (1 | (l_v27 << 3));
-        l_x28 = 7;
+    const int l_cmd201 = ((arr_server_log(w, 2) >> 8) & 7);
+    const int l_c202 = ((l_cmd201 >= 4) ? 1 : 0);
+    const int l_q203 = (l_cmd201 - (((l_cmd201 >= 4) ? 1 : 0) * 3));
+    if ((((3 < l_upto180) && (l_cmd201 != 0)) && ((l_c202 ? l_ls1183 : l_ls0182) < l_q203))) {
+      const int l_c204 = ((l_cmd201 >= 4) ? 1 : 0);
+      const int l_op205 = (int)((p.op_pk >> ((2 * ((l_c204) * 3 + (((l_cmd201 - (((l_cmd201 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v206 = (int)((p.val_pk >> ((2 * ((l_c204) * 3 + (((l_cmd201 - (((l_cmd201 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x207 = 0;
+      if ((l_op205 == 1)) {
+        l_kv181 = (1 | (l_v206 << 3));
+        l_x207 = 7;
       }
-      if ((l_op26 == 2)) {
-        const int l_len29 = (l_kv2 & 7);
-        l_kv2 = (((l_len29 + 1) | (l_kv2 & -8)) | (l_v27 << (3 + (l_len29 * 2))));
-        l_x28 = l_kv2;
+      if ((l_op205 == 2)) {
+        const int l_len208 = (l_kv181 & 7);
+        l_kv181 = (((l_len208 + 1) | (l_kv181 & -8)) | (l_v206 << (3 + (l_len208 * 2))));
+        l_x207 = l_kv181;
       }
-      if ((l_op26 == 3)) {
-        l_x28 = (((l_kv2 & 7) != 0) ? l_kv2 : 6);
+      if ((l_op205 == 3)) {
+        l_x207 = (((l_kv181 & 7) != 0) ? l_kv181 : 6);
       }
-      if ((l_c23 != 0)) {
-        l_ls14 = l_q24;
+      if ((l_c202 != 0)) {
+        l_ls1183 = l_q203;
       } else {
-        l_ls03 = l_q24;
+        l_ls0182 = l_q203;
       }
-      if (((l_c23 == l_c) && (l_q24 == l_q))) {
-        l_r5 = l_x28;
+      if (((l_c202 == l_c) && (l_q203 == l_q))) {
+        l_r184 = l_x207;
       }
     }
-    const int l_cmd30 = ((arr_server_log(w, 3) >> 8) & 7);
-    const int l_c31 = ((l_cmd30 >= 4) ? 1 : 0);
-    const int l_q32 = (l_cmd30 - (((l_cmd30 >= 4) ? 1 : 0) * 3));
-    if ((((4 < l_upto1) && (l_cmd30 != 0)) && ((l_c31 ? l_ls14 : l_ls03) < l_q32))) {
-      const int l_c33 = ((l_cmd30 >= 4) ? 1 : 0);
-      const int l_op34 = (int)((p.op_pk >> ((2 * ((l_c33) * 3 + (((l_cmd30 - (((l_cmd30 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v35 = (int)((p.val_pk >> ((2 * ((l_c33) * 3 + (((l_cmd30 - (((l_cmd30 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x36 = 0;
-      if ((l_op34 == 1)) {
-        l_kv2 = (1 | (l_v35 << 3));
-        l_x36 = 7;
+    const int l_cmd209 = ((arr_server_log(w, 3) >> 8) & 7);
+    const int l_c210 = ((l_cmd209 >= 4) ? 1 : 0);
+    const int l_q211 = (l_cmd209 - (((l_cmd209 >= 4) ? 1 : 0) * 3));
+    if ((((4 < l_upto180) && (l_cmd209 != 0)) && ((l_c210 ? l_ls1183 : l_ls0182) < l_q211))) {
+      const int l_c212 = ((l_cmd209 >= 4) ? 1 : 0);
+      const int l_op213 = (int)((p.op_pk >> ((2 * ((l_c212) * 3 + (((l_cmd209 - (((l_cmd209 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v214 = (int)((p.val_pk >> ((2 * ((l_c212) * 3 + (((l_cmd209 - (((l_cmd209 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x215 = 0;
+      if ((l_op213 == 1)) {
+        l_kv181 = (1 | (l_v214 << 3));
+        l_x215 = 7;
       }
-      if ((l_op34 == 2)) {
-        const int l_len37 = (l_kv2 & 7);
-        l_kv2 = (((l_len37 + 1) | (l_kv2 & -8)) | (l_v35 << (3 + (l_len37 * 2))));
-        l_x36 = l_kv2;
+      if ((l_op213 == 2)) {
+        const int l_len216 = (l_kv181 & 7);
+        l_kv181 = (((l_len216 + 1) | (l_kv181 & -8)) | (l_v214 << (3 + (l_len216 * 2))));
+        l_x215 = l_kv181;
       }
-      if ((l_op34 == 3)) {
-        l_x36 = (((l_kv2 & 7) != 0) ? l_kv2 : 6);
+      if ((l_op213 == 3)) {
+        l_x215 = (((l_kv181 & 7) != 0) ? l_kv181 : 6);
       }
-      if ((l_c31 != 0)) {
-        l_ls14 = l_q32;
+      if ((l_c210 != 0)) {
+        l_ls1183 = l_q211;
       } else {
-        l_ls03 = l_q32;
+        l_ls0182 = l_q211;
       }
-      if (((l_c31 == l_c) && (l_q32 == l_q))) {
-        l_r5 = l_x36;
+      if (((l_c210 == l_c) && (l_q211 == l_q))) {
+        l_r184 = l_x215;
       }
     }
-    const int l_ls = (l_c ? l_ls14 : l_ls03);
+    const int l_ls = (l_c ? l_ls1183 : l_ls0182);
     if ((l_ls >= l_q)) {
       if (((get(w, 6, 1) != 0) && (l_ls == l_q))) {
-        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c + 1) - 1)) << 55) | ((Rec)((l_q) & 3) << 0) | ((Rec)((l_r5) & 4095) << 2));
+        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c + 1) - 1)) << 55) | ((Rec)((l_q) & 3) << 0) | ((Rec)((l_r184) & 4095) << 2));
       }
       return STEP_OK;
     }
     int l_slot = get(w, 17, 3);
     int l_inlog = 0;
-    const int l_e38 = arr_server_log(w, 0);
-    if ((((l_e38 & 3) != 0) && (2 > l_slot))) {
+    const int l_e217 = arr_server_log(w, 0);
+    if ((((l_e217 & 3) != 0) && (2 > l_slot))) {
       l_slot = 2;
     }
-    if ((((l_e38 & 3) != 0) && (((l_e38 >> 8) & 7) == l_cmd))) {
+    if ((((l_e217 & 3) != 0) && (((l_e217 >> 8) & 7) == l_cmd))) {
       l_inlog = 1;
     }
-    const int l_e39 = arr_server_log(w, 1);
-    if ((((l_e39 & 3) != 0) && (3 > l_slot))) {
+    const int l_e218 = arr_server_log(w, 1);
+    if ((((l_e218 & 3) != 0) && (3 > l_slot))) {
       l_slot = 3;
     }
-    if ((((l_e39 & 3) != 0) && (((l_e39 >> 8) & 7) == l_cmd))) {
+    if ((((l_e218 & 3) != 0) && (((l_e218 >> 8) & 7) == l_cmd))) {
       l_inlog = 1;
     }
-    const int l_e40 = arr_server_log(w, 2);
-    if ((((l_e40 & 3) != 0) && (4 > l_slot))) {
+    const int l_e219 = arr_server_log(w, 2);
+    if ((((l_e219 & 3) != 0) && (4 > l_slot))) {
       l_slot = 4;
     }
-    if ((((l_e40 & 3) != 0) && (((l_e40 >> 8) & 7) == l_cmd))) {
+    if ((((l_e219 & 3) != 0) && (((l_e219 >> 8) & 7) == l_cmd))) {
       l_inlog = 1;
     }
-    const int l_e41 = arr_server_log(w, 3);
-    if ((((l_e41 & 3) != 0) && (5 > l_slot))) {
+    const int l_e220 = arr_server_log(w, 3);
+    if ((((l_e220 & 3) != 0) && (5 > l_slot))) {
       l_slot = 5;
     }
-    if ((((l_e41 & 3) != 0) && (((l_e41 >> 8) & 7) == l_cmd))) {
+    if ((((l_e220 & 3) != 0) && (((l_e220 >> 8) & 7) == l_cmd))) {
       l_inlog = 1;
     }
     if ((((get(w, 6, 1) == 0) || (l_slot > 4)) || (l_inlog != 0))) {
@@ -417,17 +374,17 @@ struct MultiPaxosIR {
       out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((l_slot) & 7) << 6) | ((Rec)((l_cmd) & 7) << 9));
     }
     if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-      const int l_ccmd42 = ((arr_server_log(w, (l_slot - 1)) >> 8) & 7);
-      arr_put_server_log(w, (l_slot - 1), ((2 | (0 << 2)) | (l_ccmd42 << 8)));
+      const int l_ccmd221 = ((arr_server_log(w, (l_slot - 1)) >> 8) & 7);
+      arr_put_server_log(w, (l_slot - 1), ((2 | (0 << 2)) | (l_ccmd221 << 8)));
       arr_put_server_votes(w, (l_slot - 1), 0);
       if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd42) & 7) << 3));
+        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd221) & 7) << 3));
       }
       if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd42) & 7) << 3));
+        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd221) & 7) << 3));
       }
       if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd42) & 7) << 3));
+        out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd221) & 7) << 3));
       }
     }
     if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
@@ -470,40 +427,40 @@ struct MultiPaxosIR {
     }
     const int l_v = (get(w, 11, 3) | (1 << (rec_from(r) - (first_server(p) + 1 - 1))));
     put(w, 11, 3, l_v);
-    const int l_me43 = (int)((r >> 6) & 2047u);
-    const int l_mm44 = arr_server_p1blog(w, 0);
-    if (((l_me43 & 3) == 2)) {
-      arr_put_server_p1blog(w, 0, ((2 | (0 << 2)) | (((l_me43 >> 8) & 7) << 8)));
+    const int l_me222 = (int)((r >> 6) & 2047u);
+    const int l_mm223 = arr_server_p1blog(w, 0);
+    if (((l_me222 & 3) == 2)) {
+      arr_put_server_p1blog(w, 0, ((2 | (0 << 2)) | (((l_me222 >> 8) & 7) << 8)));
     } else {
-      if (((((l_me43 & 3) == 1) && ((l_mm44 & 3) != 2)) && (((l_mm44 & 3) == 0) || (((l_mm44 >> 2) & 63) < ((l_me43 >> 2) & 63))))) {
-        arr_put_server_p1blog(w, 0, l_me43);
+      if (((((l_me222 & 3) == 1) && ((l_mm223 & 3) != 2)) && (((l_mm223 & 3) == 0) || (((l_mm223 >> 2) & 63) < ((l_me222 >> 2) & 63))))) {
+        arr_put_server_p1blog(w, 0, l_me222);
       }
     }
-    const int l_me45 = (int)((r >> 17) & 2047u);
-    const int l_mm46 = arr_server_p1blog(w, 1);
-    if (((l_me45 & 3) == 2)) {
-      arr_put_server_p1blog(w, 1, ((2 | (0 << 2)) | (((l_me45 >> 8) & 7) << 8)));
+    const int l_me224 = (int)((r >> 17) & 2047u);
+    const int l_mm225 = arr_server_p1blog(w, 1);
+    if (((l_me224 & 3) == 2)) {
+      arr_put_server_p1blog(w, 1, ((2 | (0 << 2)) | (((l_me224 >> 8) & 7) << 8)));
     } else {
-      if (((((l_me45 & 3) == 1) && ((l_mm46 & 3) != 2)) && (((l_mm46 & 3) == 0) || (((l_mm46 >> 2) & 63) < ((l_me45 >> 2) & 63))))) {
-        arr_put_server_p1blog(w, 1, l_me45);
+      if (((((l_me224 & 3) == 1) && ((l_mm225 & 3) != 2)) && (((l_mm225 & 3) == 0) || (((l_mm225 >> 2) & 63) < ((l_me224 >> 2) & 63))))) {
+        arr_put_server_p1blog(w, 1, l_me224);
       }
     }
-    const int l_me47 = (int)((r >> 28) & 2047u);
-    const int l_mm48 = arr_server_p1blog(w, 2);
-    if (((l_me47 & 3) == 2)) {
-      arr_put_server_p1blog(w, 2, ((2 | (0 << 2)) | (((l_me47 >> 8) & 7) << 8)));
+    const int l_me226 = (int)((r >> 28) & 2047u);
+    const int l_mm227 = arr_server_p1blog(w, 2);
+    if (((l_me226 & 3) == 2)) {
+      arr_put_server_p1blog(w, 2, ((2 | (0 << 2)) | (((l_me226 >> 8) & 7) << 8)));
     } else {
-      if (((((l_me47 & 3) == 1) && ((l_mm48 & 3) != 2)) && (((l_mm48 & 3) == 0) || (((l_mm48 >> 2) & 63) < ((l_me47 >> 2) & 63))))) {
-        arr_put_server_p1blog(w, 2, l_me47);
+      if (((((l_me226 & 3) == 1) && ((l_mm227 & 3) != 2)) && (((l_mm227 & 3) == 0) || (((l_mm227 >> 2) & 63) < ((l_me226 >> 2) & 63))))) {
+        arr_put_server_p1blog(w, 2, l_me226);
       }
     }
-    const int l_me49 = (int)((r >> 39) & 2047u);
-    const int l_mm50 = arr_server_p1blog(w, 3);
-    if (((l_me49 & 3) == 2)) {
-      arr_put_server_p1blog(w, 3, ((2 | (0 << 2)) | (((l_me49 >> 8) & 7) << 8)));
+    const int l_me228 = (int)((r >> 39) & 2047u);
+    const int l_mm229 = arr_server_p1blog(w, 3);
+    if (((l_me228 & 3) == 2)) {
+      arr_put_server_p1blog(w, 3, ((2 | (0 << 2)) | (((l_me228 >> 8) & 7) << 8)));
     } else {
-      if (((((l_me49 & 3) == 1) && ((l_mm50 & 3) != 2)) && (((l_mm50 & 3) == 0) || (((l_mm50 >> 2) & 63) < ((l_me49 >> 2) & 63))))) {
-        arr_put_server_p1blog(w, 3, l_me49);
+      if (((((l_me228 & 3) == 1) && ((l_mm229 & 3) != 2)) && (((l_mm229 & 3) == 0) || (((l_mm229 >> 2) & 63) < ((l_me228 >> 2) & 63))))) {
+        arr_put_server_p1blog(w, 3, l_me228);
       }
     }
     if ((!(((((l_v & 1) + ((l_v >> 1) & 1)) + ((l_v >> 2) & 1)) * 2) > p.servers))) {
@@ -555,17 +512,17 @@ struct MultiPaxosIR {
     if ((!(((((l_v & 1) + ((l_v >> 1) & 1)) + ((l_v >> 2) & 1)) * 2) > p.servers))) {
       return STEP_OK;
     }
-    const int l_ccmd51 = ((arr_server_log(w, (l_slot - 1)) >> 8) & 7);
-    arr_put_server_log(w, (l_slot - 1), ((2 | (0 << 2)) | (l_ccmd51 << 8)));
+    const int l_ccmd230 = ((arr_server_log(w, (l_slot - 1)) >> 8) & 7);
+    arr_put_server_log(w, (l_slot - 1), ((2 | (0 << 2)) | (l_ccmd230 << 8)));
     arr_put_server_votes(w, (l_slot - 1), 0);
     if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd51) & 7) << 3));
+      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd230) & 7) << 3));
     }
     if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd51) & 7) << 3));
+      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd230) & 7) << 3));
     }
     if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd51) & 7) << 3));
+      out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_slot) & 7) << 0) | ((Rec)((l_ccmd230) & 7) << 3));
     }
     fl |= 1;
     return STEP_OK;
@@ -643,40 +600,40 @@ struct MultiPaxosIR {
           arr_put_server_votes(w, 3, 0);
           arr_put_server_p1blog(w, 3, 0);
           put(w, 11, 3, (1 << (i - first_server(p))));
-          const int l_me52 = arr_server_log(w, 0);
-          const int l_mm53 = arr_server_p1blog(w, 0);
-          if (((l_me52 & 3) == 2)) {
-            arr_put_server_p1blog(w, 0, ((2 | (0 << 2)) | (((l_me52 >> 8) & 7) << 8)));
+          const int l_me231 = arr_server_log(w, 0);
+          const int l_mm232 = arr_server_p1blog(w, 0);
+          if (((l_me231 & 3) == 2)) {
+            arr_put_server_p1blog(w, 0, ((2 | (0 << 2)) | (((l_me231 >> 8) & 7) << 8)));
           } else {
-            if (((((l_me52 & 3) == 1) && ((l_mm53 & 3) != 2)) && (((l_mm53 & 3) == 0) || (((l_mm53 >> 2) & 63) < ((l_me52 >> 2) & 63))))) {
-              arr_put_server_p1blog(w, 0, l_me52);
+            if (((((l_me231 & 3) == 1) && ((l_mm232 & 3) != 2)) && (((l_mm232 & 3) == 0) || (((l_mm232 >> 2) & 63) < ((l_me231 >> 2) & 63))))) {
+              arr_put_server_p1blog(w, 0, l_me231);
             }
           }
-          const int l_me54 = arr_server_log(w, 1);
-          const int l_mm55 = arr_server_p1blog(w, 1);
-          if (((l_me54 & 3) == 2)) {
-            arr_put_server_p1blog(w, 1, ((2 | (0 << 2)) | (((l_me54 >> 8) & 7) << 8)));
+          const int l_me233 = arr_server_log(w, 1);
+          const int l_mm234 = arr_server_p1blog(w, 1);
+          if (((l_me233 & 3) == 2)) {
+            arr_put_server_p1blog(w, 1, ((2 | (0 << 2)) | (((l_me233 >> 8) & 7) << 8)));
           } else {
-            if (((((l_me54 & 3) == 1) && ((l_mm55 & 3) != 2)) && (((l_mm55 & 3) == 0) || (((l_mm55 >> 2) & 63) < ((l_me54 >> 2) & 63))))) {
-              arr_put_server_p1blog(w, 1, l_me54);
+            if (((((l_me233 & 3) == 1) && ((l_mm234 & 3) != 2)) && (((l_mm234 & 3) == 0) || (((l_mm234 >> 2) & 63) < ((l_me233 >> 2) & 63))))) {
+              arr_put_server_p1blog(w, 1, l_me233);
             }
           }
-          const int l_me56 = arr_server_log(w, 2);
-          const int l_mm57 = arr_server_p1blog(w, 2);
-          if (((l_me56 & 3) == 2)) {
-            arr_put_server_p1blog(w, 2, ((2 | (0 << 2)) | (((l_me56 >> 8) & 7) << 8)));
+          const int l_me235 = arr_server_log(w, 2);
+          const int l_mm236 = arr_server_p1blog(w, 2);
+          if (((l_me235 & 3) == 2)) {
+            arr_put_server_p1blog(w, 2, ((2 | (0 << 2)) | (((l_me235 >> 8) & 7) << 8)));
           } else {
-            if (((((l_me56 & 3) == 1) && ((l_mm57 & 3) != 2)) && (((l_mm57 & 3) == 0) || (((l_mm57 >> 2) & 63) < ((l_me56 >> 2) & 63))))) {
-              arr_put_server_p1blog(w, 2, l_me56);
+            if (((((l_me235 & 3) == 1) && ((l_mm236 & 3) != 2)) && (((l_mm236 & 3) == 0) || (((l_mm236 >> 2) & 63) < ((l_me235 >> 2) & 63))))) {
+              arr_put_server_p1blog(w, 2, l_me235);
             }
           }
-          const int l_me58 = arr_server_log(w, 3);
-          const int l_mm59 = arr_server_p1blog(w, 3);
-          if (((l_me58 & 3) == 2)) {
-            arr_put_server_p1blog(w, 3, ((2 | (0 << 2)) | (((l_me58 >> 8) & 7) << 8)));
+          const int l_me237 = arr_server_log(w, 3);
+          const int l_mm238 = arr_server_p1blog(w, 3);
+          if (((l_me237 & 3) == 2)) {
+            arr_put_server_p1blog(w, 3, ((2 | (0 << 2)) | (((l_me237 >> 8) & 7) << 8)));
           } else {
-            if (((((l_me58 & 3) == 1) && ((l_mm59 & 3) != 2)) && (((l_mm59 & 3) == 0) || (((l_mm59 >> 2) & 63) < ((l_me58 >> 2) & 63))))) {
-              arr_put_server_p1blog(w, 3, l_me58);
+            if (((((l_me237 & 3) == 1) && ((l_mm238 & 3) != 2)) && (((l_mm238 & 3) == 0) || (((l_mm238 >> 2) & 63) < ((l_me237 >> 2) & 63))))) {
+              arr_put_server_p1blog(w, 3, l_me237);
             }
           }
           if (((0 < p.servers) && (0 != (i - first_server(p))))) {
@@ -692,313 +649,313 @@ struct MultiPaxosIR {
             put(w, 6, 1, 1);
             put(w, 7, 1, 0);
             put(w, 11, 3, 0);
-            const int l_mg60 = arr_server_p1blog(w, 0);
-            const int l_mg61 = arr_server_p1blog(w, 1);
-            const int l_mg62 = arr_server_p1blog(w, 2);
-            const int l_mg63 = arr_server_p1blog(w, 3);
-            int l_last64 = 0;
-            if ((((l_mg60 & 3) != 0) || ((arr_server_log(w, 0) & 3) != 0))) {
-              l_last64 = 1;
+            const int l_mg239 = arr_server_p1blog(w, 0);
+            const int l_mg240 = arr_server_p1blog(w, 1);
+            const int l_mg241 = arr_server_p1blog(w, 2);
+            const int l_mg242 = arr_server_p1blog(w, 3);
+            int l_last243 = 0;
+            if ((((l_mg239 & 3) != 0) || ((arr_server_log(w, 0) & 3) != 0))) {
+              l_last243 = 1;
             }
-            if ((((l_mg61 & 3) != 0) || ((arr_server_log(w, 1) & 3) != 0))) {
-              l_last64 = 2;
+            if ((((l_mg240 & 3) != 0) || ((arr_server_log(w, 1) & 3) != 0))) {
+              l_last243 = 2;
             }
-            if ((((l_mg62 & 3) != 0) || ((arr_server_log(w, 2) & 3) != 0))) {
-              l_last64 = 3;
+            if ((((l_mg241 & 3) != 0) || ((arr_server_log(w, 2) & 3) != 0))) {
+              l_last243 = 3;
             }
-            if ((((l_mg63 & 3) != 0) || ((arr_server_log(w, 3) & 3) != 0))) {
-              l_last64 = 4;
+            if ((((l_mg242 & 3) != 0) || ((arr_server_log(w, 3) & 3) != 0))) {
+              l_last243 = 4;
             }
             arr_put_server_p1blog(w, 0, 0);
             arr_put_server_p1blog(w, 1, 0);
             arr_put_server_p1blog(w, 2, 0);
             arr_put_server_p1blog(w, 3, 0);
-            if (((1 <= l_last64) && ((arr_server_log(w, 0) & 3) != 2))) {
-              if (((l_mg60 & 3) == 2)) {
-                arr_put_server_log(w, 0, ((2 | (0 << 2)) | (((l_mg60 >> 8) & 7) << 8)));
+            if (((1 <= l_last243) && ((arr_server_log(w, 0) & 3) != 2))) {
+              if (((l_mg239 & 3) == 2)) {
+                arr_put_server_log(w, 0, ((2 | (0 << 2)) | (((l_mg239 >> 8) & 7) << 8)));
                 arr_put_server_votes(w, 0, 0);
               } else {
-                arr_put_server_log(w, (1 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg60 & 3) == 1) ? ((l_mg60 >> 8) & 7) : 0) << 8)));
+                arr_put_server_log(w, (1 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg239 & 3) == 1) ? ((l_mg239 >> 8) & 7) : 0) << 8)));
                 arr_put_server_votes(w, (1 - 1), (1 << (i - first_server(p))));
                 if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg60 & 3) == 1) ? ((l_mg60 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg239 & 3) == 1) ? ((l_mg239 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg60 & 3) == 1) ? ((l_mg60 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg239 & 3) == 1) ? ((l_mg239 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg60 & 3) == 1) ? ((l_mg60 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg239 & 3) == 1) ? ((l_mg239 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-                  const int l_ccmd65 = ((arr_server_log(w, (1 - 1)) >> 8) & 7);
-                  arr_put_server_log(w, (1 - 1), ((2 | (0 << 2)) | (l_ccmd65 << 8)));
+                  const int l_ccmd244 = ((arr_server_log(w, (1 - 1)) >> 8) & 7);
+                  arr_put_server_log(w, (1 - 1), ((2 | (0 << 2)) | (l_ccmd244 << 8)));
                   arr_put_server_votes(w, (1 - 1), 0);
                   if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd65) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd244) & 7) << 3));
                   }
                   if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd65) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd244) & 7) << 3));
                   }
                   if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd65) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd244) & 7) << 3));
                   }
                 }
               }
             }
-            if (((2 <= l_last64) && ((arr_server_log(w, 1) & 3) != 2))) {
-              if (((l_mg61 & 3) == 2)) {
-                arr_put_server_log(w, 1, ((2 | (0 << 2)) | (((l_mg61 >> 8) & 7) << 8)));
+            if (((2 <= l_last243) && ((arr_server_log(w, 1) & 3) != 2))) {
+              if (((l_mg240 & 3) == 2)) {
+                arr_put_server_log(w, 1, ((2 | (0 << 2)) | (((l_mg240 >> 8) & 7) << 8)));
                 arr_put_server_votes(w, 1, 0);
               } else {
-                arr_put_server_log(w, (2 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg61 & 3) == 1) ? ((l_mg61 >> 8) & 7) : 0) << 8)));
+                arr_put_server_log(w, (2 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg240 & 3) == 1) ? ((l_mg240 >> 8) & 7) : 0) << 8)));
                 arr_put_server_votes(w, (2 - 1), (1 << (i - first_server(p))));
                 if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg61 & 3) == 1) ? ((l_mg61 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg240 & 3) == 1) ? ((l_mg240 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg61 & 3) == 1) ? ((l_mg61 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg240 & 3) == 1) ? ((l_mg240 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg61 & 3) == 1) ? ((l_mg61 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg240 & 3) == 1) ? ((l_mg240 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-                  const int l_ccmd66 = ((arr_server_log(w, (2 - 1)) >> 8) & 7);
-                  arr_put_server_log(w, (2 - 1), ((2 | (0 << 2)) | (l_ccmd66 << 8)));
+                  const int l_ccmd245 = ((arr_server_log(w, (2 - 1)) >> 8) & 7);
+                  arr_put_server_log(w, (2 - 1), ((2 | (0 << 2)) | (l_ccmd245 << 8)));
                   arr_put_server_votes(w, (2 - 1), 0);
                   if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd66) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd245) & 7) << 3));
                   }
                   if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd66) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd245) & 7) << 3));
                   }
                   if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd66) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd245) & 7) << 3));
                   }
                 }
               }
             }
-            if (((3 <= l_last64) && ((arr_server_log(w, 2) & 3) != 2))) {
-              if (((l_mg62 & 3) == 2)) {
-                arr_put_server_log(w, 2, ((2 | (0 << 2)) | (((l_mg62 >> 8) & 7) << 8)));
+            if (((3 <= l_last243) && ((arr_server_log(w, 2) & 3) != 2))) {
+              if (((l_mg241 & 3) == 2)) {
+                arr_put_server_log(w, 2, ((2 | (0 << 2)) | (((l_mg241 >> 8) & 7) << 8)));
                 arr_put_server_votes(w, 2, 0);
               } else {
-                arr_put_server_log(w, (3 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg62 & 3) == 1) ? ((l_mg62 >> 8) & 7) : 0) << 8)));
+                arr_put_server_log(w, (3 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg241 & 3) == 1) ? ((l_mg241 >> 8) & 7) : 0) << 8)));
                 arr_put_server_votes(w, (3 - 1), (1 << (i - first_server(p))));
                 if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg62 & 3) == 1) ? ((l_mg62 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg241 & 3) == 1) ? ((l_mg241 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg62 & 3) == 1) ? ((l_mg62 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg241 & 3) == 1) ? ((l_mg241 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg62 & 3) == 1) ? ((l_mg62 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg241 & 3) == 1) ? ((l_mg241 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-                  const int l_ccmd67 = ((arr_server_log(w, (3 - 1)) >> 8) & 7);
-                  arr_put_server_log(w, (3 - 1), ((2 | (0 << 2)) | (l_ccmd67 << 8)));
+                  const int l_ccmd246 = ((arr_server_log(w, (3 - 1)) >> 8) & 7);
+                  arr_put_server_log(w, (3 - 1), ((2 | (0 << 2)) | (l_ccmd246 << 8)));
                   arr_put_server_votes(w, (3 - 1), 0);
                   if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd67) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd246) & 7) << 3));
                   }
                   if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd67) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd246) & 7) << 3));
                   }
                   if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd67) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd246) & 7) << 3));
                   }
                 }
               }
             }
-            if (((4 <= l_last64) && ((arr_server_log(w, 3) & 3) != 2))) {
-              if (((l_mg63 & 3) == 2)) {
-                arr_put_server_log(w, 3, ((2 | (0 << 2)) | (((l_mg63 >> 8) & 7) << 8)));
+            if (((4 <= l_last243) && ((arr_server_log(w, 3) & 3) != 2))) {
+              if (((l_mg242 & 3) == 2)) {
+                arr_put_server_log(w, 3, ((2 | (0 << 2)) | (((l_mg242 >> 8) & 7) << 8)));
                 arr_put_server_votes(w, 3, 0);
               } else {
-                arr_put_server_log(w, (4 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg63 & 3) == 1) ? ((l_mg63 >> 8) & 7) : 0) << 8)));
+                arr_put_server_log(w, (4 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg242 & 3) == 1) ? ((l_mg242 >> 8) & 7) : 0) << 8)));
                 arr_put_server_votes(w, (4 - 1), (1 << (i - first_server(p))));
                 if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg63 & 3) == 1) ? ((l_mg63 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg242 & 3) == 1) ? ((l_mg242 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg63 & 3) == 1) ? ((l_mg63 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg242 & 3) == 1) ? ((l_mg242 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg63 & 3) == 1) ? ((l_mg63 >> 8) & 7) : 0)) & 7) << 9));
+                  out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg242 & 3) == 1) ? ((l_mg242 >> 8) & 7) : 0)) & 7) << 9));
                 }
                 if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-                  const int l_ccmd68 = ((arr_server_log(w, (4 - 1)) >> 8) & 7);
-                  arr_put_server_log(w, (4 - 1), ((2 | (0 << 2)) | (l_ccmd68 << 8)));
+                  const int l_ccmd247 = ((arr_server_log(w, (4 - 1)) >> 8) & 7);
+                  arr_put_server_log(w, (4 - 1), ((2 | (0 << 2)) | (l_ccmd247 << 8)));
                   arr_put_server_votes(w, (4 - 1), 0);
                   if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd68) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd247) & 7) << 3));
                   }
                   if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd68) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd247) & 7) << 3));
                   }
                   if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd68) & 7) << 3));
+                    out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd247) & 7) << 3));
                   }
                 }
               }
             }
-            put(w, 17, 3, (l_last64 + 1));
-            const int l_so069 = get(w, 14, 3);
-            const int l_act70 = get(w, 6, 1);
-            int l_kv71 = 0;
-            int l_ls072 = 0;
-            int l_ls173 = 0;
-            int l_so74 = l_so069;
-            int l_run75 = 1;
-            const int l_e76 = arr_server_log(w, 0);
-            const int l_cmd77 = ((l_e76 >> 8) & 7);
-            const int l_c78 = ((l_cmd77 >= 4) ? 1 : 0);
-            const int l_q79 = (l_cmd77 - (((l_cmd77 >= 4) ? 1 : 0) * 3));
-            const int l_before80 = (1 < l_so069);
-            const int l_now81 = (((!l_before80) && (l_run75 != 0)) && ((l_e76 & 3) == 2));
-            l_run75 = (((l_run75 != 0) && (l_before80 || l_now81)) ? 1 : 0);
-            if ((((l_before80 || l_now81) && (l_cmd77 != 0)) && ((l_c78 ? l_ls173 : l_ls072) < l_q79))) {
-              const int l_c82 = ((l_cmd77 >= 4) ? 1 : 0);
-              const int l_op83 = (int)((p.op_pk >> ((2 * ((l_c82) * 3 + (((l_cmd77 - (((l_cmd77 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              const int l_v84 = (int)((p.val_pk >> ((2 * ((l_c82) * 3 + (((l_cmd77 - (((l_cmd77 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              int l_x85 = 0;
-              if ((l_op83 == 1)) {
-                l_kv71 = (1 | (l_v84 << 3));
-                l_x85 = 7;
+            put(w, 17, 3, (l_last243 + 1));
+            const int l_so0248 = get(w, 14, 3);
+            const int l_act249 = get(w, 6, 1);
+            int l_kv250 = 0;
+            int l_ls0251 = 0;
+            int l_ls1252 = 0;
+            int l_so253 = l_so0248;
+            int l_run254 = 1;
+            const int l_e255 = arr_server_log(w, 0);
+            const int l_cmd256 = ((l_e255 >> 8) & 7);
+            const int l_c257 = ((l_cmd256 >= 4) ? 1 : 0);
+            const int l_q258 = (l_cmd256 - (((l_cmd256 >= 4) ? 1 : 0) * 3));
+            const int l_before259 = (1 < l_so0248);
+            const int l_now260 = (((!l_before259) && (l_run254 != 0)) && ((l_e255 & 3) == 2));
+            l_run254 = (((l_run254 != 0) && (l_before259 || l_now260)) ? 1 : 0);
+            if ((((l_before259 || l_now260) && (l_cmd256 != 0)) && ((l_c257 ? l_ls1252 : l_ls0251) < l_q258))) {
+              const int l_c261 = ((l_cmd256 >= 4) ? 1 : 0);
+              const int l_op262 = (int)((p.op_pk >> ((2 * ((l_c261) * 3 + (((l_cmd256 - (((l_cmd256 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              const int l_v263 = (int)((p.val_pk >> ((2 * ((l_c261) * 3 + (((l_cmd256 - (((l_cmd256 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              int l_x264 = 0;
+              if ((l_op262 == 1)) {
+                l_kv250 = (1 | (l_v263 << 3));
+                l_x264 = 7;
               }
-              if ((l_op83 == 2)) {
-                const int l_len86 = (l_kv71 & 7);
-                l_kv71 = (((l_len86 + 1) | (l_kv71 & -8)) | (l_v84 << (3 + (l_len86 * 2))));
-                l_x85 = l_kv71;
+              if ((l_op262 == 2)) {
+                const int l_len265 = (l_kv250 & 7);
+                l_kv250 = (((l_len265 + 1) | (l_kv250 & -8)) | (l_v263 << (3 + (l_len265 * 2))));
+                l_x264 = l_kv250;
               }
-              if ((l_op83 == 3)) {
-                l_x85 = (((l_kv71 & 7) != 0) ? l_kv71 : 6);
+              if ((l_op262 == 3)) {
+                l_x264 = (((l_kv250 & 7) != 0) ? l_kv250 : 6);
               }
-              if ((l_c78 != 0)) {
-                l_ls173 = l_q79;
+              if ((l_c257 != 0)) {
+                l_ls1252 = l_q258;
               } else {
-                l_ls072 = l_q79;
+                l_ls0251 = l_q258;
               }
-              if ((l_now81 && (l_act70 != 0))) {
-                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c78 + 1) - 1)) << 55) | ((Rec)((l_q79) & 3) << 0) | ((Rec)((l_x85) & 4095) << 2));
+              if ((l_now260 && (l_act249 != 0))) {
+                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c257 + 1) - 1)) << 55) | ((Rec)((l_q258) & 3) << 0) | ((Rec)((l_x264) & 4095) << 2));
               }
             }
-            if (l_now81) {
-              l_so74 = 2;
+            if (l_now260) {
+              l_so253 = 2;
             }
-            const int l_e87 = arr_server_log(w, 1);
-            const int l_cmd88 = ((l_e87 >> 8) & 7);
-            const int l_c89 = ((l_cmd88 >= 4) ? 1 : 0);
-            const int l_q90 = (l_cmd88 - (((l_cmd88 >= 4) ? 1 : 0) * 3));
-            const int l_before91 = (2 < l_so069);
-            const int l_now92 = (((!l_before91) && (l_run75 != 0)) && ((l_e87 & 3) == 2));
-            l_run75 = (((l_run75 != 0) && (l_before91 || l_now92)) ? 1 : 0);
-            if ((((l_before91 || l_now92) && (l_cmd88 != 0)) && ((l_c89 ? l_ls173 : l_ls072) < l_q90))) {
-              const int l_c93 = ((l_cmd88 >= 4) ? 1 : 0);
-              const int l_op94 = (int)((p.op_pk >> ((2 * ((l_c93) * 3 + (((l_cmd88 - (((l_cmd88 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              const int l_v95 = (int)((p.val_pk >> ((2 * ((l_c93) * 3 + (((l_cmd88 - (((l_cmd88 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              int l_x96 = 0;
-              if ((l_op94 == 1)) {
-                l_kv71 = (1 | (l_v95 << 3));
-                l_x96 = 7;
+            const int l_e266 = arr_server_log(w, 1);
+            const int l_cmd267 = ((l_e266 >> 8) & 7);
+            const int l_c268 = ((l_cmd267 >= 4) ? 1 : 0);
+            const int l_q269 = (l_cmd267 - (((l_cmd267 >= 4) ? 1 : 0) * 3));
+            const int l_before270 = (2 < l_so0248);
+            const int l_now271 = (((!l_before270) && (l_run254 != 0)) && ((l_e266 & 3) == 2));
+            l_run254 = (((l_run254 != 0) && (l_before270 || l_now271)) ? 1 : 0);
+            if ((((l_before270 || l_now271) && (l_cmd267 != 0)) && ((l_c268 ? l_ls1252 : l_ls0251) < l_q269))) {
+              const int l_c272 = ((l_cmd267 >= 4) ? 1 : 0);
+              const int l_op273 = (int)((p.op_pk >> ((2 * ((l_c272) * 3 + (((l_cmd267 - (((l_cmd267 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              const int l_v274 = (int)((p.val_pk >> ((2 * ((l_c272) * 3 + (((l_cmd267 - (((l_cmd267 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              int l_x275 = 0;
+              if ((l_op273 == 1)) {
+                l_kv250 = (1 | (l_v274 << 3));
+                l_x275 = 7;
               }
-              if ((l_op94 == 2)) {
-                const int l_len97 = (l_kv71 & 7);
-                l_kv71 = (((l_len97 + 1) | (l_kv71 & -8)) | (l_v95 << (3 + (l_len97 * 2))));
-                l_x96 = l_kv71;
+              if ((l_op273 == 2)) {
+                const int l_len276 = (l_kv250 & 7);
+                l_kv250 = (((l_len276 + 1) | (l_kv250 & -8)) | (l_v274 << (3 + (l_len276 * 2))));
+                l_x275 = l_kv250;
               }
-              if ((l_op94 == 3)) {
-                l_x96 = (((l_kv71 & 7) != 0) ? l_kv71 : 6);
+              if ((l_op273 == 3)) {
+                l_x275 = (((l_kv250 & 7) != 0) ? l_kv250 : 6);
               }
-              if ((l_c89 != 0)) {
-                l_ls173 = l_q90;
+              if ((l_c268 != 0)) {
+                l_ls1252 = l_q269;
               } else {
-                l_ls072 = l_q90;
+                l_ls0251 = l_q269;
               }
-              if ((l_now92 && (l_act70 != 0))) {
-                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c89 + 1) - 1)) << 55) | ((Rec)((l_q90) & 3) << 0) | ((Rec)((l_x96) & 4095) << 2));
+              if ((l_now271 && (l_act249 != 0))) {
+                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c268 + 1) - 1)) << 55) | ((Rec)((l_q269) & 3) << 0) | ((Rec)((l_x275) & 4095) << 2));
               }
             }
-            if (l_now92) {
-              l_so74 = 3;
+            if (l_now271) {
+              l_so253 = 3;
             }
-            const int l_e98 = arr_server_log(w, 2);
-            const int l_cmd99 = ((l_e98 >> 8) & 7);
-            const int l_c100 = ((l_cmd99 >= 4) ? 1 : 0);
-            const int l_q101 = (l_cmd99 - (((l_cmd99 >= 4) ? 1 : 0) * 3));
-            const int l_before102 = (3 < l_so069);
-            const int l_now103 = (((!l_before102) && (l_run75 != 0)) && ((l_e98 & 3) == 2));
-            l_run75 = (((l_run75 != 0) && (l_before102 || l_now103)) ? 1 : 0);
-            if ((((l_before102 || l_now103) && (l_cmd99 != 0)) && ((l_c100 ? l_ls173 : l_ls072) < l_q101))) {
-              const int l_c104 = ((l_cmd99 >= 4) ? 1 : 0);
-              const int l_op105 = (int)((p.op_pk >> ((2 * ((l_c104) * 3 + (((l_cmd99 - (((l_cmd99 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              const int l_v106 = (int)((p.val_pk >> ((2 * ((l_c104) * 3 + (((l_cmd99 - (((l_cmd99 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              int l_x107 = 0;
-              if ((l_op105 == 1)) {
-                l_kv71 = (1 | (l_v106 << 3));
-                l_x107 = 7;
+            const int l_e277 = arr_server_log(w, 2);
+            const int l_cmd278 = ((l_e277 >> 8) & 7);
+            const int l_c279 = ((l_cmd278 >= 4) ? 1 : 0);
+            const int l_q280 = (l_cmd278 - (((l_cmd278 >= 4) ? 1 : 0) * 3));
+            const int l_before281 = (3 < l_so0248);
+            const int l_now282 = (((!l_before281) && (l_run254 != 0)) && ((l_e277 & 3) == 2));
+            l_run254 = (((l_run254 != 0) && (l_before281 || l_now282)) ? 1 : 0);
+            if ((((l_before281 || l_now282) && (l_cmd278 != 0)) && ((l_c279 ? l_ls1252 : l_ls0251) < l_q280))) {
+              const int l_c283 = ((l_cmd278 >= 4) ? 1 : 0);
+              const int l_op284 = (int)((p.op_pk >> ((2 * ((l_c283) * 3 + (((l_cmd278 - (((l_cmd278 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              const int l_v285 = (int)((p.val_pk >> ((2 * ((l_c283) * 3 + (((l_cmd278 - (((l_cmd278 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              int l_x286 = 0;
+              if ((l_op284 == 1)) {
+                l_kv250 = (1 | (l_v285 << 3));
+                l_x286 = 7;
               }
-              if ((l_op105 == 2)) {
-                const int l_len108 = (l_kv71 & 7);
-                l_kv71 = (((l_len108 + 1) | (l_kv71 & -8)) | (l_v106 << (3 + (l_len108 * 2))));
-                l_x107 = l_kv71;
+              if ((l_op284 == 2)) {
+                const int l_len287 = (l_kv250 & 7);
+                l_kv250 = (((l_len287 + 1) | (l_kv250 & -8)) | (l_v285 << (3 + (l_len287 * 2))));
+                l_x286 = l_kv250;
               }
-              if ((l_op105 == 3)) {
-                l_x107 = (((l_kv71 & 7) != 0) ? l_kv71 : 6);
+              if ((l_op284 == 3)) {
+                l_x286 = (((l_kv250 & 7) != 0) ? l_kv250 : 6);
               }
-              if ((l_c100 != 0)) {
-                l_ls173 = l_q101;
+              if ((l_c279 != 0)) {
+                l_ls1252 = l_q280;
               } else {
-                l_ls072 = l_q101;
+                l_ls0251 = l_q280;
               }
-              if ((l_now103 && (l_act70 != 0))) {
-                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c100 + 1) - 1)) << 55) | ((Rec)((l_q101) & 3) << 0) | ((Rec)((l_x107) & 4095) << 2));
+              if ((l_now282 && (l_act249 != 0))) {
+                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c279 + 1) - 1)) << 55) | ((Rec)((l_q280) & 3) << 0) | ((Rec)((l_x286) & 4095) << 2));
               }
             }
-            if (l_now103) {
-              l_so74 = 4;
+            if (l_now282) {
+              l_so253 = 4;
             }
-            const int l_e109 = arr_server_log(w, 3);
-            const int l_cmd110 = ((l_e109 >> 8) & 7);
-            const int l_c111 = ((l_cmd110 >= 4) ? 1 : 0);
-            const int l_q112 = (l_cmd110 - (((l_cmd110 >= 4) ? 1 : 0) * 3));
-            const int l_before113 = (4 < l_so069);
-            const int l_now114 = (((!l_before113) && (l_run75 != 0)) && ((l_e109 & 3) == 2));
-            l_run75 = (((l_run75 != 0) && (l_before113 || l_now114)) ? 1 : 0);
-            if ((((l_before113 || l_now114) && (l_cmd110 != 0)) && ((l_c111 ? l_ls173 : l_ls072) < l_q112))) {
-              const int l_c115 = ((l_cmd110 >= 4) ? 1 : 0);
-              const int l_op116 = (int)((p.op_pk >> ((2 * ((l_c115) * 3 + (((l_cmd110 - (((l_cmd110 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              const int l_v117 = (int)((p.val_pk >> ((2 * ((l_c115) * 3 + (((l_cmd110 - (((l_cmd110 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-              int l_x118 = 0;
-              if ((l_op116 == 1)) {
-                l_kv71 = (1 | (l_v117 << 3));
-                l_x118 = 7;
+            const int l_e288 = arr_server_log(w, 3);
+            const int l_cmd289 = ((l_e288 >> 8) & 7);
+            const int l_c290 = ((l_cmd289 >= 4) ? 1 : 0);
+            const int l_q291 = (l_cmd289 - (((l_cmd289 >= 4) ? 1 : 0) * 3));
+            const int l_before292 = (4 < l_so0248);
+            const int l_now293 = (((!l_before292) && (l_run254 != 0)) && ((l_e288 & 3) == 2));
+            l_run254 = (((l_run254 != 0) && (l_before292 || l_now293)) ? 1 : 0);
+            if ((((l_before292 || l_now293) && (l_cmd289 != 0)) && ((l_c290 ? l_ls1252 : l_ls0251) < l_q291))) {
+              const int l_c294 = ((l_cmd289 >= 4) ? 1 : 0);
+              const int l_op295 = (int)((p.op_pk >> ((2 * ((l_c294) * 3 + (((l_cmd289 - (((l_cmd289 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              const int l_v296 = (int)((p.val_pk >> ((2 * ((l_c294) * 3 + (((l_cmd289 - (((l_cmd289 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+              int l_x297 = 0;
+              if ((l_op295 == 1)) {
+                l_kv250 = (1 | (l_v296 << 3));
+                l_x297 = 7;
               }
-              if ((l_op116 == 2)) {
-                const int l_len119 = (l_kv71 & 7);
-                l_kv71 = (((l_len119 + 1) | (l_kv71 & -8)) | (l_v117 << (3 + (l_len119 * 2))));
-                l_x118 = l_kv71;
+              if ((l_op295 == 2)) {
+                const int l_len298 = (l_kv250 & 7);
+                l_kv250 = (((l_len298 + 1) | (l_kv250 & -8)) | (l_v296 << (3 + (l_len298 * 2))));
+                l_x297 = l_kv250;
               }
-              if ((l_op116 == 3)) {
-                l_x118 = (((l_kv71 & 7) != 0) ? l_kv71 : 6);
+              if ((l_op295 == 3)) {
+                l_x297 = (((l_kv250 & 7) != 0) ? l_kv250 : 6);
               }
-              if ((l_c111 != 0)) {
-                l_ls173 = l_q112;
+              if ((l_c290 != 0)) {
+                l_ls1252 = l_q291;
               } else {
-                l_ls072 = l_q112;
+                l_ls0251 = l_q291;
               }
-              if ((l_now114 && (l_act70 != 0))) {
-                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c111 + 1) - 1)) << 55) | ((Rec)((l_q112) & 3) << 0) | ((Rec)((l_x118) & 4095) << 2));
+              if ((l_now293 && (l_act249 != 0))) {
+                out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c290 + 1) - 1)) << 55) | ((Rec)((l_q291) & 3) << 0) | ((Rec)((l_x297) & 4095) << 2));
               }
             }
-            if (l_now114) {
-              l_so74 = 5;
+            if (l_now293) {
+              l_so253 = 5;
             }
-            put(w, 14, 3, l_so74);
+            put(w, 14, 3, l_so253);
           }
         }
       }
     }
-    if (!push_timer_server(w, (0 << 2))) return STEP_OVERFLOW;
+    // set Tick: the queue stays [Tick]
     return STEP_OK;
   }
   template <class O>
@@ -1008,309 +965,309 @@ struct MultiPaxosIR {
       put(w, 6, 1, 1);
       put(w, 7, 1, 0);
       put(w, 11, 3, 0);
-      const int l_mg120 = arr_server_p1blog(w, 0);
-      const int l_mg121 = arr_server_p1blog(w, 1);
-      const int l_mg122 = arr_server_p1blog(w, 2);
-      const int l_mg123 = arr_server_p1blog(w, 3);
-      int l_last124 = 0;
-      if ((((l_mg120 & 3) != 0) || ((arr_server_log(w, 0) & 3) != 0))) {
-        l_last124 = 1;
+      const int l_mg299 = arr_server_p1blog(w, 0);
+      const int l_mg300 = arr_server_p1blog(w, 1);
+      const int l_mg301 = arr_server_p1blog(w, 2);
+      const int l_mg302 = arr_server_p1blog(w, 3);
+      int l_last303 = 0;
+      if ((((l_mg299 & 3) != 0) || ((arr_server_log(w, 0) & 3) != 0))) {
+        l_last303 = 1;
       }
-      if ((((l_mg121 & 3) != 0) || ((arr_server_log(w, 1) & 3) != 0))) {
-        l_last124 = 2;
+      if ((((l_mg300 & 3) != 0) || ((arr_server_log(w, 1) & 3) != 0))) {
+        l_last303 = 2;
       }
-      if ((((l_mg122 & 3) != 0) || ((arr_server_log(w, 2) & 3) != 0))) {
-        l_last124 = 3;
+      if ((((l_mg301 & 3) != 0) || ((arr_server_log(w, 2) & 3) != 0))) {
+        l_last303 = 3;
       }
-      if ((((l_mg123 & 3) != 0) || ((arr_server_log(w, 3) & 3) != 0))) {
-        l_last124 = 4;
+      if ((((l_mg302 & 3) != 0) || ((arr_server_log(w, 3) & 3) != 0))) {
+        l_last303 = 4;
       }
       arr_put_server_p1blog(w, 0, 0);
       arr_put_server_p1blog(w, 1, 0);
       arr_put_server_p1blog(w, 2, 0);
       arr_put_server_p1blog(w, 3, 0);
-      if (((1 <= l_last124) && ((arr_server_log(w, 0) & 3) != 2))) {
-        if (((l_mg120 & 3) == 2)) {
-          arr_put_server_log(w, 0, ((2 | (0 << 2)) | (((l_mg120 >> 8) & 7) << 8)));
+      if (((1 <= l_last303) && ((arr_server_log(w, 0) & 3) != 2))) {
+        if (((l_mg299 & 3) == 2)) {
+          arr_put_server_log(w, 0, ((2 | (0 << 2)) | (((l_mg299 >> 8) & 7) << 8)));
           arr_put_server_votes(w, 0, 0);
         } else {
-          arr_put_server_log(w, (1 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0) << 8)));
+          arr_put_server_log(w, (1 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0) << 8)));
           arr_put_server_votes(w, (1 - 1), (1 << (i - first_server(p))));
           if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((1) & 7) << 6) | ((Rec)(((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-            const int l_ccmd125 = ((arr_server_log(w, (1 - 1)) >> 8) & 7);
-            arr_put_server_log(w, (1 - 1), ((2 | (0 << 2)) | (l_ccmd125 << 8)));
+            const int l_ccmd304 = ((arr_server_log(w, (1 - 1)) >> 8) & 7);
+            arr_put_server_log(w, (1 - 1), ((2 | (0 << 2)) | (l_ccmd304 << 8)));
             arr_put_server_votes(w, (1 - 1), 0);
             if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd125) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd304) & 7) << 3));
             }
             if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd125) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd304) & 7) << 3));
             }
             if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd125) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((1) & 7) << 0) | ((Rec)((l_ccmd304) & 7) << 3));
             }
           }
         }
       }
-      if (((2 <= l_last124) && ((arr_server_log(w, 1) & 3) != 2))) {
-        if (((l_mg121 & 3) == 2)) {
-          arr_put_server_log(w, 1, ((2 | (0 << 2)) | (((l_mg121 >> 8) & 7) << 8)));
+      if (((2 <= l_last303) && ((arr_server_log(w, 1) & 3) != 2))) {
+        if (((l_mg300 & 3) == 2)) {
+          arr_put_server_log(w, 1, ((2 | (0 << 2)) | (((l_mg300 >> 8) & 7) << 8)));
           arr_put_server_votes(w, 1, 0);
         } else {
-          arr_put_server_log(w, (2 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0) << 8)));
+          arr_put_server_log(w, (2 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0) << 8)));
           arr_put_server_votes(w, (2 - 1), (1 << (i - first_server(p))));
           if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((2) & 7) << 6) | ((Rec)(((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-            const int l_ccmd126 = ((arr_server_log(w, (2 - 1)) >> 8) & 7);
-            arr_put_server_log(w, (2 - 1), ((2 | (0 << 2)) | (l_ccmd126 << 8)));
+            const int l_ccmd305 = ((arr_server_log(w, (2 - 1)) >> 8) & 7);
+            arr_put_server_log(w, (2 - 1), ((2 | (0 << 2)) | (l_ccmd305 << 8)));
             arr_put_server_votes(w, (2 - 1), 0);
             if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd126) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd305) & 7) << 3));
             }
             if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd126) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd305) & 7) << 3));
             }
             if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd126) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((2) & 7) << 0) | ((Rec)((l_ccmd305) & 7) << 3));
             }
           }
         }
       }
-      if (((3 <= l_last124) && ((arr_server_log(w, 2) & 3) != 2))) {
-        if (((l_mg122 & 3) == 2)) {
-          arr_put_server_log(w, 2, ((2 | (0 << 2)) | (((l_mg122 >> 8) & 7) << 8)));
+      if (((3 <= l_last303) && ((arr_server_log(w, 2) & 3) != 2))) {
+        if (((l_mg301 & 3) == 2)) {
+          arr_put_server_log(w, 2, ((2 | (0 << 2)) | (((l_mg301 >> 8) & 7) << 8)));
           arr_put_server_votes(w, 2, 0);
         } else {
-          arr_put_server_log(w, (3 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0) << 8)));
+          arr_put_server_log(w, (3 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0) << 8)));
           arr_put_server_votes(w, (3 - 1), (1 << (i - first_server(p))));
           if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((3) & 7) << 6) | ((Rec)(((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-            const int l_ccmd127 = ((arr_server_log(w, (3 - 1)) >> 8) & 7);
-            arr_put_server_log(w, (3 - 1), ((2 | (0 << 2)) | (l_ccmd127 << 8)));
+            const int l_ccmd306 = ((arr_server_log(w, (3 - 1)) >> 8) & 7);
+            arr_put_server_log(w, (3 - 1), ((2 | (0 << 2)) | (l_ccmd306 << 8)));
             arr_put_server_votes(w, (3 - 1), 0);
             if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd127) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd306) & 7) << 3));
             }
             if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd127) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd306) & 7) << 3));
             }
             if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd127) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((3) & 7) << 0) | ((Rec)((l_ccmd306) & 7) << 3));
             }
           }
         }
       }
-      if (((4 <= l_last124) && ((arr_server_log(w, 3) & 3) != 2))) {
-        if (((l_mg123 & 3) == 2)) {
-          arr_put_server_log(w, 3, ((2 | (0 << 2)) | (((l_mg123 >> 8) & 7) << 8)));
+      if (((4 <= l_last303) && ((arr_server_log(w, 3) & 3) != 2))) {
+        if (((l_mg302 & 3) == 2)) {
+          arr_put_server_log(w, 3, ((2 | (0 << 2)) | (((l_mg302 >> 8) & 7) << 8)));
           arr_put_server_votes(w, 3, 0);
         } else {
-          arr_put_server_log(w, (4 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg123 & 3) == 1) ? ((l_mg123 >> 8) & 7) : 0) << 8)));
+          arr_put_server_log(w, (4 - 1), ((1 | (((get(w, 0, 4) << 2) | get(w, 4, 2)) << 2)) | ((((l_mg302 & 3) == 1) ? ((l_mg302 >> 8) & 7) : 0) << 8)));
           arr_put_server_votes(w, (4 - 1), (1 << (i - first_server(p))));
           if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg123 & 3) == 1) ? ((l_mg123 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg302 & 3) == 1) ? ((l_mg302 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg123 & 3) == 1) ? ((l_mg123 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg302 & 3) == 1) ? ((l_mg302 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg123 & 3) == 1) ? ((l_mg123 >> 8) & 7) : 0)) & 7) << 9));
+            out.send(((Rec)4 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((get(w, 0, 4)) & 15) << 0) | ((Rec)((get(w, 4, 2)) & 3) << 4) | ((Rec)((4) & 7) << 6) | ((Rec)(((((l_mg302 & 3) == 1) ? ((l_mg302 >> 8) & 7) : 0)) & 7) << 9));
           }
           if (((((((1 << (i - first_server(p))) & 1) + (((1 << (i - first_server(p))) >> 1) & 1)) + (((1 << (i - first_server(p))) >> 2) & 1)) * 2) > p.servers)) {
-            const int l_ccmd128 = ((arr_server_log(w, (4 - 1)) >> 8) & 7);
-            arr_put_server_log(w, (4 - 1), ((2 | (0 << 2)) | (l_ccmd128 << 8)));
+            const int l_ccmd307 = ((arr_server_log(w, (4 - 1)) >> 8) & 7);
+            arr_put_server_log(w, (4 - 1), ((2 | (0 << 2)) | (l_ccmd307 << 8)));
             arr_put_server_votes(w, (4 - 1), 0);
             if (((0 < p.servers) && (0 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd128) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd307) & 7) << 3));
             }
             if (((1 < p.servers) && (1 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd128) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd307) & 7) << 3));
             }
             if (((2 < p.servers) && (2 != (i - first_server(p))))) {
-              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd128) & 7) << 3));
+              out.send(((Rec)6 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((4) & 7) << 0) | ((Rec)((l_ccmd307) & 7) << 3));
             }
           }
         }
       }
-      put(w, 17, 3, (l_last124 + 1));
+      put(w, 17, 3, (l_last303 + 1));
     }
-    const int l_so0129 = get(w, 14, 3);
-    const int l_act130 = get(w, 6, 1);
-    int l_kv131 = 0;
-    int l_ls0132 = 0;
-    int l_ls1133 = 0;
-    int l_so134 = l_so0129;
-    int l_run135 = 1;
-    const int l_e136 = arr_server_log(w, 0);
-    const int l_cmd137 = ((l_e136 >> 8) & 7);
-    const int l_c138 = ((l_cmd137 >= 4) ? 1 : 0);
-    const int l_q139 = (l_cmd137 - (((l_cmd137 >= 4) ? 1 : 0) * 3));
-    const int l_before140 = (1 < l_so0129);
-    const int l_now141 = (((!l_before140) && (l_run135 != 0)) && ((l_e136 & 3) == 2));
-    l_run135 = (((l_run135 != 0) && (l_before140 || l_now141)) ? 1 : 0);
-    if ((((l_before140 || l_now141) && (l_cmd137 != 0)) && ((l_c138 ? l_ls1133 : l_ls0132) < l_q139))) {
-      const int l_c142 = ((l_cmd137 >= 4) ? 1 : 0);
-      const int l_op143 = (int)((p.op_pk >> ((2 * ((l_c142) * 3 + (((l_cmd137 - (((l_cmd137 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v144 = (int)((p.val_pk >> ((2 * ((l_c142) * 3 + (((l_cmd137 - (((l_cmd137 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x145 = 0;
-      if ((l_op143 == 1)) {
-        l_kv131 = (1 | (l_v144 << 3));
-        l_x145 = 7;
+    const int l_so0308 = get(w, 14, 3);
+    const int l_act309 = get(w, 6, 1);
+    int l_kv310 = 0;
+    int l_ls0311 = 0;
+    int l_ls1312 = 0;
+    int l_so313 = l_so0308;
+    int l_run314 = 1;
+    const int l_e315 = arr_server_log(w, 0);
+    const int l_cmd316 = ((l_e315 >> 8) & 7);
+    const int l_c317 = ((l_cmd316 >= 4) ? 1 : 0);
+    const int l_q318 = (l_cmd316 - (((l_cmd316 >= 4) ? 1 : 0) * 3));
+    const int l_before319 = (1 < l_so0308);
+    const int l_now320 = (((!l_before319) && (l_run314 != 0)) && ((l_e315 & 3) == 2));
+    l_run314 = (((l_run314 != 0) && (l_before319 || l_now320)) ? 1 : 0);
+    if ((((l_before319 || l_now320) && (l_cmd316 != 0)) && ((l_c317 ? l_ls1312 : l_ls0311) < l_q318))) {
+      const int l_c321 = ((l_cmd316 >= 4) ? 1 : 0);
+      const int l_op322 = (int)((p.op_pk >> ((2 * ((l_c321) * 3 + (((l_cmd316 - (((l_cmd316 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v323 = (int)((p.val_pk >> ((2 * ((l_c321) * 3 + (((l_cmd316 - (((l_cmd316 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x324 = 0;
+      if ((l_op322 == 1)) {
+        l_kv310 = (1 | (l_v323 << 3));
+        l_x324 = 7;
       }
-      if ((l_op143 == 2)) {
-        const int l_len146 = (l_kv131 & 7);
-        l_kv131 = (((l_len146 + 1) | (l_kv131 & -8)) | (l_v144 << (3 + (l_len146 * 2))));
-        l_x145 = l_kv131;
+      if ((l_op322 == 2)) {
+        const int l_len325 = (l_kv310 & 7);
+        l_kv310 = (((l_len325 + 1) | (l_kv310 & -8)) | (l_v323 << (3 + (l_len325 * 2))));
+        l_x324 = l_kv310;
       }
-      if ((l_op143 == 3)) {
-        l_x145 = (((l_kv131 & 7) != 0) ? l_kv131 : 6);
+      if ((l_op322 == 3)) {
+        l_x324 = (((l_kv310 & 7) != 0) ? l_kv310 : 6);
       }
-      if ((l_c138 != 0)) {
-        l_ls1133 = l_q139;
+      if ((l_c317 != 0)) {
+        l_ls1312 = l_q318;
       } else {
-        l_ls0132 = l_q139;
+        l_ls0311 = l_q318;
       }
-      if ((l_now141 && (l_act130 != 0))) {
-        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c138 + 1) - 1)) << 55) | ((Rec)((l_q139) & 3) << 0) | ((Rec)((l_x145) & 4095) << 2));
+      if ((l_now320 && (l_act309 != 0))) {
+        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c317 + 1) - 1)) << 55) | ((Rec)((l_q318) & 3) << 0) | ((Rec)((l_x324) & 4095) << 2));
       }
     }
-    if (l_now141) {
-      l_so134 = 2;
+    if (l_now320) {
+      l_so313 = 2;
     }
-    const int l_e147 = arr_server_log(w, 1);
-    const int l_cmd148 = ((l_e147 >> 8) & 7);
-    const int l_c149 = ((l_cmd148 >= 4) ? 1 : 0);
-    const int l_q150 = (l_cmd148 - (((l_cmd148 >= 4) ? 1 : 0) * 3));
-    const int l_before151 = (2 < l_so0129);
-    const int l_now152 = (((!l_before151) && (l_run135 != 0)) && ((l_e147 & 3) == 2));
-    l_run135 = (((l_run135 != 0) && (l_before151 || l_now152)) ? 1 : 0);
-    if ((((l_before151 || l_now152) && (l_cmd148 != 0)) && ((l_c149 ? l_ls1133 : l_ls0132) < l_q150))) {
-      const int l_c153 = ((l_cmd148 >= 4) ? 1 : 0);
-      const int l_op154 = (int)((p.op_pk >> ((2 * ((l_c153) * 3 + (((l_cmd148 - (((l_cmd148 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v155 = (int)((p.val_pk >> ((2 * ((l_c153) * 3 + (((l_cmd148 - (((l_cmd148 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x156 = 0;
-      if ((l_op154 == 1)) {
-        l_kv131 = (1 | (l_v155 << 3));
-        l_x156 = 7;
+    const int l_e326 = arr_server_log(w, 1);
+    const int l_cmd327 = ((l_e326 >> 8) & 7);
+    const int l_c328 = ((l_cmd327 >= 4) ? 1 : 0);
+    const int l_q329 = (l_cmd327 - (((l_cmd327 >= 4) ? 1 : 0) * 3));
+    const int l_before330 = (2 < l_so0308);
+    const int l_now331 = (((!l_before330) && (l_run314 != 0)) && ((l_e326 & 3) == 2));
+    l_run314 = (((l_run314 != 0) && (l_before330 || l_now331)) ? 1 : 0);
+    if ((((l_before330 || l_now331) && (l_cmd327 != 0)) && ((l_c328 ? l_ls1312 : l_ls0311) < l_q329))) {
+      const int l_c332 = ((l_cmd327 >= 4) ? 1 : 0);
+      const int l_op333 = (int)((p.op_pk >> ((2 * ((l_c332) * 3 + (((l_cmd327 - (((l_cmd327 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v334 = (int)((p.val_pk >> ((2 * ((l_c332) * 3 + (((l_cmd327 - (((l_cmd327 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x335 = 0;
+      if ((l_op333 == 1)) {
+        l_kv310 = (1 | (l_v334 << 3));
+        l_x335 = 7;
       }
-      if ((l_op154 == 2)) {
-        const int l_len157 = (l_kv131 & 7);
-        l_kv131 = (((l_len157 + 1) | (l_kv131 & -8)) | (l_v155 << (3 + (l_len157 * 2))));
-        l_x156 = l_kv131;
+      if ((l_op333 == 2)) {
+        const int l_len336 = (l_kv310 & 7);
+        l_kv310 = (((l_len336 + 1) | (l_kv310 & -8)) | (l_v334 << (3 + (l_len336 * 2))));
+        l_x335 = l_kv310;
       }
-      if ((l_op154 == 3)) {
-        l_x156 = (((l_kv131 & 7) != 0) ? l_kv131 : 6);
+      if ((l_op333 == 3)) {
+        l_x335 = (((l_kv310 & 7) != 0) ? l_kv310 : 6);
       }
-      if ((l_c149 != 0)) {
-        l_ls1133 = l_q150;
+      if ((l_c328 != 0)) {
+        l_ls1312 = l_q329;
       } else {
-        l_ls0132 = l_q150;
+        l_ls0311 = l_q329;
       }
-      if ((l_now152 && (l_act130 != 0))) {
-        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c149 + 1) - 1)) << 55) | ((Rec)((l_q150) & 3) << 0) | ((Rec)((l_x156) & 4095) << 2));
+      if ((l_now331 && (l_act309 != 0))) {
+        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c328 + 1) - 1)) << 55) | ((Rec)((l_q329) & 3) << 0) | ((Rec)((l_x335) & 4095) << 2));
       }
     }
-    if (l_now152) {
-      l_so134 = 3;
+    if (l_now331) {
+      l_so313 = 3;
     }
-    const int l_e158 = arr_server_log(w, 2);
-    const int l_cmd159 = ((l_e158 >> 8) & 7);
-    const int l_c160 = ((l_cmd159 >= 4) ? 1 : 0);
-    const int l_q161 = (l_cmd159 - (((l_cmd159 >= 4) ? 1 : 0) * 3));
-    const int l_before162 = (3 < l_so0129);
-    const int l_now163 = (((!l_before162) && (l_run135 != 0)) && ((l_e158 & 3) == 2));
-    l_run135 = (((l_run135 != 0) && (l_before162 || l_now163)) ? 1 : 0);
-    if ((((l_before162 || l_now163) && (l_cmd159 != 0)) && ((l_c160 ? l_ls1133 : l_ls0132) < l_q161))) {
-      const int l_c164 = ((l_cmd159 >= 4) ? 1 : 0);
-      const int l_op165 = (int)((p.op_pk >> ((2 * ((l_c164) * 3 + (((l_cmd159 - (((l_cmd159 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v166 = (int)((p.val_pk >> ((2 * ((l_c164) * 3 + (((l_cmd159 - (((l_cmd159 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x167 = 0;
-      if ((l_op165 == 1)) {
-        l_kv131 = (1 | (l_v166 << 3));
-        l_x167 = 7;
+    const int l_e337 = arr_server_log(w, 2);
+    const int l_cmd338 = ((l_e337 >> 8) & 7);
+    const int l_c339 = ((l_cmd338 >= 4) ? 1 : 0);
+    const int l_q340 = (l_cmd338 - (((l_cmd338 >= 4) ? 1 : 0) * 3));
+    const int l_before341 = (3 < l_so0308);
+    const int l_now342 = (((!l_before341) && (l_run314 != 0)) && ((l_e337 & 3) == 2));
+    l_run314 = (((l_run314 != 0) && (l_before341 || l_now342)) ? 1 : 0);
+    if ((((l_before341 || l_now342) && (l_cmd338 != 0)) && ((l_c339 ? l_ls1312 : l_ls0311) < l_q340))) {
+      const int l_c343 = ((l_cmd338 >= 4) ? 1 : 0);
+      const int l_op344 = (int)((p.op_pk >> ((2 * ((l_c343) * 3 + (((l_cmd338 - (((l_cmd338 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v345 = (int)((p.val_pk >> ((2 * ((l_c343) * 3 + (((l_cmd338 - (((l_cmd338 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x346 = 0;
+      if ((l_op344 == 1)) {
+        l_kv310 = (1 | (l_v345 << 3));
+        l_x346 = 7;
       }
-      if ((l_op165 == 2)) {
-        const int l_len168 = (l_kv131 & 7);
-        l_kv131 = (((l_len168 + 1) | (l_kv131 & -8)) | (l_v166 << (3 + (l_len168 * 2))));
-        l_x167 = l_kv131;
+      if ((l_op344 == 2)) {
+        const int l_len347 = (l_kv310 & 7);
+        l_kv310 = (((l_len347 + 1) | (l_kv310 & -8)) | (l_v345 << (3 + (l_len347 * 2))));
+        l_x346 = l_kv310;
       }
-      if ((l_op165 == 3)) {
-        l_x167 = (((l_kv131 & 7) != 0) ? l_kv131 : 6);
+      if ((l_op344 == 3)) {
+        l_x346 = (((l_kv310 & 7) != 0) ? l_kv310 : 6);
       }
-      if ((l_c160 != 0)) {
-        l_ls1133 = l_q161;
+      if ((l_c339 != 0)) {
+        l_ls1312 = l_q340;
       } else {
-        l_ls0132 = l_q161;
+        l_ls0311 = l_q340;
       }
-      if ((l_now163 && (l_act130 != 0))) {
-        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c160 + 1) - 1)) << 55) | ((Rec)((l_q161) & 3) << 0) | ((Rec)((l_x167) & 4095) << 2));
+      if ((l_now342 && (l_act309 != 0))) {
+        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c339 + 1) - 1)) << 55) | ((Rec)((l_q340) & 3) << 0) | ((Rec)((l_x346) & 4095) << 2));
       }
     }
-    if (l_now163) {
-      l_so134 = 4;
+    if (l_now342) {
+      l_so313 = 4;
     }
-    const int l_e169 = arr_server_log(w, 3);
-    const int l_cmd170 = ((l_e169 >> 8) & 7);
-    const int l_c171 = ((l_cmd170 >= 4) ? 1 : 0);
-    const int l_q172 = (l_cmd170 - (((l_cmd170 >= 4) ? 1 : 0) * 3));
-    const int l_before173 = (4 < l_so0129);
-    const int l_now174 = (((!l_before173) && (l_run135 != 0)) && ((l_e169 & 3) == 2));
-    l_run135 = (((l_run135 != 0) && (l_before173 || l_now174)) ? 1 : 0);
-    if ((((l_before173 || l_now174) && (l_cmd170 != 0)) && ((l_c171 ? l_ls1133 : l_ls0132) < l_q172))) {
-      const int l_c175 = ((l_cmd170 >= 4) ? 1 : 0);
-      const int l_op176 = (int)((p.op_pk >> ((2 * ((l_c175) * 3 + (((l_cmd170 - (((l_cmd170 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      const int l_v177 = (int)((p.val_pk >> ((2 * ((l_c175) * 3 + (((l_cmd170 - (((l_cmd170 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
-      int l_x178 = 0;
-      if ((l_op176 == 1)) {
-        l_kv131 = (1 | (l_v177 << 3));
-        l_x178 = 7;
+    const int l_e348 = arr_server_log(w, 3);
+    const int l_cmd349 = ((l_e348 >> 8) & 7);
+    const int l_c350 = ((l_cmd349 >= 4) ? 1 : 0);
+    const int l_q351 = (l_cmd349 - (((l_cmd349 >= 4) ? 1 : 0) * 3));
+    const int l_before352 = (4 < l_so0308);
+    const int l_now353 = (((!l_before352) && (l_run314 != 0)) && ((l_e348 & 3) == 2));
+    l_run314 = (((l_run314 != 0) && (l_before352 || l_now353)) ? 1 : 0);
+    if ((((l_before352 || l_now353) && (l_cmd349 != 0)) && ((l_c350 ? l_ls1312 : l_ls0311) < l_q351))) {
+      const int l_c354 = ((l_cmd349 >= 4) ? 1 : 0);
+      const int l_op355 = (int)((p.op_pk >> ((2 * ((l_c354) * 3 + (((l_cmd349 - (((l_cmd349 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      const int l_v356 = (int)((p.val_pk >> ((2 * ((l_c354) * 3 + (((l_cmd349 - (((l_cmd349 >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u);
+      int l_x357 = 0;
+      if ((l_op355 == 1)) {
+        l_kv310 = (1 | (l_v356 << 3));
+        l_x357 = 7;
       }
-      if ((l_op176 == 2)) {
-        const int l_len179 = (l_kv131 & 7);
-        l_kv131 = (((l_len179 + 1) | (l_kv131 & -8)) | (l_v177 << (3 + (l_len179 * 2))));
-        l_x178 = l_kv131;
+      if ((l_op355 == 2)) {
+        const int l_len358 = (l_kv310 & 7);
+        l_kv310 = (((l_len358 + 1) | (l_kv310 & -8)) | (l_v356 << (3 + (l_len358 * 2))));
+        l_x357 = l_kv310;
       }
-      if ((l_op176 == 3)) {
-        l_x178 = (((l_kv131 & 7) != 0) ? l_kv131 : 6);
+      if ((l_op355 == 3)) {
+        l_x357 = (((l_kv310 & 7) != 0) ? l_kv310 : 6);
       }
-      if ((l_c171 != 0)) {
-        l_ls1133 = l_q172;
+      if ((l_c350 != 0)) {
+        l_ls1312 = l_q351;
       } else {
-        l_ls0132 = l_q172;
+        l_ls0311 = l_q351;
       }
-      if ((l_now174 && (l_act130 != 0))) {
-        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c171 + 1) - 1)) << 55) | ((Rec)((l_q172) & 3) << 0) | ((Rec)((l_x178) & 4095) << 2));
+      if ((l_now353 && (l_act309 != 0))) {
+        out.send(((Rec)1 << 61) | ((Rec)(i) << 58) | ((Rec)((first_client(p) + (l_c350 + 1) - 1)) << 55) | ((Rec)((l_q351) & 3) << 0) | ((Rec)((l_x357) & 4095) << 2));
       }
     }
-    if (l_now174) {
-      l_so134 = 5;
+    if (l_now353) {
+      l_so313 = 5;
     }
-    put(w, 14, 3, l_so134);
+    put(w, 14, 3, l_so313);
     return STEP_OK;
   }
   template <class O>
@@ -1327,15 +1284,15 @@ struct MultiPaxosIR {
     (void)i; (void)w; (void)out; (void)p;
     const int tf_seq = (e >> 0) & 3;
     if (((get(w, 2, 1) != 0) && (tf_seq == get(w, 0, 2)))) {
-      const int l_cid180 = (((i - first_client(p)) * 3) + tf_seq);
+      const int l_cid359 = (((i - first_client(p)) * 3) + tf_seq);
       if ((0 < p.servers)) {
-        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_cid180) & 7) << 0));
+        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 1 - 1)) << 55) | ((Rec)((l_cid359) & 7) << 0));
       }
       if ((1 < p.servers)) {
-        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_cid180) & 7) << 0));
+        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 2 - 1)) << 55) | ((Rec)((l_cid359) & 7) << 0));
       }
       if ((2 < p.servers)) {
-        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_cid180) & 7) << 0));
+        out.send(((Rec)0 << 61) | ((Rec)(i) << 58) | ((Rec)((first_server(p) + 3 - 1)) << 55) | ((Rec)((l_cid359) & 7) << 0));
       }
       if (!push_timer_client(w, (((tf_seq) & 3) << 0) | (1 << 2))) return STEP_OVERFLOW;
     }
@@ -1370,16 +1327,8 @@ struct MultiPaxosIR {
   static DSL_HD int on_timer(int i, uint32_t* w, int j, O& out, const Params& p) {
     (void)w; (void)j; (void)out;
     if (is_server(i, p)) {
-      const int q = deliverable_server(w, j);
-      if (q < 0) return STEP_NULL;
-      const int e = arr_server__timers(w, q);
-      if (ttype(e) == 0) {  // Tick
-        const int rc = ht_server_Tick(i, w, e, out, p);
-        if (rc != STEP_OK) return rc;
-        remove_timer_server(w, e);  // SearchState.stepTimer: the first equal entry
-        return STEP_OK;
-      }
-      return STEP_EXCEPTION;  // no handler for this timer
+      if (j != 0) return STEP_NULL;
+      return ht_server_Tick(i, w, (0 << 2), out, p);  // Tick
     }
     if (is_client(i, p)) {
       const int q = deliverable_client(w, j);
@@ -1426,236 +1375,245 @@ struct MultiPaxosIR {
       case 400:  // LOGS_CONSISTENT_ALL_SLOTS / LOGS_CONSISTENT
       case 401:  // LOGS_CONSISTENT_ALL_SLOTS / LOGS_CONSISTENT
       {
-        int l_isch181 = 0;
-        int l_confl182 = 0;
-        int l_chosen183 = 0;
-        int l_count184 = 0;
+        uint32_t pn_server_0[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 0);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_0[w_] = q_[w_]; }
+        uint32_t pn_server_1[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 1);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_1[w_] = q_[w_]; }
+        uint32_t pn_server_2[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 2);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_2[w_] = q_[w_]; }
+        int l_isch360 = 0;
+        int l_confl361 = 0;
+        int l_chosen362 = 0;
+        int l_count363 = 0;
         if ((0 < p.servers)) {
-          const int l_e185 = arr_server_log(v.node(first_server(p) + 0), 0);
-          if (((l_e185 & 3) == 2)) {
-            const int l_x186 = ((((l_e185 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e185 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e185 >> 8) & 7) - (((((l_e185 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e185 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e185 >> 8) & 7) - (((((l_e185 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch181 != 0) && (l_x186 != l_chosen183))) {
-              l_confl182 = 1;
+          const int l_e364 = arr_server_log(pn_server_0, 0);
+          if (((l_e364 & 3) == 2)) {
+            const int l_x365 = ((((l_e364 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e364 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e364 >> 8) & 7) - (((((l_e364 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e364 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e364 >> 8) & 7) - (((((l_e364 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch360 != 0) && (l_x365 != l_chosen362))) {
+              l_confl361 = 1;
             }
-            l_chosen183 = l_x186;
-            l_isch181 = 1;
+            l_chosen362 = l_x365;
+            l_isch360 = 1;
           }
         }
         if ((1 < p.servers)) {
-          const int l_e187 = arr_server_log(v.node(first_server(p) + 1), 0);
-          if (((l_e187 & 3) == 2)) {
-            const int l_x188 = ((((l_e187 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e187 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e187 >> 8) & 7) - (((((l_e187 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e187 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e187 >> 8) & 7) - (((((l_e187 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch181 != 0) && (l_x188 != l_chosen183))) {
-              l_confl182 = 1;
+          const int l_e366 = arr_server_log(pn_server_1, 0);
+          if (((l_e366 & 3) == 2)) {
+            const int l_x367 = ((((l_e366 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e366 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e366 >> 8) & 7) - (((((l_e366 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e366 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e366 >> 8) & 7) - (((((l_e366 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch360 != 0) && (l_x367 != l_chosen362))) {
+              l_confl361 = 1;
             }
-            l_chosen183 = l_x188;
-            l_isch181 = 1;
+            l_chosen362 = l_x367;
+            l_isch360 = 1;
           }
         }
         if ((2 < p.servers)) {
-          const int l_e189 = arr_server_log(v.node(first_server(p) + 2), 0);
-          if (((l_e189 & 3) == 2)) {
-            const int l_x190 = ((((l_e189 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e189 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e189 >> 8) & 7) - (((((l_e189 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e189 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e189 >> 8) & 7) - (((((l_e189 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch181 != 0) && (l_x190 != l_chosen183))) {
-              l_confl182 = 1;
+          const int l_e368 = arr_server_log(pn_server_2, 0);
+          if (((l_e368 & 3) == 2)) {
+            const int l_x369 = ((((l_e368 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e368 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e368 >> 8) & 7) - (((((l_e368 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e368 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e368 >> 8) & 7) - (((((l_e368 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch360 != 0) && (l_x369 != l_chosen362))) {
+              l_confl361 = 1;
             }
-            l_chosen183 = l_x190;
-            l_isch181 = 1;
+            l_chosen362 = l_x369;
+            l_isch360 = 1;
           }
         }
         if ((0 < p.servers)) {
-          const int l_e191 = arr_server_log(v.node(first_server(p) + 0), 0);
-          if ((((l_e191 & 3) != 0) && (((l_e191 & 3) != 1) || (((((l_e191 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e191 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e191 >> 8) & 7) - (((((l_e191 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e191 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e191 >> 8) & 7) - (((((l_e191 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen183)))) {
-            l_count184 = (l_count184 + 1);
+          const int l_e370 = arr_server_log(pn_server_0, 0);
+          if ((((l_e370 & 3) != 0) && (((l_e370 & 3) != 1) || (((((l_e370 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e370 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e370 >> 8) & 7) - (((((l_e370 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e370 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e370 >> 8) & 7) - (((((l_e370 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen362)))) {
+            l_count363 = (l_count363 + 1);
           }
         }
         if ((1 < p.servers)) {
-          const int l_e192 = arr_server_log(v.node(first_server(p) + 1), 0);
-          if ((((l_e192 & 3) != 0) && (((l_e192 & 3) != 1) || (((((l_e192 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e192 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e192 >> 8) & 7) - (((((l_e192 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e192 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e192 >> 8) & 7) - (((((l_e192 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen183)))) {
-            l_count184 = (l_count184 + 1);
+          const int l_e371 = arr_server_log(pn_server_1, 0);
+          if ((((l_e371 & 3) != 0) && (((l_e371 & 3) != 1) || (((((l_e371 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e371 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e371 >> 8) & 7) - (((((l_e371 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e371 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e371 >> 8) & 7) - (((((l_e371 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen362)))) {
+            l_count363 = (l_count363 + 1);
           }
         }
         if ((2 < p.servers)) {
-          const int l_e193 = arr_server_log(v.node(first_server(p) + 2), 0);
-          if ((((l_e193 & 3) != 0) && (((l_e193 & 3) != 1) || (((((l_e193 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e193 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e193 >> 8) & 7) - (((((l_e193 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e193 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e193 >> 8) & 7) - (((((l_e193 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen183)))) {
-            l_count184 = (l_count184 + 1);
+          const int l_e372 = arr_server_log(pn_server_2, 0);
+          if ((((l_e372 & 3) != 0) && (((l_e372 & 3) != 1) || (((((l_e372 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e372 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e372 >> 8) & 7) - (((((l_e372 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e372 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e372 >> 8) & 7) - (((((l_e372 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen362)))) {
+            l_count363 = (l_count363 + 1);
           }
         }
-        if (((l_isch181 != 0) && ((l_confl182 != 0) || ((l_count184 * 2) <= p.servers)))) {
+        if (((l_isch360 != 0) && ((l_confl361 != 0) || ((l_count363 * 2) <= p.servers)))) {
           return PV_FALSE;
         }
-        int l_isch194 = 0;
-        int l_confl195 = 0;
-        int l_chosen196 = 0;
-        int l_count197 = 0;
+        int l_isch373 = 0;
+        int l_confl374 = 0;
+        int l_chosen375 = 0;
+        int l_count376 = 0;
         if ((0 < p.servers)) {
-          const int l_e198 = arr_server_log(v.node(first_server(p) + 0), 1);
-          if (((l_e198 & 3) == 2)) {
-            const int l_x199 = ((((l_e198 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e198 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e198 >> 8) & 7) - (((((l_e198 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e198 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e198 >> 8) & 7) - (((((l_e198 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch194 != 0) && (l_x199 != l_chosen196))) {
-              l_confl195 = 1;
+          const int l_e377 = arr_server_log(pn_server_0, 1);
+          if (((l_e377 & 3) == 2)) {
+            const int l_x378 = ((((l_e377 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e377 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e377 >> 8) & 7) - (((((l_e377 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e377 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e377 >> 8) & 7) - (((((l_e377 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch373 != 0) && (l_x378 != l_chosen375))) {
+              l_confl374 = 1;
             }
-            l_chosen196 = l_x199;
-            l_isch194 = 1;
+            l_chosen375 = l_x378;
+            l_isch373 = 1;
           }
         }
         if ((1 < p.servers)) {
-          const int l_e200 = arr_server_log(v.node(first_server(p) + 1), 1);
-          if (((l_e200 & 3) == 2)) {
-            const int l_x201 = ((((l_e200 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e200 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e200 >> 8) & 7) - (((((l_e200 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e200 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e200 >> 8) & 7) - (((((l_e200 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch194 != 0) && (l_x201 != l_chosen196))) {
-              l_confl195 = 1;
+          const int l_e379 = arr_server_log(pn_server_1, 1);
+          if (((l_e379 & 3) == 2)) {
+            const int l_x380 = ((((l_e379 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e379 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e379 >> 8) & 7) - (((((l_e379 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e379 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e379 >> 8) & 7) - (((((l_e379 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch373 != 0) && (l_x380 != l_chosen375))) {
+              l_confl374 = 1;
             }
-            l_chosen196 = l_x201;
-            l_isch194 = 1;
+            l_chosen375 = l_x380;
+            l_isch373 = 1;
           }
         }
         if ((2 < p.servers)) {
-          const int l_e202 = arr_server_log(v.node(first_server(p) + 2), 1);
-          if (((l_e202 & 3) == 2)) {
-            const int l_x203 = ((((l_e202 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e202 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e202 >> 8) & 7) - (((((l_e202 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e202 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e202 >> 8) & 7) - (((((l_e202 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch194 != 0) && (l_x203 != l_chosen196))) {
-              l_confl195 = 1;
+          const int l_e381 = arr_server_log(pn_server_2, 1);
+          if (((l_e381 & 3) == 2)) {
+            const int l_x382 = ((((l_e381 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e381 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e381 >> 8) & 7) - (((((l_e381 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e381 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e381 >> 8) & 7) - (((((l_e381 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch373 != 0) && (l_x382 != l_chosen375))) {
+              l_confl374 = 1;
             }
-            l_chosen196 = l_x203;
-            l_isch194 = 1;
+            l_chosen375 = l_x382;
+            l_isch373 = 1;
           }
         }
         if ((0 < p.servers)) {
-          const int l_e204 = arr_server_log(v.node(first_server(p) + 0), 1);
-          if ((((l_e204 & 3) != 0) && (((l_e204 & 3) != 1) || (((((l_e204 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e204 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e204 >> 8) & 7) - (((((l_e204 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e204 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e204 >> 8) & 7) - (((((l_e204 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen196)))) {
-            l_count197 = (l_count197 + 1);
+          const int l_e383 = arr_server_log(pn_server_0, 1);
+          if ((((l_e383 & 3) != 0) && (((l_e383 & 3) != 1) || (((((l_e383 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e383 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e383 >> 8) & 7) - (((((l_e383 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e383 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e383 >> 8) & 7) - (((((l_e383 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen375)))) {
+            l_count376 = (l_count376 + 1);
           }
         }
         if ((1 < p.servers)) {
-          const int l_e205 = arr_server_log(v.node(first_server(p) + 1), 1);
-          if ((((l_e205 & 3) != 0) && (((l_e205 & 3) != 1) || (((((l_e205 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e205 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e205 >> 8) & 7) - (((((l_e205 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e205 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e205 >> 8) & 7) - (((((l_e205 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen196)))) {
-            l_count197 = (l_count197 + 1);
+          const int l_e384 = arr_server_log(pn_server_1, 1);
+          if ((((l_e384 & 3) != 0) && (((l_e384 & 3) != 1) || (((((l_e384 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e384 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e384 >> 8) & 7) - (((((l_e384 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e384 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e384 >> 8) & 7) - (((((l_e384 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen375)))) {
+            l_count376 = (l_count376 + 1);
           }
         }
         if ((2 < p.servers)) {
-          const int l_e206 = arr_server_log(v.node(first_server(p) + 2), 1);
-          if ((((l_e206 & 3) != 0) && (((l_e206 & 3) != 1) || (((((l_e206 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e206 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e206 >> 8) & 7) - (((((l_e206 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e206 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e206 >> 8) & 7) - (((((l_e206 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen196)))) {
-            l_count197 = (l_count197 + 1);
+          const int l_e385 = arr_server_log(pn_server_2, 1);
+          if ((((l_e385 & 3) != 0) && (((l_e385 & 3) != 1) || (((((l_e385 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e385 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e385 >> 8) & 7) - (((((l_e385 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e385 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e385 >> 8) & 7) - (((((l_e385 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen375)))) {
+            l_count376 = (l_count376 + 1);
           }
         }
-        if (((l_isch194 != 0) && ((l_confl195 != 0) || ((l_count197 * 2) <= p.servers)))) {
+        if (((l_isch373 != 0) && ((l_confl374 != 0) || ((l_count376 * 2) <= p.servers)))) {
           return PV_FALSE;
         }
-        int l_isch207 = 0;
-        int l_confl208 = 0;
-        int l_chosen209 = 0;
-        int l_count210 = 0;
+        int l_isch386 = 0;
+        int l_confl387 = 0;
+        int l_chosen388 = 0;
+        int l_count389 = 0;
         if ((0 < p.servers)) {
-          const int l_e211 = arr_server_log(v.node(first_server(p) + 0), 2);
-          if (((l_e211 & 3) == 2)) {
-            const int l_x212 = ((((l_e211 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e211 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e211 >> 8) & 7) - (((((l_e211 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e211 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e211 >> 8) & 7) - (((((l_e211 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch207 != 0) && (l_x212 != l_chosen209))) {
-              l_confl208 = 1;
+          const int l_e390 = arr_server_log(pn_server_0, 2);
+          if (((l_e390 & 3) == 2)) {
+            const int l_x391 = ((((l_e390 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e390 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e390 >> 8) & 7) - (((((l_e390 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e390 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e390 >> 8) & 7) - (((((l_e390 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch386 != 0) && (l_x391 != l_chosen388))) {
+              l_confl387 = 1;
             }
-            l_chosen209 = l_x212;
-            l_isch207 = 1;
+            l_chosen388 = l_x391;
+            l_isch386 = 1;
           }
         }
         if ((1 < p.servers)) {
-          const int l_e213 = arr_server_log(v.node(first_server(p) + 1), 2);
-          if (((l_e213 & 3) == 2)) {
-            const int l_x214 = ((((l_e213 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e213 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e213 >> 8) & 7) - (((((l_e213 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e213 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e213 >> 8) & 7) - (((((l_e213 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch207 != 0) && (l_x214 != l_chosen209))) {
-              l_confl208 = 1;
+          const int l_e392 = arr_server_log(pn_server_1, 2);
+          if (((l_e392 & 3) == 2)) {
+            const int l_x393 = ((((l_e392 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e392 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e392 >> 8) & 7) - (((((l_e392 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e392 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e392 >> 8) & 7) - (((((l_e392 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch386 != 0) && (l_x393 != l_chosen388))) {
+              l_confl387 = 1;
             }
-            l_chosen209 = l_x214;
-            l_isch207 = 1;
+            l_chosen388 = l_x393;
+            l_isch386 = 1;
           }
         }
         if ((2 < p.servers)) {
-          const int l_e215 = arr_server_log(v.node(first_server(p) + 2), 2);
-          if (((l_e215 & 3) == 2)) {
-            const int l_x216 = ((((l_e215 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e215 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e215 >> 8) & 7) - (((((l_e215 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e215 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e215 >> 8) & 7) - (((((l_e215 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch207 != 0) && (l_x216 != l_chosen209))) {
-              l_confl208 = 1;
+          const int l_e394 = arr_server_log(pn_server_2, 2);
+          if (((l_e394 & 3) == 2)) {
+            const int l_x395 = ((((l_e394 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e394 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e394 >> 8) & 7) - (((((l_e394 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e394 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e394 >> 8) & 7) - (((((l_e394 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch386 != 0) && (l_x395 != l_chosen388))) {
+              l_confl387 = 1;
             }
-            l_chosen209 = l_x216;
-            l_isch207 = 1;
+            l_chosen388 = l_x395;
+            l_isch386 = 1;
           }
         }
         if ((0 < p.servers)) {
-          const int l_e217 = arr_server_log(v.node(first_server(p) + 0), 2);
-          if ((((l_e217 & 3) != 0) && (((l_e217 & 3) != 1) || (((((l_e217 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e217 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e217 >> 8) & 7) - (((((l_e217 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e217 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e217 >> 8) & 7) - (((((l_e217 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen209)))) {
-            l_count210 = (l_count210 + 1);
+          const int l_e396 = arr_server_log(pn_server_0, 2);
+          if ((((l_e396 & 3) != 0) && (((l_e396 & 3) != 1) || (((((l_e396 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e396 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e396 >> 8) & 7) - (((((l_e396 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e396 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e396 >> 8) & 7) - (((((l_e396 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen388)))) {
+            l_count389 = (l_count389 + 1);
           }
         }
         if ((1 < p.servers)) {
-          const int l_e218 = arr_server_log(v.node(first_server(p) + 1), 2);
-          if ((((l_e218 & 3) != 0) && (((l_e218 & 3) != 1) || (((((l_e218 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e218 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e218 >> 8) & 7) - (((((l_e218 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e218 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e218 >> 8) & 7) - (((((l_e218 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen209)))) {
-            l_count210 = (l_count210 + 1);
+          const int l_e397 = arr_server_log(pn_server_1, 2);
+          if ((((l_e397 & 3) != 0) && (((l_e397 & 3) != 1) || (((((l_e397 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e397 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e397 >> 8) & 7) - (((((l_e397 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e397 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e397 >> 8) & 7) - (((((l_e397 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen388)))) {
+            l_count389 = (l_count389 + 1);
           }
         }
         if ((2 < p.servers)) {
-          const int l_e219 = arr_server_log(v.node(first_server(p) + 2), 2);
-          if ((((l_e219 & 3) != 0) && (((l_e219 & 3) != 1) || (((((l_e219 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e219 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e219 >> 8) & 7) - (((((l_e219 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e219 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e219 >> 8) & 7) - (((((l_e219 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen209)))) {
-            l_count210 = (l_count210 + 1);
+          const int l_e398 = arr_server_log(pn_server_2, 2);
+          if ((((l_e398 & 3) != 0) && (((l_e398 & 3) != 1) || (((((l_e398 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e398 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e398 >> 8) & 7) - (((((l_e398 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e398 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e398 >> 8) & 7) - (((((l_e398 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen388)))) {
+            l_count389 = (l_count389 + 1);
           }
         }
-        if (((l_isch207 != 0) && ((l_confl208 != 0) || ((l_count210 * 2) <= p.servers)))) {
+        if (((l_isch386 != 0) && ((l_confl387 != 0) || ((l_count389 * 2) <= p.servers)))) {
           return PV_FALSE;
         }
-        int l_isch220 = 0;
-        int l_confl221 = 0;
-        int l_chosen222 = 0;
-        int l_count223 = 0;
+        int l_isch399 = 0;
+        int l_confl400 = 0;
+        int l_chosen401 = 0;
+        int l_count402 = 0;
         if ((0 < p.servers)) {
-          const int l_e224 = arr_server_log(v.node(first_server(p) + 0), 3);
-          if (((l_e224 & 3) == 2)) {
-            const int l_x225 = ((((l_e224 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e224 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e224 >> 8) & 7) - (((((l_e224 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e224 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e224 >> 8) & 7) - (((((l_e224 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch220 != 0) && (l_x225 != l_chosen222))) {
-              l_confl221 = 1;
+          const int l_e403 = arr_server_log(pn_server_0, 3);
+          if (((l_e403 & 3) == 2)) {
+            const int l_x404 = ((((l_e403 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e403 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e403 >> 8) & 7) - (((((l_e403 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e403 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e403 >> 8) & 7) - (((((l_e403 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch399 != 0) && (l_x404 != l_chosen401))) {
+              l_confl400 = 1;
             }
-            l_chosen222 = l_x225;
-            l_isch220 = 1;
+            l_chosen401 = l_x404;
+            l_isch399 = 1;
           }
         }
         if ((1 < p.servers)) {
-          const int l_e226 = arr_server_log(v.node(first_server(p) + 1), 3);
-          if (((l_e226 & 3) == 2)) {
-            const int l_x227 = ((((l_e226 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e226 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e226 >> 8) & 7) - (((((l_e226 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e226 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e226 >> 8) & 7) - (((((l_e226 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch220 != 0) && (l_x227 != l_chosen222))) {
-              l_confl221 = 1;
+          const int l_e405 = arr_server_log(pn_server_1, 3);
+          if (((l_e405 & 3) == 2)) {
+            const int l_x406 = ((((l_e405 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e405 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e405 >> 8) & 7) - (((((l_e405 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e405 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e405 >> 8) & 7) - (((((l_e405 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch399 != 0) && (l_x406 != l_chosen401))) {
+              l_confl400 = 1;
             }
-            l_chosen222 = l_x227;
-            l_isch220 = 1;
+            l_chosen401 = l_x406;
+            l_isch399 = 1;
           }
         }
         if ((2 < p.servers)) {
-          const int l_e228 = arr_server_log(v.node(first_server(p) + 2), 3);
-          if (((l_e228 & 3) == 2)) {
-            const int l_x229 = ((((l_e228 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e228 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e228 >> 8) & 7) - (((((l_e228 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e228 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e228 >> 8) & 7) - (((((l_e228 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch220 != 0) && (l_x229 != l_chosen222))) {
-              l_confl221 = 1;
+          const int l_e407 = arr_server_log(pn_server_2, 3);
+          if (((l_e407 & 3) == 2)) {
+            const int l_x408 = ((((l_e407 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e407 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e407 >> 8) & 7) - (((((l_e407 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e407 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e407 >> 8) & 7) - (((((l_e407 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch399 != 0) && (l_x408 != l_chosen401))) {
+              l_confl400 = 1;
             }
-            l_chosen222 = l_x229;
-            l_isch220 = 1;
+            l_chosen401 = l_x408;
+            l_isch399 = 1;
           }
         }
         if ((0 < p.servers)) {
-          const int l_e230 = arr_server_log(v.node(first_server(p) + 0), 3);
-          if ((((l_e230 & 3) != 0) && (((l_e230 & 3) != 1) || (((((l_e230 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e230 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e230 >> 8) & 7) - (((((l_e230 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e230 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e230 >> 8) & 7) - (((((l_e230 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen222)))) {
-            l_count223 = (l_count223 + 1);
+          const int l_e409 = arr_server_log(pn_server_0, 3);
+          if ((((l_e409 & 3) != 0) && (((l_e409 & 3) != 1) || (((((l_e409 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e409 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e409 >> 8) & 7) - (((((l_e409 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e409 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e409 >> 8) & 7) - (((((l_e409 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen401)))) {
+            l_count402 = (l_count402 + 1);
           }
         }
         if ((1 < p.servers)) {
-          const int l_e231 = arr_server_log(v.node(first_server(p) + 1), 3);
-          if ((((l_e231 & 3) != 0) && (((l_e231 & 3) != 1) || (((((l_e231 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e231 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e231 >> 8) & 7) - (((((l_e231 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e231 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e231 >> 8) & 7) - (((((l_e231 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen222)))) {
-            l_count223 = (l_count223 + 1);
+          const int l_e410 = arr_server_log(pn_server_1, 3);
+          if ((((l_e410 & 3) != 0) && (((l_e410 & 3) != 1) || (((((l_e410 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e410 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e410 >> 8) & 7) - (((((l_e410 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e410 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e410 >> 8) & 7) - (((((l_e410 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen401)))) {
+            l_count402 = (l_count402 + 1);
           }
         }
         if ((2 < p.servers)) {
-          const int l_e232 = arr_server_log(v.node(first_server(p) + 2), 3);
-          if ((((l_e232 & 3) != 0) && (((l_e232 & 3) != 1) || (((((l_e232 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e232 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e232 >> 8) & 7) - (((((l_e232 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e232 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e232 >> 8) & 7) - (((((l_e232 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen222)))) {
-            l_count223 = (l_count223 + 1);
+          const int l_e411 = arr_server_log(pn_server_2, 3);
+          if ((((l_e411 & 3) != 0) && (((l_e411 & 3) != 1) || (((((l_e411 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e411 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e411 >> 8) & 7) - (((((l_e411 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e411 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e411 >> 8) & 7) - (((((l_e411 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen401)))) {
+            l_count402 = (l_count402 + 1);
           }
         }
-        if (((l_isch220 != 0) && ((l_confl221 != 0) || ((l_count223 * 2) <= p.servers)))) {
+        if (((l_isch399 != 0) && ((l_confl400 != 0) || ((l_count402 * 2) <= p.servers)))) {
           return PV_FALSE;
         }
         return PV_TRUE;
@@ -1663,6 +1621,15 @@ struct MultiPaxosIR {
       }
       case 402:  // slotValid
       {
+        uint32_t pn_server_0[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 0);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_0[w_] = q_[w_]; }
+        uint32_t pn_server_1[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 1);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_1[w_] = q_[w_]; }
+        uint32_t pn_server_2[kNodeWords];
+        { const uint32_t* q_ = v.node(first_server(p) + 2);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_server_2[w_] = q_[w_]; }
         const int l_i = (int)pr.arg0;
         if ((l_i < 1)) {
           return PV_FALSE;
@@ -1675,53 +1642,53 @@ struct MultiPaxosIR {
         int l_chosen = 0;
         int l_count = 0;
         if ((0 < p.servers)) {
-          const int l_e233 = arr_server_log(v.node(first_server(p) + 0), (l_i - 1));
-          if (((l_e233 & 3) == 2)) {
-            const int l_x234 = ((((l_e233 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch != 0) && (l_x234 != l_chosen))) {
+          const int l_e412 = arr_server_log(pn_server_0, (l_i - 1));
+          if (((l_e412 & 3) == 2)) {
+            const int l_x413 = ((((l_e412 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e412 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e412 >> 8) & 7) - (((((l_e412 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e412 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e412 >> 8) & 7) - (((((l_e412 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x413 != l_chosen))) {
               l_confl = 1;
             }
-            l_chosen = l_x234;
+            l_chosen = l_x413;
             l_isch = 1;
           }
         }
         if ((1 < p.servers)) {
-          const int l_e235 = arr_server_log(v.node(first_server(p) + 1), (l_i - 1));
-          if (((l_e235 & 3) == 2)) {
-            const int l_x236 = ((((l_e235 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch != 0) && (l_x236 != l_chosen))) {
+          const int l_e414 = arr_server_log(pn_server_1, (l_i - 1));
+          if (((l_e414 & 3) == 2)) {
+            const int l_x415 = ((((l_e414 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e414 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e414 >> 8) & 7) - (((((l_e414 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e414 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e414 >> 8) & 7) - (((((l_e414 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x415 != l_chosen))) {
               l_confl = 1;
             }
-            l_chosen = l_x236;
+            l_chosen = l_x415;
             l_isch = 1;
           }
         }
         if ((2 < p.servers)) {
-          const int l_e237 = arr_server_log(v.node(first_server(p) + 2), (l_i - 1));
-          if (((l_e237 & 3) == 2)) {
-            const int l_x238 = ((((l_e237 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
-            if (((l_isch != 0) && (l_x238 != l_chosen))) {
+          const int l_e416 = arr_server_log(pn_server_2, (l_i - 1));
+          if (((l_e416 & 3) == 2)) {
+            const int l_x417 = ((((l_e416 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e416 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e416 >> 8) & 7) - (((((l_e416 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e416 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e416 >> 8) & 7) - (((((l_e416 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0);
+            if (((l_isch != 0) && (l_x417 != l_chosen))) {
               l_confl = 1;
             }
-            l_chosen = l_x238;
+            l_chosen = l_x417;
             l_isch = 1;
           }
         }
         if ((0 < p.servers)) {
-          const int l_e239 = arr_server_log(v.node(first_server(p) + 0), (l_i - 1));
-          if ((((l_e239 & 3) != 0) && (((l_e239 & 3) != 1) || (((((l_e239 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+          const int l_e418 = arr_server_log(pn_server_0, (l_i - 1));
+          if ((((l_e418 & 3) != 0) && (((l_e418 & 3) != 1) || (((((l_e418 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e418 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e418 >> 8) & 7) - (((((l_e418 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e418 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e418 >> 8) & 7) - (((((l_e418 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
             l_count = (l_count + 1);
           }
         }
         if ((1 < p.servers)) {
-          const int l_e240 = arr_server_log(v.node(first_server(p) + 1), (l_i - 1));
-          if ((((l_e240 & 3) != 0) && (((l_e240 & 3) != 1) || (((((l_e240 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+          const int l_e419 = arr_server_log(pn_server_1, (l_i - 1));
+          if ((((l_e419 & 3) != 0) && (((l_e419 & 3) != 1) || (((((l_e419 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e419 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e419 >> 8) & 7) - (((((l_e419 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e419 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e419 >> 8) & 7) - (((((l_e419 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
             l_count = (l_count + 1);
           }
         }
         if ((2 < p.servers)) {
-          const int l_e241 = arr_server_log(v.node(first_server(p) + 2), (l_i - 1));
-          if ((((l_e241 & 3) != 0) && (((l_e241 & 3) != 1) || (((((l_e241 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
+          const int l_e420 = arr_server_log(pn_server_2, (l_i - 1));
+          if ((((l_e420 & 3) != 0) && (((l_e420 & 3) != 1) || (((((l_e420 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_e420 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e420 >> 8) & 7) - (((((l_e420 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_e420 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_e420 >> 8) & 7) - (((((l_e420 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0) == l_chosen)))) {
             l_count = (l_count + 1);
           }
         }
@@ -1733,16 +1700,16 @@ struct MultiPaxosIR {
       }
       case 403:  // hasStatus
       {
-        const int l_k242 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
-        if (((l_k242 < 0) || (l_k242 >= p.servers))) {
+        const int l_k421 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
+        if (((l_k421 < 0) || (l_k421 >= p.servers))) {
           return PV_THREW;
         }
-        const int l_slot243 = ((int)pr.arg1 >> 4);
-        int l_se244 = 0;
-        if (((l_slot243 >= 1) && (l_slot243 <= 4))) {
-          l_se244 = arr_server_log(v.node(first_server(p) + l_k242), (l_slot243 - 1));
+        const int l_slot422 = ((int)pr.arg1 >> 4);
+        int l_se423 = 0;
+        if (((l_slot422 >= 1) && (l_slot422 <= 4))) {
+          l_se423 = arr_server_log(v.node(first_server(p) + l_k421), (l_slot422 - 1));
         }
-        if (((l_se244 & 3) == ((int)pr.arg1 & 15))) {
+        if (((l_se423 & 3) == ((int)pr.arg1 & 15))) {
           return PV_TRUE;
         }
         return PV_FALSE;
@@ -1750,16 +1717,16 @@ struct MultiPaxosIR {
       }
       case 404:  // hasCommand
       {
-        const int l_k245 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
-        if (((l_k245 < 0) || (l_k245 >= p.servers))) {
+        const int l_k424 = ((int)pr.arg0 - (first_server(p) + 1 - 1));
+        if (((l_k424 < 0) || (l_k424 >= p.servers))) {
           return PV_THREW;
         }
-        const int l_slot246 = ((int)pr.arg1 >> 8);
-        int l_se247 = 0;
-        if (((l_slot246 >= 1) && (l_slot246 <= 4))) {
-          l_se247 = arr_server_log(v.node(first_server(p) + l_k245), (l_slot246 - 1));
+        const int l_slot425 = ((int)pr.arg1 >> 8);
+        int l_se426 = 0;
+        if (((l_slot425 >= 1) && (l_slot425 <= 4))) {
+          l_se426 = arr_server_log(v.node(first_server(p) + l_k424), (l_slot425 - 1));
         }
-        const int l_cc = (((l_se247 & 3) == 0) ? 0 : ((((l_se247 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0));
+        const int l_cc = (((l_se426 & 3) == 0) ? 0 : ((((l_se426 >> 8) & 7) != 0) ? (((int)((p.op_pk >> ((2 * ((((((l_se426 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se426 >> 8) & 7) - (((((l_se426 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u) << 2) | (int)((p.val_pk >> ((2 * ((((((l_se426 >> 8) & 7) >= 4) ? 1 : 0)) * 3 + (((((l_se426 >> 8) & 7) - (((((l_se426 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)))) & 63)) & 3u)) : 0));
         if ((l_cc == ((int)pr.arg1 & 255))) {
           return PV_TRUE;
         }
@@ -1768,177 +1735,183 @@ struct MultiPaxosIR {
       }
       case 300:  // APPENDS_LINEARIZABLE
       {
-        const int l_pres248 = ((0 < p.clients) && (0 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres248 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u) != 2))) {
+        uint32_t pn_client_0[kNodeWords];
+        { const uint32_t* q_ = v.node(first_client(p) + 0);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_client_0[w_] = q_[w_]; }
+        uint32_t pn_client_1[kNodeWords];
+        { const uint32_t* q_ = v.node(first_client(p) + 1);  // < kNodes: in bounds for any run
+          for (int w_ = 0; w_ < kNodeWords; w_++) pn_client_1[w_] = q_[w_]; }
+        const int l_pres427 = ((0 < p.clients) && (0 < get(pn_client_0, 26, 2)));
+        if ((l_pres427 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res249 = (l_pres248 ? arr_client__results(v.node(first_client(p) + 0), 0) : 0);
-        const int l_rlen250 = (l_res249 & 7);
-        if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u))))) {
+        const int l_res428 = (l_pres427 ? arr_client__results(pn_client_0, 0) : 0);
+        const int l_rlen429 = (l_res428 & 7);
+        if ((l_pres427 && (((l_rlen429 == 0) || (l_rlen429 > 4)) || (((l_res428 >> (1 + (l_rlen429 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (0))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        const int l_pres251 = ((0 < p.clients) && (1 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres251 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u) != 2))) {
+        const int l_pres430 = ((0 < p.clients) && (1 < get(pn_client_0, 26, 2)));
+        if ((l_pres430 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res252 = (l_pres251 ? arr_client__results(v.node(first_client(p) + 0), 1) : 0);
-        const int l_rlen253 = (l_res252 & 7);
-        if ((l_pres251 && (((l_rlen253 == 0) || (l_rlen253 > 4)) || (((l_res252 >> (1 + (l_rlen253 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u))))) {
+        const int l_res431 = (l_pres430 ? arr_client__results(pn_client_0, 1) : 0);
+        const int l_rlen432 = (l_res431 & 7);
+        if ((l_pres430 && (((l_rlen432 == 0) || (l_rlen432 > 4)) || (((l_res431 >> (1 + (l_rlen432 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (1))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        const int l_pres254 = ((0 < p.clients) && (2 < get(v.node(first_client(p) + 0), 26, 2)));
-        if ((l_pres254 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u) != 2))) {
+        const int l_pres433 = ((0 < p.clients) && (2 < get(pn_client_0, 26, 2)));
+        if ((l_pres433 && ((int)((p.op_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res255 = (l_pres254 ? arr_client__results(v.node(first_client(p) + 0), 2) : 0);
-        const int l_rlen256 = (l_res255 & 7);
-        if ((l_pres254 && (((l_rlen256 == 0) || (l_rlen256 > 4)) || (((l_res255 >> (1 + (l_rlen256 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u))))) {
+        const int l_res434 = (l_pres433 ? arr_client__results(pn_client_0, 2) : 0);
+        const int l_rlen435 = (l_res434 & 7);
+        if ((l_pres433 && (((l_rlen435 == 0) || (l_rlen435 > 4)) || (((l_res434 >> (1 + (l_rlen435 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((0) * 3 + (2))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        const int l_pres257 = ((1 < p.clients) && (0 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres257 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u) != 2))) {
+        const int l_pres436 = ((1 < p.clients) && (0 < get(pn_client_1, 26, 2)));
+        if ((l_pres436 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res258 = (l_pres257 ? arr_client__results(v.node(first_client(p) + 1), 0) : 0);
-        const int l_rlen259 = (l_res258 & 7);
-        if ((l_pres257 && (((l_rlen259 == 0) || (l_rlen259 > 4)) || (((l_res258 >> (1 + (l_rlen259 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u))))) {
+        const int l_res437 = (l_pres436 ? arr_client__results(pn_client_1, 0) : 0);
+        const int l_rlen438 = (l_res437 & 7);
+        if ((l_pres436 && (((l_rlen438 == 0) || (l_rlen438 > 4)) || (((l_res437 >> (1 + (l_rlen438 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (0))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        const int l_pres260 = ((1 < p.clients) && (1 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres260 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u) != 2))) {
+        const int l_pres439 = ((1 < p.clients) && (1 < get(pn_client_1, 26, 2)));
+        if ((l_pres439 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res261 = (l_pres260 ? arr_client__results(v.node(first_client(p) + 1), 1) : 0);
-        const int l_rlen262 = (l_res261 & 7);
-        if ((l_pres260 && (((l_rlen262 == 0) || (l_rlen262 > 4)) || (((l_res261 >> (1 + (l_rlen262 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u))))) {
+        const int l_res440 = (l_pres439 ? arr_client__results(pn_client_1, 1) : 0);
+        const int l_rlen441 = (l_res440 & 7);
+        if ((l_pres439 && (((l_rlen441 == 0) || (l_rlen441 > 4)) || (((l_res440 >> (1 + (l_rlen441 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (1))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        const int l_pres263 = ((1 < p.clients) && (2 < get(v.node(first_client(p) + 1), 26, 2)));
-        if ((l_pres263 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u) != 2))) {
+        const int l_pres442 = ((1 < p.clients) && (2 < get(pn_client_1, 26, 2)));
+        if ((l_pres442 && ((int)((p.op_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u) != 2))) {
           return PV_THREW;
         }
-        const int l_res264 = (l_pres263 ? arr_client__results(v.node(first_client(p) + 1), 2) : 0);
-        const int l_rlen265 = (l_res264 & 7);
-        if ((l_pres263 && (((l_rlen265 == 0) || (l_rlen265 > 4)) || (((l_res264 >> (1 + (l_rlen265 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u))))) {
+        const int l_res443 = (l_pres442 ? arr_client__results(pn_client_1, 2) : 0);
+        const int l_rlen444 = (l_res443 & 7);
+        if ((l_pres442 && (((l_rlen444 == 0) || (l_rlen444 > 4)) || (((l_res443 >> (1 + (l_rlen444 * 2))) & 3) != (int)((p.val_pk >> ((2 * ((1) * 3 + (2))) & 63)) & 3u))))) {
           return PV_FALSE;
         }
-        if ((l_pres248 && l_pres251)) {
-          if ((l_rlen250 == l_rlen253)) {
+        if ((l_pres427 && l_pres430)) {
+          if ((l_rlen429 == l_rlen432)) {
             return PV_FALSE;
           }
-          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)) != ((l_res252 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres248 && l_pres254)) {
-          if ((l_rlen250 == l_rlen256)) {
-            return PV_FALSE;
-          }
-          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)))) {
+          if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen432) ? l_rlen429 : l_rlen432) * 2)) - 1)) != ((l_res431 >> 3) & ((1 << (((l_rlen429 < l_rlen432) ? l_rlen429 : l_rlen432) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres248 && l_pres257)) {
-          if ((l_rlen250 == l_rlen259)) {
+        if ((l_pres427 && l_pres433)) {
+          if ((l_rlen429 == l_rlen435)) {
             return PV_FALSE;
           }
-          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres248 && l_pres260)) {
-          if ((l_rlen250 == l_rlen262)) {
-            return PV_FALSE;
-          }
-          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)))) {
+          if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen435) ? l_rlen429 : l_rlen435) * 2)) - 1)) != ((l_res434 >> 3) & ((1 << (((l_rlen429 < l_rlen435) ? l_rlen429 : l_rlen435) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres248 && l_pres263)) {
-          if ((l_rlen250 == l_rlen265)) {
+        if ((l_pres427 && l_pres436)) {
+          if ((l_rlen429 == l_rlen438)) {
             return PV_FALSE;
           }
-          if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres251 && l_pres254)) {
-          if ((l_rlen253 == l_rlen256)) {
-            return PV_FALSE;
-          }
-          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)))) {
+          if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen438) ? l_rlen429 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen429 < l_rlen438) ? l_rlen429 : l_rlen438) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres251 && l_pres257)) {
-          if ((l_rlen253 == l_rlen259)) {
+        if ((l_pres427 && l_pres439)) {
+          if ((l_rlen429 == l_rlen441)) {
             return PV_FALSE;
           }
-          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres251 && l_pres260)) {
-          if ((l_rlen253 == l_rlen262)) {
-            return PV_FALSE;
-          }
-          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)))) {
+          if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen441) ? l_rlen429 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen429 < l_rlen441) ? l_rlen429 : l_rlen441) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres251 && l_pres263)) {
-          if ((l_rlen253 == l_rlen265)) {
+        if ((l_pres427 && l_pres442)) {
+          if ((l_rlen429 == l_rlen444)) {
             return PV_FALSE;
           }
-          if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres254 && l_pres257)) {
-          if ((l_rlen256 == l_rlen259)) {
-            return PV_FALSE;
-          }
-          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)))) {
+          if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen444) ? l_rlen429 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen429 < l_rlen444) ? l_rlen429 : l_rlen444) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres254 && l_pres260)) {
-          if ((l_rlen256 == l_rlen262)) {
+        if ((l_pres430 && l_pres433)) {
+          if ((l_rlen432 == l_rlen435)) {
             return PV_FALSE;
           }
-          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres254 && l_pres263)) {
-          if ((l_rlen256 == l_rlen265)) {
-            return PV_FALSE;
-          }
-          if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)))) {
+          if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen435) ? l_rlen432 : l_rlen435) * 2)) - 1)) != ((l_res434 >> 3) & ((1 << (((l_rlen432 < l_rlen435) ? l_rlen432 : l_rlen435) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres257 && l_pres260)) {
-          if ((l_rlen259 == l_rlen262)) {
+        if ((l_pres430 && l_pres436)) {
+          if ((l_rlen432 == l_rlen438)) {
             return PV_FALSE;
           }
-          if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)))) {
-            return PV_FALSE;
-          }
-        }
-        if ((l_pres257 && l_pres263)) {
-          if ((l_rlen259 == l_rlen265)) {
-            return PV_FALSE;
-          }
-          if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)))) {
+          if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen438) ? l_rlen432 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen432 < l_rlen438) ? l_rlen432 : l_rlen438) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
-        if ((l_pres260 && l_pres263)) {
-          if ((l_rlen262 == l_rlen265)) {
+        if ((l_pres430 && l_pres439)) {
+          if ((l_rlen432 == l_rlen441)) {
             return PV_FALSE;
           }
-          if ((((l_res261 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)))) {
+          if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen441) ? l_rlen432 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen432 < l_rlen441) ? l_rlen432 : l_rlen441) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres430 && l_pres442)) {
+          if ((l_rlen432 == l_rlen444)) {
+            return PV_FALSE;
+          }
+          if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen444) ? l_rlen432 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen432 < l_rlen444) ? l_rlen432 : l_rlen444) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres433 && l_pres436)) {
+          if ((l_rlen435 == l_rlen438)) {
+            return PV_FALSE;
+          }
+          if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen438) ? l_rlen435 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen435 < l_rlen438) ? l_rlen435 : l_rlen438) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres433 && l_pres439)) {
+          if ((l_rlen435 == l_rlen441)) {
+            return PV_FALSE;
+          }
+          if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen441) ? l_rlen435 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen435 < l_rlen441) ? l_rlen435 : l_rlen441) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres433 && l_pres442)) {
+          if ((l_rlen435 == l_rlen444)) {
+            return PV_FALSE;
+          }
+          if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen444) ? l_rlen435 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen435 < l_rlen444) ? l_rlen435 : l_rlen444) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres436 && l_pres439)) {
+          if ((l_rlen438 == l_rlen441)) {
+            return PV_FALSE;
+          }
+          if ((((l_res437 >> 3) & ((1 << (((l_rlen438 < l_rlen441) ? l_rlen438 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen438 < l_rlen441) ? l_rlen438 : l_rlen441) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres436 && l_pres442)) {
+          if ((l_rlen438 == l_rlen444)) {
+            return PV_FALSE;
+          }
+          if ((((l_res437 >> 3) & ((1 << (((l_rlen438 < l_rlen444) ? l_rlen438 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen438 < l_rlen444) ? l_rlen438 : l_rlen444) * 2)) - 1)))) {
+            return PV_FALSE;
+          }
+        }
+        if ((l_pres439 && l_pres442)) {
+          if ((l_rlen441 == l_rlen444)) {
+            return PV_FALSE;
+          }
+          if ((((l_res440 >> 3) & ((1 << (((l_rlen441 < l_rlen444) ? l_rlen441 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen441 < l_rlen444) ? l_rlen441 : l_rlen444) * 2)) - 1)))) {
             return PV_FALSE;
           }
         }
@@ -2092,9 +2065,8 @@ struct MultiPaxosIR {
     e->from = e->to = i;
     (void)w; (void)j; (void)p;
     if (is_server(i, p)) {
-      const int q = deliverable_server(w, j);
-      if (q < 0) return;
-      const int x = arr_server__timers(w, q);
+      if (j != 0) return;
+      const int x = (0 << 2);
       e->type = 8 + ttype(x);
       int mn = 0, mx = 0;
       tbounds(ttype(x), mn, mx);

@@ -47,14 +47,6 @@ struct PBIR {
   };
   static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
   static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
-  static DSL_HD int arr_viewserver__timers(const uint32_t* w, int j) {
-    return (int)((((uint64_t)w[0]) >> (17 + 4 * (j))) & 15u);
-  }
-  static DSL_HD void arr_put_viewserver__timers(uint32_t* w, int j, int v) {
-    const int sh = 17 + 4 * (j);
-    const uint64_t x = (((uint64_t)w[0]) & ~((uint64_t)15u << sh)) | ((uint64_t)((uint32_t)v & 15u) << sh);
-    w[0] = (uint32_t)x;
-  }
   static DSL_HD int arr_server_kv(const uint32_t* w, int j) {
     return (int)((((uint64_t)w[0]) >> (13 + 8 * (j))) & 255u);
   }
@@ -70,14 +62,6 @@ struct PBIR {
     const int sh = 0 + (j) / 2 * 32 + (j) % 2 * 12;
     const uint64_t x = (((uint64_t)w[1]) & ~((uint64_t)4095u << sh)) | ((uint64_t)((uint32_t)v & 4095u) << sh);
     w[1] = (uint32_t)x;
-  }
-  static DSL_HD int arr_server__timers(const uint32_t* w, int j) {
-    return (int)((((uint64_t)w[2]) >> (2 + 4 * (j))) & 15u);
-  }
-  static DSL_HD void arr_put_server__timers(uint32_t* w, int j, int v) {
-    const int sh = 2 + 4 * (j);
-    const uint64_t x = (((uint64_t)w[2]) & ~((uint64_t)15u << sh)) | ((uint64_t)((uint32_t)v & 15u) << sh);
-    w[2] = (uint32_t)x;
   }
   static DSL_HD int arr_client__timers(const uint32_t* w, int j) {
     return (int)((((uint64_t)w[1]) >> (0 + 4 * (j))) & 15u);
@@ -115,68 +99,6 @@ struct PBIR {
     if (type == 2) { mn = 100; mx = 100; }
   }
   static DSL_HD int ttype(int e) { return e >> 2; }
-  static DSL_HD bool push_timer_viewserver(uint32_t* w, int e) {
-    const int n = get(w, 15, 2);
-    if (n >= 2) return false;
-    arr_put_viewserver__timers(w, n, e);
-    put(w, 15, 2, n + 1);
-    return true;
-  }
-  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)
-  static DSL_HD int deliverable_viewserver(const uint32_t* w, int j) {
-    const int n = get(w, 15, 2);
-    int mm = 0x7fffffff, c = 0;
-    for (int q = 0; q < n; q++) {
-      int mn = 0, mx = 0;
-      tbounds(ttype(arr_viewserver__timers(w, q)), mn, mx);
-      if (q > 0 && mn >= mm) continue;
-      if (c == j) return q;
-      c++;
-      if (mx < mm) mm = mx;
-    }
-    return j < 0 ? c : -1;
-  }
-  static DSL_HD void remove_timer_viewserver(uint32_t* w, int e) {  // the first equal entry
-    const int n = get(w, 15, 2);
-    int q0 = n;
-    for (int q = n - 1; q >= 0; q--)
-      if (arr_viewserver__timers(w, q) == e) q0 = q;
-    if (q0 >= n) return;
-    for (int q = q0; q + 1 < n; q++) arr_put_viewserver__timers(w, q, arr_viewserver__timers(w, q + 1));
-    arr_put_viewserver__timers(w, n - 1, 0);
-    put(w, 15, 2, n - 1);
-  }
-  static DSL_HD bool push_timer_server(uint32_t* w, int e) {
-    const int n = get(w, 64, 2);
-    if (n >= 2) return false;
-    arr_put_server__timers(w, n, e);
-    put(w, 64, 2, n + 1);
-    return true;
-  }
-  // TimerQueue.deliverable(): the index of deliverable entry j (-1: none), or their count (j < 0)
-  static DSL_HD int deliverable_server(const uint32_t* w, int j) {
-    const int n = get(w, 64, 2);
-    int mm = 0x7fffffff, c = 0;
-    for (int q = 0; q < n; q++) {
-      int mn = 0, mx = 0;
-      tbounds(ttype(arr_server__timers(w, q)), mn, mx);
-      if (q > 0 && mn >= mm) continue;
-      if (c == j) return q;
-      c++;
-      if (mx < mm) mm = mx;
-    }
-    return j < 0 ? c : -1;
-  }
-  static DSL_HD void remove_timer_server(uint32_t* w, int e) {  // the first equal entry
-    const int n = get(w, 64, 2);
-    int q0 = n;
-    for (int q = n - 1; q >= 0; q--)
-      if (arr_server__timers(w, q) == e) q0 = q;
-    if (q0 >= n) return;
-    for (int q = q0; q + 1 < n; q++) arr_put_server__timers(w, q, arr_server__timers(w, q + 1));
-    arr_put_server__timers(w, n - 1, 0);
-    put(w, 64, 2, n - 1);
-  }
   static DSL_HD bool push_timer_client(uint32_t* w, int e) {
     const int n = get(w, 18, 3);
     if (n >= 4) return false;
@@ -251,8 +173,8 @@ struct PBIR {
     }
   }
   static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {
-    if (is_viewserver(i, p)) return deliverable_viewserver(w, -1);
-    if (is_server(i, p)) return deliverable_server(w, -1);
+    if (is_viewserver(i, p)) return 1;  // [PingCheckTimer] in every state
+    if (is_server(i, p)) return 1;  // [PingTimer] in every state
     if (is_client(i, p)) return deliverable_client(w, -1);
     (void)i; (void)w; (void)p;
     return 0;
@@ -260,7 +182,7 @@ struct PBIR {
   template <class O>
   static DSL_HD int init_viewserver(int i, uint32_t* w, O& out, const Params& p) {
     (void)i; (void)p; (void)out;
-    if (!push_timer_viewserver(w, (0 << 2))) return STEP_OVERFLOW;
+    // set PingCheckTimer: the queue stays [PingCheckTimer]
     return STEP_OK;
   }
   template <class O>
@@ -384,14 +306,14 @@ struct PBIR {
         }
       }
     }
-    if (!push_timer_viewserver(w, (0 << 2))) return STEP_OVERFLOW;
+    // set PingCheckTimer: the queue stays [PingCheckTimer]
     return STEP_OK;
   }
   template <class O>
   static DSL_HD int init_server(int i, uint32_t* w, O& out, const Params& p) {
     (void)i; (void)p; (void)out;
     out.send(((Rec)0 << 60) | ((Rec)(i) << 57) | ((Rec)((first_viewserver(p) + 1 - 1)) << 54) | ((Rec)((0) & 15) << 0));
-    if (!push_timer_server(w, (1 << 2))) return STEP_OVERFLOW;
+    // set PingTimer: the queue stays [PingTimer]
     return STEP_OK;
   }
   template <class O>
@@ -609,7 +531,7 @@ struct PBIR {
     } else {
       out.send(((Rec)0 << 60) | ((Rec)(i) << 57) | ((Rec)((first_viewserver(p) + 1 - 1)) << 54) | ((Rec)((l_n) & 15) << 0));
     }
-    if (!push_timer_server(w, (1 << 2))) return STEP_OVERFLOW;
+    // set PingTimer: the queue stays [PingTimer]
     return STEP_OK;
   }
   template <class O>
@@ -684,28 +606,12 @@ struct PBIR {
   static DSL_HD int on_timer(int i, uint32_t* w, int j, O& out, const Params& p) {
     (void)w; (void)j; (void)out;
     if (is_viewserver(i, p)) {
-      const int q = deliverable_viewserver(w, j);
-      if (q < 0) return STEP_NULL;
-      const int e = arr_viewserver__timers(w, q);
-      if (ttype(e) == 0) {  // PingCheckTimer
-        const int rc = ht_viewserver_PingCheckTimer(i, w, e, out, p);
-        if (rc != STEP_OK) return rc;
-        remove_timer_viewserver(w, e);  // SearchState.stepTimer: the first equal entry
-        return STEP_OK;
-      }
-      return STEP_EXCEPTION;  // no handler for this timer
+      if (j != 0) return STEP_NULL;
+      return ht_viewserver_PingCheckTimer(i, w, (0 << 2), out, p);  // PingCheckTimer
     }
     if (is_server(i, p)) {
-      const int q = deliverable_server(w, j);
-      if (q < 0) return STEP_NULL;
-      const int e = arr_server__timers(w, q);
-      if (ttype(e) == 1) {  // PingTimer
-        const int rc = ht_server_PingTimer(i, w, e, out, p);
-        if (rc != STEP_OK) return rc;
-        remove_timer_server(w, e);  // SearchState.stepTimer: the first equal entry
-        return STEP_OK;
-      }
-      return STEP_EXCEPTION;  // no handler for this timer
+      if (j != 0) return STEP_NULL;
+      return ht_server_PingTimer(i, w, (1 << 2), out, p);  // PingTimer
     }
     if (is_client(i, p)) {
       const int q = deliverable_client(w, j);
@@ -928,9 +834,8 @@ struct PBIR {
     e->from = e->to = i;
     (void)w; (void)j; (void)p;
     if (is_viewserver(i, p)) {
-      const int q = deliverable_viewserver(w, j);
-      if (q < 0) return;
-      const int x = arr_viewserver__timers(w, q);
+      if (j != 0) return;
+      const int x = (0 << 2);
       e->type = 9 + ttype(x);
       int mn = 0, mx = 0;
       tbounds(ttype(x), mn, mx);
@@ -948,9 +853,8 @@ struct PBIR {
       }
     }
     if (is_server(i, p)) {
-      const int q = deliverable_server(w, j);
-      if (q < 0) return;
-      const int x = arr_server__timers(w, q);
+      if (j != 0) return;
+      const int x = (1 << 2);
       e->type = 9 + ttype(x);
       int mn = 0, mx = 0;
       tbounds(ttype(x), mn, mx);

@@ -190,6 +190,9 @@ class NodeKind:
     tail_fn: Optional[Callable] = None  # common tail of the message handlers (see tail())
     flags: List[str] = field(default_factory=list)
     first: int = 0                 # node index of the first instance (at the maximum counts)
+    # a timer queue that is [T] in every reachable state (Protocol.fixed_timer): the device form
+    # keeps no queue for it (one deliverable timer, re-armed by its own handler)
+    fixed_timer: Optional["RecordType"] = None
 
     def on(self, msg: RecordType):
         def deco(fn):
@@ -313,9 +316,61 @@ class Protocol:
             k.first = idx
             idx += k.max_count
         self.max_nodes = idx
+        if not getattr(self, "_fixed_done", False):  # once per protocol (handlers are recorded on a first layout)
+            self._fixed_done = True
+            self._place()
+            for k in self.kinds:
+                k.fixed_timer = self.fixed_timer(k)
+        self._place()
+
+    def fixed_timer(self, k: "NodeKind") -> Optional["RecordType"]:
+        """T when k's timer queue is [T] in every reachable state: k handles exactly one timer
+        type T, which has no fields; its init sets T once, unconditionally; T's handler re-sets T
+        as its last top-level statement, sets no other timer and never returns early; no message
+        handler (nor the common tail) sets a timer. Then SearchState.stepTimer's remove of the
+        delivered entry and the handler's re-set leave [T] as it was, so the device form keeps
+        no queue (the oracle form keeps the TimerQueue and checks the claim by parity)."""
+        if not k.timer_cap or k.client or len(k.timer_handlers) != 1 or not k.init_fn:
+            return None
+        tname, fn = next(iter(k.timer_handlers.items()))
+        t = next(x for x in self.timers if x.name == tname)
+        if t.fields:
+            return None
+
+        def walk(ss):
+            for st in ss:
+                yield st
+                if isinstance(st, IfS):
+                    yield from walk(st.then)
+                    yield from walk(st.other)
+                elif isinstance(st, ForS):
+                    yield from walk(st.body)
+
+        def sets(ss):
+            return [st for st in walk(ss) if isinstance(st, SetTimerS)]
+
+        init = record(self, k, k.init_fn)
+        top = [st for st in init if isinstance(st, SetTimerS)]
+        if len(sets(init)) != 1 or len(top) != 1 or top[0].timer is not t:
+            return None
+        hs = record(self, k, fn, event=t, is_timer=True)
+        if not hs or not isinstance(hs[-1], SetTimerS) or hs[-1].timer is not t or len(sets(hs)) != 1:
+            return None
+        if any(isinstance(st, RetS) for st in walk(hs)):
+            return None
+        for m in self.messages:
+            if m.name in k.handlers and sets(record(self, k, k.handlers[m.name], event=m)):
+                return None
+        if k.tail_fn and sets(record(self, k, k.tail_fn)):
+            return None
+        return t
+
+    def _place(self):
         words = 1
         for k in self.kinds:
-            if k.timer_cap and not any(f.name == "_timers" for f in k.fields):
+            if k.fixed_timer is not None:
+                k.fields = [f for f in k.fields if f.name != "_timers"]
+            elif k.timer_cap and not any(f.name == "_timers" for f in k.fields):
                 k.fields.append(FieldDecl("_timers", self.timer_entry_bits(), k.timer_cap))
             if k.client and not any(f.name == "_results" for f in k.fields):
                 rb = max(f.bits for f in k.fields if f.name == k.result_field)
@@ -697,9 +752,16 @@ class PredHandler(Handler):
 
     def __init__(self, proto: Protocol):
         super().__init__(proto, proto.kinds[0])
+        self.cached: List[Tuple[str, int]] = []  # (kind, instance) read at a constant instance
 
-    @staticmethod
-    def _node_dev(kind: NodeKind, k) -> str:
+    def _node_dev(self, kind: NodeKind, k) -> str:
+        """A constant instance reads a register copy of its words (pn_<kind>_<k>, loaded once at the
+        predicate's top: independent LDS reads, none of them under the `k < count` guards, which
+        would otherwise keep each read where it is); a run-time instance reads through the view."""
+        if isinstance(k, int):
+            if (kind.name, k) not in self.cached:
+                self.cached.append((kind.name, k))
+            return f"pn_{kind.name}_{k}"
         return f"v.node(first_{kind.name}(p) + {lit(k).dev})"
 
     @staticmethod
@@ -782,9 +844,13 @@ class _MsgView:
         raise KeyError(f"{m.name} has no field {name}")
 
 
-def record_pred(proto: Protocol, fn: Callable) -> List[Stmt]:
+def record_pred(proto: Protocol, fn: Callable, cached: Optional[list] = None) -> List[Stmt]:
+    """The predicate's statements; `cached` receives the (kind, constant instance) pairs whose
+    words the device form reads from a register copy."""
     q = PredHandler(proto)
     fn(q)
+    if cached is not None:
+        cached.extend(q.cached)
     return q.stmts
 
 

@@ -51,8 +51,10 @@ def _stmts(p: Protocol, k: NodeKind, ss: List[Stmt], d: int) -> List[str]:
         elif isinstance(s, SendS):
             out.append(f"{_ind(d)}out.send({_rec_expr(p, s)});")
         elif isinstance(s, SetTimerS):
-            tf = next(f for f in k.fields if f.name == "_timers")
-            out.append(f"{_ind(d)}if (!push_timer_{k.name}(w, {_timer_entry(p, s.timer, s.vals)})) return STEP_OVERFLOW;")
+            if k.fixed_timer is s.timer:  # the queue stays [T] (Protocol.fixed_timer): nothing is stored
+                out.append(f"{_ind(d)}// set {s.timer.name}: the queue stays [{s.timer.name}]")
+            else:
+                out.append(f"{_ind(d)}if (!push_timer_{k.name}(w, {_timer_entry(p, s.timer, s.vals)})) return STEP_OVERFLOW;")
         elif isinstance(s, ThrowS):
             out.append(f"{_ind(d)}return STEP_EXCEPTION;  // {s.what}")
         elif isinstance(s, VarS):
@@ -173,7 +175,7 @@ def generate(p: Protocol, source: str) -> str:
     a("  }")
     a(f"  static DSL_HD int ttype(int e) {{ return {'e >> ' + str(fb) if len(p.timers) > 1 else '0'}; }}")
     for k in p.kinds:
-        if not k.timer_cap:
+        if not k.timer_cap or k.fixed_timer is not None:
             continue
         tf = next(f for f in k.fields if f.name == "_timers")
         a(f"  static DSL_HD bool push_timer_{k.name}(uint32_t* w, int e) {{")
@@ -257,7 +259,9 @@ def generate(p: Protocol, source: str) -> str:
     a("  }")
     a("  static DSL_HD int num_timer_events(int i, const uint32_t* w, const Params& p) {")
     for k in p.kinds:
-        if k.timer_cap:
+        if k.fixed_timer is not None:
+            a(f"    if (is_{k.name}(i, p)) return 1;  // [{k.fixed_timer.name}] in every state")
+        elif k.timer_cap:
             a(f"    if (is_{k.name}(i, p)) return deliverable_{k.name}(w, -1);")
     a("    (void)i; (void)w; (void)p;")
     a("    return 0;")
@@ -335,6 +339,13 @@ def generate(p: Protocol, source: str) -> str:
     for k in p.kinds:
         if not k.timer_cap:
             continue
+        if k.fixed_timer is not None:  # stepTimer's remove and the handler's re-set cancel out
+            t = k.fixed_timer
+            a(f"    if (is_{k.name}(i, p)) {{")
+            a("      if (j != 0) return STEP_NULL;")
+            a(f"      return ht_{k.name}_{t.name}(i, w, {_timer_entry(p, t, [])}, out, p);  // {t.name}")
+            a("    }")
+            continue
         tf = next(f for f in k.fields if f.name == "_timers")
         a(f"    if (is_{k.name}(i, p)) {{")
         a(f"      const int q = deliverable_{k.name}(w, j);")
@@ -394,7 +405,13 @@ def generate(p: Protocol, source: str) -> str:
             for pid in pd.ids:
                 a(f"      case {pid}:  // {' / '.join(pd.names)}")
             a("      {")
-            L.extend(_stmts(p, k, record_pred(p, pd.fn), 4))
+            cached = []
+            body = _stmts(p, k, record_pred(p, pd.fn, cached), 4)
+            for kn, inst in cached:  # register copies of the constant instances' words (DCE keeps the used ones)
+                a(f"        uint32_t pn_{kn}_{inst}[kNodeWords];")
+                a(f"        {{ const uint32_t* q_ = v.node(first_{kn}(p) + {inst});  // < kNodes: in bounds for any run")
+                a(f"          for (int w_ = 0; w_ < kNodeWords; w_++) pn_{kn}_{inst}[w_] = q_[w_]; }}")
+            L.extend(body)
             a("        return PV_TRUE;")
             a("      }")
         a("      default:")
@@ -530,11 +547,15 @@ def generate(p: Protocol, source: str) -> str:
     for k in p.kinds:
         if not k.timer_cap:
             continue
-        tf = next(f for f in k.fields if f.name == "_timers")
         a(f"    if (is_{k.name}(i, p)) {{")
-        a(f"      const int q = deliverable_{k.name}(w, j);")
-        a("      if (q < 0) return;")
-        a(f"      const int x = {lget(k, tf, 'w', 'q')};")
+        if k.fixed_timer is not None:
+            a("      if (j != 0) return;")
+            a(f"      const int x = {_timer_entry(p, k.fixed_timer, [])};")
+        else:
+            tf = next(f for f in k.fields if f.name == "_timers")
+            a(f"      const int q = deliverable_{k.name}(w, j);")
+            a("      if (q < 0) return;")
+            a(f"      const int x = {lget(k, tf, 'w', 'q')};")
         a(f"      e->type = {len(p.messages)} + ttype(x);")
         a("      int mn = 0, mx = 0;")
         a("      tbounds(ttype(x), mn, mx);")

@@ -90,162 +90,162 @@ struct N_server : Node {
         const int l_cmd = std::stoi(m.f[0]);
         const int l_c = ((l_cmd >= 4) ? 1 : 0);
         const int l_q = (l_cmd - (((l_cmd >= 4) ? 1 : 0) * 3));
-        const int l_upto0 = slotout;
-        int l_kv1 = 0;
-        int l_ls02 = 0;
-        int l_ls13 = 0;
-        int l_r4 = 0;
-        const int l_cmd5 = ((log[0] >> 8) & 7);
-        const int l_c6 = ((l_cmd5 >= 4) ? 1 : 0);
-        const int l_q7 = (l_cmd5 - (((l_cmd5 >= 4) ? 1 : 0) * 3));
-        if ((((1 < l_upto0) && (l_cmd5 != 0)) && ((l_c6 ? l_ls13 : l_ls02) < l_q7))) {
-          const int l_c8 = ((l_cmd5 >= 4) ? 1 : 0);
-          const int l_op9 = prm.op[l_c8][((l_cmd5 - (((l_cmd5 >= 4) ? 1 : 0) * 3)) - 1)];
-          const int l_v10 = prm.val[l_c8][((l_cmd5 - (((l_cmd5 >= 4) ? 1 : 0) * 3)) - 1)];
-          int l_x11 = 0;
-          if ((l_op9 == 1)) {
-            l_kv1 = (1 | (l_v10 << 3));
-            l_x11 = 7;
+        const int l_upto179 = slotout;
+        int l_kv180 = 0;
+        int l_ls0181 = 0;
+        int l_ls1182 = 0;
+        int l_r183 = 0;
+        const int l_cmd184 = ((log[0] >> 8) & 7);
+        const int l_c185 = ((l_cmd184 >= 4) ? 1 : 0);
+        const int l_q186 = (l_cmd184 - (((l_cmd184 >= 4) ? 1 : 0) * 3));
+        if ((((1 < l_upto179) && (l_cmd184 != 0)) && ((l_c185 ? l_ls1182 : l_ls0181) < l_q186))) {
+          const int l_c187 = ((l_cmd184 >= 4) ? 1 : 0);
+          const int l_op188 = prm.op[l_c187][((l_cmd184 - (((l_cmd184 >= 4) ? 1 : 0) * 3)) - 1)];
+          const int l_v189 = prm.val[l_c187][((l_cmd184 - (((l_cmd184 >= 4) ? 1 : 0) * 3)) - 1)];
+          int l_x190 = 0;
+          if ((l_op188 == 1)) {
+            l_kv180 = (1 | (l_v189 << 3));
+            l_x190 = 7;
           }
-          if ((l_op9 == 2)) {
-            const int l_len12 = (l_kv1 & 7);
-            l_kv1 = (((l_len12 + 1) | (l_kv1 & -8)) | (l_v10 << (3 + (l_len12 * 2))));
-            l_x11 = l_kv1;
+          if ((l_op188 == 2)) {
+            const int l_len191 = (l_kv180 & 7);
+            l_kv180 = (((l_len191 + 1) | (l_kv180 & -8)) | (l_v189 << (3 + (l_len191 * 2))));
+            l_x190 = l_kv180;
           }
-          if ((l_op9 == 3)) {
-            l_x11 = (((l_kv1 & 7) != 0) ? l_kv1 : 6);
+          if ((l_op188 == 3)) {
+            l_x190 = (((l_kv180 & 7) != 0) ? l_kv180 : 6);
           }
-          if ((l_c6 != 0)) {
-            l_ls13 = l_q7;
+          if ((l_c185 != 0)) {
+            l_ls1182 = l_q186;
           } else {
-            l_ls02 = l_q7;
+            l_ls0181 = l_q186;
           }
-          if (((l_c6 == l_c) && (l_q7 == l_q))) {
-            l_r4 = l_x11;
+          if (((l_c185 == l_c) && (l_q186 == l_q))) {
+            l_r183 = l_x190;
           }
         }
-        const int l_cmd13 = ((log[1] >> 8) & 7);
-        const int l_c14 = ((l_cmd13 >= 4) ? 1 : 0);
-        const int l_q15 = (l_cmd13 - (((l_cmd13 >= 4) ? 1 : 0) * 3));
-        if ((((2 < l_upto0) && (l_cmd13 != 0)) && ((l_c14 ? l_ls13 : l_ls02) < l_q15))) {
-          const int l_c16 = ((l_cmd13 >= 4) ? 1 : 0);
-          const int l_op17 = prm.op[l_c16][((l_cmd13 - (((l_cmd13 >= 4) ? 1 : 0) * 3)) - 1)];
-          const int l_v18 = prm.val[l_c16][((l_cmd13 - (((l_cmd13 >= 4) ? 1 : 0) * 3)) - 1)];
-          int l_x19 = 0;
-          if ((l_op17 == 1)) {
-            l_kv1 = (1 | (l_v18 << 3));
-            l_x19 = 7;
+        const int l_cmd192 = ((log[1] >> 8) & 7);
+        const int l_c193 = ((l_cmd192 >= 4) ? 1 : 0);
+        const int l_q194 = (l_cmd192 - (((l_cmd192 >= 4) ? 1 : 0) * 3));
+        if ((((2 < l_upto179) && (l_cmd192 != 0)) && ((l_c193 ? l_ls1182 : l_ls0181) < l_q194))) {
+          const int l_c195 = ((l_cmd192 >= 4) ? 1 : 0);
+          const int l_op196 = prm.op[l_c195][((l_cmd192 - (((l_cmd192 >= 4) ? 1 : 0) * 3)) - 1)];
+          const int l_v197 = prm.val[l_c195][((l_cmd192 - (((l_cmd192 >= 4) ? 1 : 0) * 3)) - 1)];
+          int l_x198 = 0;
+          if ((l_op196 == 1)) {
+            l_kv180 = (1 | (l_v197 << 3));
+            l_x198 = 7;
           }
-          if ((l_op17 == 2)) {
-            const int l_len20 = (l_kv1 & 7);
-            l_kv1 = (((l_len20 + 1) | (l_kv1 & -8)) | (l_v18 << (3 + (l_len20 * 2))));
-            l_x19 = l_kv1;
+          if ((l_op196 == 2)) {
+            const int l_len199 = (l_kv180 & 7);
+            l_kv180 = (((l_len199 + 1) | (l_kv180 & -8)) | (l_v197 << (3 + (l_len199 * 2))));
+            l_x198 = l_kv180;
           }
-          if ((l_op17 == 3)) {
-            l_x19 = (((l_kv1 & 7) != 0) ? l_kv1 : 6);
+          if ((l_op196 == 3)) {
+            l_x198 = (((l_kv180 & 7) != 0) ? l_kv180 : 6);
           }
-          if ((l_c14 != 0)) {
-            l_ls13 = l_q15;
+          if ((l_c193 != 0)) {
+            l_ls1182 = l_q194;
           } else {
-            l_ls02 = l_q15;
+            l_ls0181 = l_q194;
           }
-          if (((l_c14 == l_c) && (l_q15 == l_q))) {
-            l_r4 = l_x19;
+          if (((l_c193 == l_c) && (l_q194 == l_q))) {
+            l_r183 = l_x198;
           }
         }
-        const int l_cmd21 = ((log[2] >> 8) & 7);
-        const int l_c22 = ((l_cmd21 >= 4) ? 1 : 0);
-        const int l_q23 = (l_cmd21 - (((l_cmd21 >= 4) ? 1 : 0) * 3));
-        if ((((3 < l_upto0) && (l_cmd21 != 0)) && ((l_c22 ? l_ls13 : l_ls02) < l_q23))) {
-          const int l_c24 = ((l_cmd21 >= 4) ? 1 : 0);
-          const int l_op25 = prm.op[l_c24][((l_cmd21 - (((l_cmd21 >= 4) ? 1 : 0) * 3)) - 1)];
-          const int l_v26 = prm.val[l_c24][((l_cmd21 - (((l_cmd21 >= 4) ? 1 : 0) * 3)) - 1)];
-          int l_x27 = 0;
-          if ((l_op25 == 1)) {
-            l_kv1 = (1 | (l_v26 << 3));
-            l_x27 = 7;
+        const int l_cmd200 = ((log[2] >> 8) & 7);
+        const int l_c201 = ((l_cmd200 >= 4) ? 1 : 0);
+        const int l_q202 = (l_cmd200 - (((l_cmd200 >= 4) ? 1 : 0) * 3));
+        if ((((3 < l_upto179) && (l_cmd200 != 0)) && ((l_c201 ? l_ls1182 : l_ls0181) < l_q202))) {
+          const int l_c203 = ((l_cmd200 >= 4) ? 1 : 0);
+          const int l_op204 = prm.op[l_c203][((l_cmd200 - (((l_cmd200 >= 4) ? 1 : 0) * 3)) - 1)];
+          const int l_v205 = prm.val[l_c203][((l_cmd200 - (((l_cmd200 >= 4) ? 1 : 0) * 3)) - 1)];
+          int l_x206 = 0;
+          if ((l_op204 == 1)) {
+            l_kv180 = (1 | (l_v205 << 3));
+            l_x206 = 7;
           }
-          if ((l_op25 == 2)) {
-            const int l_len28 = (l_kv1 & 7);
-            l_kv1 = (((l_len28 + 1) | (l_kv1 & -8)) | (l_v26 << (3 + (l_len28 * 2))));
-            l_x27 = l_kv1;
+          if ((l_op204 == 2)) {
+            const int l_len207 = (l_kv180 & 7);
+            l_kv180 = (((l_len207 + 1) | (l_kv180 & -8)) | (l_v205 << (3 + (l_len207 * 2))));
+            l_x206 = l_kv180;
           }
-          if ((l_op25 == 3)) {
-            l_x27 = (((l_kv1 & 7) != 0) ? l_kv1 : 6);
+          if ((l_op204 == 3)) {
+            l_x206 = (((l_kv180 & 7) != 0) ? l_kv180 : 6);
           }
-          if ((l_c22 != 0)) {
-            l_ls13 = l_q23;
+          if ((l_c201 != 0)) {
+            l_ls1182 = l_q202;
           } else {
-            l_ls02 = l_q23;
+            l_ls0181 = l_q202;
           }
-          if (((l_c22 == l_c) && (l_q23 == l_q))) {
-            l_r4 = l_x27;
+          if (((l_c201 == l_c) && (l_q202 == l_q))) {
+            l_r183 = l_x206;
           }
         }
-        const int l_cmd29 = ((log[3] >> 8) & 7);
-        const int l_c30 = ((l_cmd29 >= 4) ? 1 : 0);
-        const int l_q31 = (l_cmd29 - (((l_cmd29 >= 4) ? 1 : 0) * 3));
-        if ((((4 < l_upto0) && (l_cmd29 != 0)) && ((l_c30 ? l_ls13 : l_ls02) < l_q31))) {
-          const int l_c32 = ((l_cmd29 >= 4) ? 1 : 0);
-          const int l_op33 = prm.op[l_c32][((l_cmd29 - (((l_cmd29 >= 4) ? 1 : 0) * 3)) - 1)];
-          const int l_v34 = prm.val[l_c32][((l_cmd29 - (((l_cmd29 >= 4) ? 1 : 0) * 3)) - 1)];
-          int l_x35 = 0;
-          if ((l_op33 == 1)) {
-            l_kv1 = (1 | (l_v34 << 3));
-            l_x35 = 7;
+        const int l_cmd208 = ((log[3] >> 8) & 7);
+        const int l_c209 = ((l_cmd208 >= 4) ? 1 : 0);
+        const int l_q210 = (l_cmd208 - (((l_cmd208 >= 4) ? 1 : 0) * 3));
+        if ((((4 < l_upto179) && (l_cmd208 != 0)) && ((l_c209 ? l_ls1182 : l_ls0181) < l_q210))) {
+          const int l_c211 = ((l_cmd208 >= 4) ? 1 : 0);
+          const int l_op212 = prm.op[l_c211][((l_cmd208 - (((l_cmd208 >= 4) ? 1 : 0) * 3)) - 1)];
+          const int l_v213 = prm.val[l_c211][((l_cmd208 - (((l_cmd208 >= 4) ? 1 : 0) * 3)) - 1)];
+          int l_x214 = 0;
+          if ((l_op212 == 1)) {
+            l_kv180 = (1 | (l_v213 << 3));
+            l_x214 = 7;
           }
-          if ((l_op33 == 2)) {
-            const int l_len36 = (l_kv1 & 7);
-            l_kv1 = (((l_len36 + 1) | (l_kv1 & -8)) | (l_v34 << (3 + (l_len36 * 2))));
-            l_x35 = l_kv1;
+          if ((l_op212 == 2)) {
+            const int l_len215 = (l_kv180 & 7);
+            l_kv180 = (((l_len215 + 1) | (l_kv180 & -8)) | (l_v213 << (3 + (l_len215 * 2))));
+            l_x214 = l_kv180;
           }
-          if ((l_op33 == 3)) {
-            l_x35 = (((l_kv1 & 7) != 0) ? l_kv1 : 6);
+          if ((l_op212 == 3)) {
+            l_x214 = (((l_kv180 & 7) != 0) ? l_kv180 : 6);
           }
-          if ((l_c30 != 0)) {
-            l_ls13 = l_q31;
+          if ((l_c209 != 0)) {
+            l_ls1182 = l_q210;
           } else {
-            l_ls02 = l_q31;
+            l_ls0181 = l_q210;
           }
-          if (((l_c30 == l_c) && (l_q31 == l_q))) {
-            l_r4 = l_x35;
+          if (((l_c209 == l_c) && (l_q210 == l_q))) {
+            l_r183 = l_x214;
           }
         }
-        const int l_ls = (l_c ? l_ls13 : l_ls02);
+        const int l_ls = (l_c ? l_ls1182 : l_ls0181);
         if ((l_ls >= l_q)) {
           if (((active != 0) && (l_ls == l_q))) {
-            ctx.send(Rec{"Reply", {std::to_string(l_q), std::to_string(l_r4)}}, (first_client(prm) + (l_c + 1) - 1));
+            ctx.send(Rec{"Reply", {std::to_string(l_q), std::to_string(l_r183)}}, (first_client(prm) + (l_c + 1) - 1));
           }
           return;
         }
         int l_slot = slotin;
         int l_inlog = 0;
-        const int l_e37 = log[0];
-        if ((((l_e37 & 3) != 0) && (2 > l_slot))) {
+        const int l_e216 = log[0];
+        if ((((l_e216 & 3) != 0) && (2 > l_slot))) {
           l_slot = 2;
         }
-        if ((((l_e37 & 3) != 0) && (((l_e37 >> 8) & 7) == l_cmd))) {
+        if ((((l_e216 & 3) != 0) && (((l_e216 >> 8) & 7) == l_cmd))) {
           l_inlog = 1;
         }
-        const int l_e38 = log[1];
-        if ((((l_e38 & 3) != 0) && (3 > l_slot))) {
+        const int l_e217 = log[1];
+        if ((((l_e217 & 3) != 0) && (3 > l_slot))) {
           l_slot = 3;
         }
-        if ((((l_e38 & 3) != 0) && (((l_e38 >> 8) & 7) == l_cmd))) {
+        if ((((l_e217 & 3) != 0) && (((l_e217 >> 8) & 7) == l_cmd))) {
           l_inlog = 1;
         }
-        const int l_e39 = log[2];
-        if ((((l_e39 & 3) != 0) && (4 > l_slot))) {
+        const int l_e218 = log[2];
+        if ((((l_e218 & 3) != 0) && (4 > l_slot))) {
           l_slot = 4;
         }
-        if ((((l_e39 & 3) != 0) && (((l_e39 >> 8) & 7) == l_cmd))) {
+        if ((((l_e218 & 3) != 0) && (((l_e218 >> 8) & 7) == l_cmd))) {
           l_inlog = 1;
         }
-        const int l_e40 = log[3];
-        if ((((l_e40 & 3) != 0) && (5 > l_slot))) {
+        const int l_e219 = log[3];
+        if ((((l_e219 & 3) != 0) && (5 > l_slot))) {
           l_slot = 5;
         }
-        if ((((l_e40 & 3) != 0) && (((l_e40 >> 8) & 7) == l_cmd))) {
+        if ((((l_e219 & 3) != 0) && (((l_e219 >> 8) & 7) == l_cmd))) {
           l_inlog = 1;
         }
         if ((((active == 0) || (l_slot > 4)) || (l_inlog != 0))) {
@@ -264,17 +264,17 @@ struct N_server : Node {
           ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(l_slot), std::to_string(l_cmd)}}, (first_server(prm) + 3 - 1));
         }
         if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-          const int l_ccmd41 = ((log[(l_slot - 1)] >> 8) & 7);
-          log[(l_slot - 1)] = ((2 | (0 << 2)) | (l_ccmd41 << 8));
+          const int l_ccmd220 = ((log[(l_slot - 1)] >> 8) & 7);
+          log[(l_slot - 1)] = ((2 | (0 << 2)) | (l_ccmd220 << 8));
           votes[(l_slot - 1)] = 0;
           if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd41)}}, (first_server(prm) + 1 - 1));
+            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd220)}}, (first_server(prm) + 1 - 1));
           }
           if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd41)}}, (first_server(prm) + 2 - 1));
+            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd220)}}, (first_server(prm) + 2 - 1));
           }
           if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd41)}}, (first_server(prm) + 3 - 1));
+            ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd220)}}, (first_server(prm) + 3 - 1));
           }
         }
         if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
@@ -317,40 +317,40 @@ struct N_server : Node {
         }
         const int l_v = (p1bvotes | (1 << (from - (first_server(prm) + 1 - 1))));
         p1bvotes = l_v;
-        const int l_me42 = std::stoi(m.f[2]);
-        const int l_mm43 = p1blog[0];
-        if (((l_me42 & 3) == 2)) {
-          p1blog[0] = ((2 | (0 << 2)) | (((l_me42 >> 8) & 7) << 8));
+        const int l_me221 = std::stoi(m.f[2]);
+        const int l_mm222 = p1blog[0];
+        if (((l_me221 & 3) == 2)) {
+          p1blog[0] = ((2 | (0 << 2)) | (((l_me221 >> 8) & 7) << 8));
         } else {
-          if (((((l_me42 & 3) == 1) && ((l_mm43 & 3) != 2)) && (((l_mm43 & 3) == 0) || (((l_mm43 >> 2) & 63) < ((l_me42 >> 2) & 63))))) {
-            p1blog[0] = l_me42;
+          if (((((l_me221 & 3) == 1) && ((l_mm222 & 3) != 2)) && (((l_mm222 & 3) == 0) || (((l_mm222 >> 2) & 63) < ((l_me221 >> 2) & 63))))) {
+            p1blog[0] = l_me221;
           }
         }
-        const int l_me44 = std::stoi(m.f[3]);
-        const int l_mm45 = p1blog[1];
-        if (((l_me44 & 3) == 2)) {
-          p1blog[1] = ((2 | (0 << 2)) | (((l_me44 >> 8) & 7) << 8));
+        const int l_me223 = std::stoi(m.f[3]);
+        const int l_mm224 = p1blog[1];
+        if (((l_me223 & 3) == 2)) {
+          p1blog[1] = ((2 | (0 << 2)) | (((l_me223 >> 8) & 7) << 8));
         } else {
-          if (((((l_me44 & 3) == 1) && ((l_mm45 & 3) != 2)) && (((l_mm45 & 3) == 0) || (((l_mm45 >> 2) & 63) < ((l_me44 >> 2) & 63))))) {
-            p1blog[1] = l_me44;
+          if (((((l_me223 & 3) == 1) && ((l_mm224 & 3) != 2)) && (((l_mm224 & 3) == 0) || (((l_mm224 >> 2) & 63) < ((l_me223 >> 2) & 63))))) {
+            p1blog[1] = l_me223;
           }
         }
-        const int l_me46 = std::stoi(m.f[4]);
-        const int l_mm47 = p1blog[2];
-        if (((l_me46 & 3) == 2)) {
-          p1blog[2] = ((2 | (0 << 2)) | (((l_me46 >> 8) & 7) << 8));
+        const int l_me225 = std::stoi(m.f[4]);
+        const int l_mm226 = p1blog[2];
+        if (((l_me225 & 3) == 2)) {
+          p1blog[2] = ((2 | (0 << 2)) | (((l_me225 >> 8) & 7) << 8));
         } else {
-          if (((((l_me46 & 3) == 1) && ((l_mm47 & 3) != 2)) && (((l_mm47 & 3) == 0) || (((l_mm47 >> 2) & 63) < ((l_me46 >> 2) & 63))))) {
-            p1blog[2] = l_me46;
+          if (((((l_me225 & 3) == 1) && ((l_mm226 & 3) != 2)) && (((l_mm226 & 3) == 0) || (((l_mm226 >> 2) & 63) < ((l_me225 >> 2) & 63))))) {
+            p1blog[2] = l_me225;
           }
         }
-        const int l_me48 = std::stoi(m.f[5]);
-        const int l_mm49 = p1blog[3];
-        if (((l_me48 & 3) == 2)) {
-          p1blog[3] = ((2 | (0 << 2)) | (((l_me48 >> 8) & 7) << 8));
+        const int l_me227 = std::stoi(m.f[5]);
+        const int l_mm228 = p1blog[3];
+        if (((l_me227 & 3) == 2)) {
+          p1blog[3] = ((2 | (0 << 2)) | (((l_me227 >> 8) & 7) << 8));
         } else {
-          if (((((l_me48 & 3) == 1) && ((l_mm49 & 3) != 2)) && (((l_mm49 & 3) == 0) || (((l_mm49 >> 2) & 63) < ((l_me48 >> 2) & 63))))) {
-            p1blog[3] = l_me48;
+          if (((((l_me227 & 3) == 1) && ((l_mm228 & 3) != 2)) && (((l_mm228 & 3) == 0) || (((l_mm228 >> 2) & 63) < ((l_me227 >> 2) & 63))))) {
+            p1blog[3] = l_me227;
           }
         }
         if ((!(((((l_v & 1) + ((l_v >> 1) & 1)) + ((l_v >> 2) & 1)) * 2) > prm.servers))) {
@@ -402,17 +402,17 @@ struct N_server : Node {
         if ((!(((((l_v & 1) + ((l_v >> 1) & 1)) + ((l_v >> 2) & 1)) * 2) > prm.servers))) {
           return;
         }
-        const int l_ccmd50 = ((log[(l_slot - 1)] >> 8) & 7);
-        log[(l_slot - 1)] = ((2 | (0 << 2)) | (l_ccmd50 << 8));
+        const int l_ccmd229 = ((log[(l_slot - 1)] >> 8) & 7);
+        log[(l_slot - 1)] = ((2 | (0 << 2)) | (l_ccmd229 << 8));
         votes[(l_slot - 1)] = 0;
         if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd50)}}, (first_server(prm) + 1 - 1));
+          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd229)}}, (first_server(prm) + 1 - 1));
         }
         if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd50)}}, (first_server(prm) + 2 - 1));
+          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd229)}}, (first_server(prm) + 2 - 1));
         }
         if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd50)}}, (first_server(prm) + 3 - 1));
+          ctx.send(Rec{"Decision", {std::to_string(l_slot), std::to_string(l_ccmd229)}}, (first_server(prm) + 3 - 1));
         }
         fl_ |= 1;
       }();
@@ -460,309 +460,309 @@ struct N_server : Node {
         active = 1;
         electing = 0;
         p1bvotes = 0;
-        const int l_mg51 = p1blog[0];
-        const int l_mg52 = p1blog[1];
-        const int l_mg53 = p1blog[2];
-        const int l_mg54 = p1blog[3];
-        int l_last55 = 0;
-        if ((((l_mg51 & 3) != 0) || ((log[0] & 3) != 0))) {
-          l_last55 = 1;
+        const int l_mg230 = p1blog[0];
+        const int l_mg231 = p1blog[1];
+        const int l_mg232 = p1blog[2];
+        const int l_mg233 = p1blog[3];
+        int l_last234 = 0;
+        if ((((l_mg230 & 3) != 0) || ((log[0] & 3) != 0))) {
+          l_last234 = 1;
         }
-        if ((((l_mg52 & 3) != 0) || ((log[1] & 3) != 0))) {
-          l_last55 = 2;
+        if ((((l_mg231 & 3) != 0) || ((log[1] & 3) != 0))) {
+          l_last234 = 2;
         }
-        if ((((l_mg53 & 3) != 0) || ((log[2] & 3) != 0))) {
-          l_last55 = 3;
+        if ((((l_mg232 & 3) != 0) || ((log[2] & 3) != 0))) {
+          l_last234 = 3;
         }
-        if ((((l_mg54 & 3) != 0) || ((log[3] & 3) != 0))) {
-          l_last55 = 4;
+        if ((((l_mg233 & 3) != 0) || ((log[3] & 3) != 0))) {
+          l_last234 = 4;
         }
         p1blog[0] = 0;
         p1blog[1] = 0;
         p1blog[2] = 0;
         p1blog[3] = 0;
-        if (((1 <= l_last55) && ((log[0] & 3) != 2))) {
-          if (((l_mg51 & 3) == 2)) {
-            log[0] = ((2 | (0 << 2)) | (((l_mg51 >> 8) & 7) << 8));
+        if (((1 <= l_last234) && ((log[0] & 3) != 2))) {
+          if (((l_mg230 & 3) == 2)) {
+            log[0] = ((2 | (0 << 2)) | (((l_mg230 >> 8) & 7) << 8));
             votes[0] = 0;
           } else {
-            log[(1 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg51 & 3) == 1) ? ((l_mg51 >> 8) & 7) : 0) << 8));
+            log[(1 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg230 & 3) == 1) ? ((l_mg230 >> 8) & 7) : 0) << 8));
             votes[(1 - 1)] = (1 << (self - first_server(prm)));
             if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg51 & 3) == 1) ? ((l_mg51 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg230 & 3) == 1) ? ((l_mg230 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
             }
             if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg51 & 3) == 1) ? ((l_mg51 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg230 & 3) == 1) ? ((l_mg230 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
             }
             if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg51 & 3) == 1) ? ((l_mg51 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg230 & 3) == 1) ? ((l_mg230 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
             }
             if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-              const int l_ccmd56 = ((log[(1 - 1)] >> 8) & 7);
-              log[(1 - 1)] = ((2 | (0 << 2)) | (l_ccmd56 << 8));
+              const int l_ccmd235 = ((log[(1 - 1)] >> 8) & 7);
+              log[(1 - 1)] = ((2 | (0 << 2)) | (l_ccmd235 << 8));
               votes[(1 - 1)] = 0;
               if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd56)}}, (first_server(prm) + 1 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd235)}}, (first_server(prm) + 1 - 1));
               }
               if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd56)}}, (first_server(prm) + 2 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd235)}}, (first_server(prm) + 2 - 1));
               }
               if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd56)}}, (first_server(prm) + 3 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd235)}}, (first_server(prm) + 3 - 1));
               }
             }
           }
         }
-        if (((2 <= l_last55) && ((log[1] & 3) != 2))) {
-          if (((l_mg52 & 3) == 2)) {
-            log[1] = ((2 | (0 << 2)) | (((l_mg52 >> 8) & 7) << 8));
+        if (((2 <= l_last234) && ((log[1] & 3) != 2))) {
+          if (((l_mg231 & 3) == 2)) {
+            log[1] = ((2 | (0 << 2)) | (((l_mg231 >> 8) & 7) << 8));
             votes[1] = 0;
           } else {
-            log[(2 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg52 & 3) == 1) ? ((l_mg52 >> 8) & 7) : 0) << 8));
+            log[(2 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg231 & 3) == 1) ? ((l_mg231 >> 8) & 7) : 0) << 8));
             votes[(2 - 1)] = (1 << (self - first_server(prm)));
             if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg52 & 3) == 1) ? ((l_mg52 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg231 & 3) == 1) ? ((l_mg231 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
             }
             if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg52 & 3) == 1) ? ((l_mg52 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg231 & 3) == 1) ? ((l_mg231 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
             }
             if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg52 & 3) == 1) ? ((l_mg52 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg231 & 3) == 1) ? ((l_mg231 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
             }
             if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-              const int l_ccmd57 = ((log[(2 - 1)] >> 8) & 7);
-              log[(2 - 1)] = ((2 | (0 << 2)) | (l_ccmd57 << 8));
+              const int l_ccmd236 = ((log[(2 - 1)] >> 8) & 7);
+              log[(2 - 1)] = ((2 | (0 << 2)) | (l_ccmd236 << 8));
               votes[(2 - 1)] = 0;
               if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd57)}}, (first_server(prm) + 1 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd236)}}, (first_server(prm) + 1 - 1));
               }
               if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd57)}}, (first_server(prm) + 2 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd236)}}, (first_server(prm) + 2 - 1));
               }
               if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd57)}}, (first_server(prm) + 3 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd236)}}, (first_server(prm) + 3 - 1));
               }
             }
           }
         }
-        if (((3 <= l_last55) && ((log[2] & 3) != 2))) {
-          if (((l_mg53 & 3) == 2)) {
-            log[2] = ((2 | (0 << 2)) | (((l_mg53 >> 8) & 7) << 8));
+        if (((3 <= l_last234) && ((log[2] & 3) != 2))) {
+          if (((l_mg232 & 3) == 2)) {
+            log[2] = ((2 | (0 << 2)) | (((l_mg232 >> 8) & 7) << 8));
             votes[2] = 0;
           } else {
-            log[(3 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg53 & 3) == 1) ? ((l_mg53 >> 8) & 7) : 0) << 8));
+            log[(3 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg232 & 3) == 1) ? ((l_mg232 >> 8) & 7) : 0) << 8));
             votes[(3 - 1)] = (1 << (self - first_server(prm)));
             if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg53 & 3) == 1) ? ((l_mg53 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg232 & 3) == 1) ? ((l_mg232 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
             }
             if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg53 & 3) == 1) ? ((l_mg53 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg232 & 3) == 1) ? ((l_mg232 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
             }
             if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg53 & 3) == 1) ? ((l_mg53 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg232 & 3) == 1) ? ((l_mg232 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
             }
             if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-              const int l_ccmd58 = ((log[(3 - 1)] >> 8) & 7);
-              log[(3 - 1)] = ((2 | (0 << 2)) | (l_ccmd58 << 8));
+              const int l_ccmd237 = ((log[(3 - 1)] >> 8) & 7);
+              log[(3 - 1)] = ((2 | (0 << 2)) | (l_ccmd237 << 8));
               votes[(3 - 1)] = 0;
               if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd58)}}, (first_server(prm) + 1 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd237)}}, (first_server(prm) + 1 - 1));
               }
               if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd58)}}, (first_server(prm) + 2 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd237)}}, (first_server(prm) + 2 - 1));
               }
               if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd58)}}, (first_server(prm) + 3 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd237)}}, (first_server(prm) + 3 - 1));
               }
             }
           }
         }
-        if (((4 <= l_last55) && ((log[3] & 3) != 2))) {
-          if (((l_mg54 & 3) == 2)) {
-            log[3] = ((2 | (0 << 2)) | (((l_mg54 >> 8) & 7) << 8));
+        if (((4 <= l_last234) && ((log[3] & 3) != 2))) {
+          if (((l_mg233 & 3) == 2)) {
+            log[3] = ((2 | (0 << 2)) | (((l_mg233 >> 8) & 7) << 8));
             votes[3] = 0;
           } else {
-            log[(4 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg54 & 3) == 1) ? ((l_mg54 >> 8) & 7) : 0) << 8));
+            log[(4 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg233 & 3) == 1) ? ((l_mg233 >> 8) & 7) : 0) << 8));
             votes[(4 - 1)] = (1 << (self - first_server(prm)));
             if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg54 & 3) == 1) ? ((l_mg54 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg233 & 3) == 1) ? ((l_mg233 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
             }
             if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg54 & 3) == 1) ? ((l_mg54 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg233 & 3) == 1) ? ((l_mg233 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
             }
             if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg54 & 3) == 1) ? ((l_mg54 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+              ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg233 & 3) == 1) ? ((l_mg233 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
             }
             if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-              const int l_ccmd59 = ((log[(4 - 1)] >> 8) & 7);
-              log[(4 - 1)] = ((2 | (0 << 2)) | (l_ccmd59 << 8));
+              const int l_ccmd238 = ((log[(4 - 1)] >> 8) & 7);
+              log[(4 - 1)] = ((2 | (0 << 2)) | (l_ccmd238 << 8));
               votes[(4 - 1)] = 0;
               if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd59)}}, (first_server(prm) + 1 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd238)}}, (first_server(prm) + 1 - 1));
               }
               if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd59)}}, (first_server(prm) + 2 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd238)}}, (first_server(prm) + 2 - 1));
               }
               if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd59)}}, (first_server(prm) + 3 - 1));
+                ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd238)}}, (first_server(prm) + 3 - 1));
               }
             }
           }
         }
-        slotin = (l_last55 + 1);
+        slotin = (l_last234 + 1);
       }
-      const int l_so060 = slotout;
-      const int l_act61 = active;
-      int l_kv62 = 0;
-      int l_ls063 = 0;
-      int l_ls164 = 0;
-      int l_so65 = l_so060;
-      int l_run66 = 1;
-      const int l_e67 = log[0];
-      const int l_cmd68 = ((l_e67 >> 8) & 7);
-      const int l_c69 = ((l_cmd68 >= 4) ? 1 : 0);
-      const int l_q70 = (l_cmd68 - (((l_cmd68 >= 4) ? 1 : 0) * 3));
-      const int l_before71 = (1 < l_so060);
-      const int l_now72 = (((!l_before71) && (l_run66 != 0)) && ((l_e67 & 3) == 2));
-      l_run66 = (((l_run66 != 0) && (l_before71 || l_now72)) ? 1 : 0);
-      if ((((l_before71 || l_now72) && (l_cmd68 != 0)) && ((l_c69 ? l_ls164 : l_ls063) < l_q70))) {
-        const int l_c73 = ((l_cmd68 >= 4) ? 1 : 0);
-        const int l_op74 = prm.op[l_c73][((l_cmd68 - (((l_cmd68 >= 4) ? 1 : 0) * 3)) - 1)];
-        const int l_v75 = prm.val[l_c73][((l_cmd68 - (((l_cmd68 >= 4) ? 1 : 0) * 3)) - 1)];
-        int l_x76 = 0;
-        if ((l_op74 == 1)) {
-          l_kv62 = (1 | (l_v75 << 3));
-          l_x76 = 7;
+      const int l_so0239 = slotout;
+      const int l_act240 = active;
+      int l_kv241 = 0;
+      int l_ls0242 = 0;
+      int l_ls1243 = 0;
+      int l_so244 = l_so0239;
+      int l_run245 = 1;
+      const int l_e246 = log[0];
+      const int l_cmd247 = ((l_e246 >> 8) & 7);
+      const int l_c248 = ((l_cmd247 >= 4) ? 1 : 0);
+      const int l_q249 = (l_cmd247 - (((l_cmd247 >= 4) ? 1 : 0) * 3));
+      const int l_before250 = (1 < l_so0239);
+      const int l_now251 = (((!l_before250) && (l_run245 != 0)) && ((l_e246 & 3) == 2));
+      l_run245 = (((l_run245 != 0) && (l_before250 || l_now251)) ? 1 : 0);
+      if ((((l_before250 || l_now251) && (l_cmd247 != 0)) && ((l_c248 ? l_ls1243 : l_ls0242) < l_q249))) {
+        const int l_c252 = ((l_cmd247 >= 4) ? 1 : 0);
+        const int l_op253 = prm.op[l_c252][((l_cmd247 - (((l_cmd247 >= 4) ? 1 : 0) * 3)) - 1)];
+        const int l_v254 = prm.val[l_c252][((l_cmd247 - (((l_cmd247 >= 4) ? 1 : 0) * 3)) - 1)];
+        int l_x255 = 0;
+        if ((l_op253 == 1)) {
+          l_kv241 = (1 | (l_v254 << 3));
+          l_x255 = 7;
         }
-        if ((l_op74 == 2)) {
-          const int l_len77 = (l_kv62 & 7);
-          l_kv62 = (((l_len77 + 1) | (l_kv62 & -8)) | (l_v75 << (3 + (l_len77 * 2))));
-          l_x76 = l_kv62;
+        if ((l_op253 == 2)) {
+          const int l_len256 = (l_kv241 & 7);
+          l_kv241 = (((l_len256 + 1) | (l_kv241 & -8)) | (l_v254 << (3 + (l_len256 * 2))));
+          l_x255 = l_kv241;
         }
-        if ((l_op74 == 3)) {
-          l_x76 = (((l_kv62 & 7) != 0) ? l_kv62 : 6);
+        if ((l_op253 == 3)) {
+          l_x255 = (((l_kv241 & 7) != 0) ? l_kv241 : 6);
         }
-        if ((l_c69 != 0)) {
-          l_ls164 = l_q70;
+        if ((l_c248 != 0)) {
+          l_ls1243 = l_q249;
         } else {
-          l_ls063 = l_q70;
+          l_ls0242 = l_q249;
         }
-        if ((l_now72 && (l_act61 != 0))) {
-          ctx.send(Rec{"Reply", {std::to_string(l_q70), std::to_string(l_x76)}}, (first_client(prm) + (l_c69 + 1) - 1));
+        if ((l_now251 && (l_act240 != 0))) {
+          ctx.send(Rec{"Reply", {std::to_string(l_q249), std::to_string(l_x255)}}, (first_client(prm) + (l_c248 + 1) - 1));
         }
       }
-      if (l_now72) {
-        l_so65 = 2;
+      if (l_now251) {
+        l_so244 = 2;
       }
-      const int l_e78 = log[1];
-      const int l_cmd79 = ((l_e78 >> 8) & 7);
-      const int l_c80 = ((l_cmd79 >= 4) ? 1 : 0);
-      const int l_q81 = (l_cmd79 - (((l_cmd79 >= 4) ? 1 : 0) * 3));
-      const int l_before82 = (2 < l_so060);
-      const int l_now83 = (((!l_before82) && (l_run66 != 0)) && ((l_e78 & 3) == 2));
-      l_run66 = (((l_run66 != 0) && (l_before82 || l_now83)) ? 1 : 0);
-      if ((((l_before82 || l_now83) && (l_cmd79 != 0)) && ((l_c80 ? l_ls164 : l_ls063) < l_q81))) {
-        const int l_c84 = ((l_cmd79 >= 4) ? 1 : 0);
-        const int l_op85 = prm.op[l_c84][((l_cmd79 - (((l_cmd79 >= 4) ? 1 : 0) * 3)) - 1)];
-        const int l_v86 = prm.val[l_c84][((l_cmd79 - (((l_cmd79 >= 4) ? 1 : 0) * 3)) - 1)];
-        int l_x87 = 0;
-        if ((l_op85 == 1)) {
-          l_kv62 = (1 | (l_v86 << 3));
-          l_x87 = 7;
+      const int l_e257 = log[1];
+      const int l_cmd258 = ((l_e257 >> 8) & 7);
+      const int l_c259 = ((l_cmd258 >= 4) ? 1 : 0);
+      const int l_q260 = (l_cmd258 - (((l_cmd258 >= 4) ? 1 : 0) * 3));
+      const int l_before261 = (2 < l_so0239);
+      const int l_now262 = (((!l_before261) && (l_run245 != 0)) && ((l_e257 & 3) == 2));
+      l_run245 = (((l_run245 != 0) && (l_before261 || l_now262)) ? 1 : 0);
+      if ((((l_before261 || l_now262) && (l_cmd258 != 0)) && ((l_c259 ? l_ls1243 : l_ls0242) < l_q260))) {
+        const int l_c263 = ((l_cmd258 >= 4) ? 1 : 0);
+        const int l_op264 = prm.op[l_c263][((l_cmd258 - (((l_cmd258 >= 4) ? 1 : 0) * 3)) - 1)];
+        const int l_v265 = prm.val[l_c263][((l_cmd258 - (((l_cmd258 >= 4) ? 1 : 0) * 3)) - 1)];
+        int l_x266 = 0;
+        if ((l_op264 == 1)) {
+          l_kv241 = (1 | (l_v265 << 3));
+          l_x266 = 7;
         }
-        if ((l_op85 == 2)) {
-          const int l_len88 = (l_kv62 & 7);
-          l_kv62 = (((l_len88 + 1) | (l_kv62 & -8)) | (l_v86 << (3 + (l_len88 * 2))));
-          l_x87 = l_kv62;
+        if ((l_op264 == 2)) {
+          const int l_len267 = (l_kv241 & 7);
+          l_kv241 = (((l_len267 + 1) | (l_kv241 & -8)) | (l_v265 << (3 + (l_len267 * 2))));
+          l_x266 = l_kv241;
         }
-        if ((l_op85 == 3)) {
-          l_x87 = (((l_kv62 & 7) != 0) ? l_kv62 : 6);
+        if ((l_op264 == 3)) {
+          l_x266 = (((l_kv241 & 7) != 0) ? l_kv241 : 6);
         }
-        if ((l_c80 != 0)) {
-          l_ls164 = l_q81;
+        if ((l_c259 != 0)) {
+          l_ls1243 = l_q260;
         } else {
-          l_ls063 = l_q81;
+          l_ls0242 = l_q260;
         }
-        if ((l_now83 && (l_act61 != 0))) {
-          ctx.send(Rec{"Reply", {std::to_string(l_q81), std::to_string(l_x87)}}, (first_client(prm) + (l_c80 + 1) - 1));
+        if ((l_now262 && (l_act240 != 0))) {
+          ctx.send(Rec{"Reply", {std::to_string(l_q260), std::to_string(l_x266)}}, (first_client(prm) + (l_c259 + 1) - 1));
         }
       }
-      if (l_now83) {
-        l_so65 = 3;
+      if (l_now262) {
+        l_so244 = 3;
       }
-      const int l_e89 = log[2];
-      const int l_cmd90 = ((l_e89 >> 8) & 7);
-      const int l_c91 = ((l_cmd90 >= 4) ? 1 : 0);
-      const int l_q92 = (l_cmd90 - (((l_cmd90 >= 4) ? 1 : 0) * 3));
-      const int l_before93 = (3 < l_so060);
-      const int l_now94 = (((!l_before93) && (l_run66 != 0)) && ((l_e89 & 3) == 2));
-      l_run66 = (((l_run66 != 0) && (l_before93 || l_now94)) ? 1 : 0);
-      if ((((l_before93 || l_now94) && (l_cmd90 != 0)) && ((l_c91 ? l_ls164 : l_ls063) < l_q92))) {
-        const int l_c95 = ((l_cmd90 >= 4) ? 1 : 0);
-        const int l_op96 = prm.op[l_c95][((l_cmd90 - (((l_cmd90 >= 4) ? 1 : 0) * 3)) - 1)];
-        const int l_v97 = prm.val[l_c95][((l_cmd90 - (((l_cmd90 >= 4) ? 1 : 0) * 3)) - 1)];
-        int l_x98 = 0;
-        if ((l_op96 == 1)) {
-          l_kv62 = (1 | (l_v97 << 3));
-          l_x98 = 7;
+      const int l_e268 = log[2];
+      const int l_cmd269 = ((l_e268 >> 8) & 7);
+      const int l_c270 = ((l_cmd269 >= 4) ? 1 : 0);
+      const int l_q271 = (l_cmd269 - (((l_cmd269 >= 4) ? 1 : 0) * 3));
+      const int l_before272 = (3 < l_so0239);
+      const int l_now273 = (((!l_before272) && (l_run245 != 0)) && ((l_e268 & 3) == 2));
+      l_run245 = (((l_run245 != 0) && (l_before272 || l_now273)) ? 1 : 0);
+      if ((((l_before272 || l_now273) && (l_cmd269 != 0)) && ((l_c270 ? l_ls1243 : l_ls0242) < l_q271))) {
+        const int l_c274 = ((l_cmd269 >= 4) ? 1 : 0);
+        const int l_op275 = prm.op[l_c274][((l_cmd269 - (((l_cmd269 >= 4) ? 1 : 0) * 3)) - 1)];
+        const int l_v276 = prm.val[l_c274][((l_cmd269 - (((l_cmd269 >= 4) ? 1 : 0) * 3)) - 1)];
+        int l_x277 = 0;
+        if ((l_op275 == 1)) {
+          l_kv241 = (1 | (l_v276 << 3));
+          l_x277 = 7;
         }
-        if ((l_op96 == 2)) {
-          const int l_len99 = (l_kv62 & 7);
-          l_kv62 = (((l_len99 + 1) | (l_kv62 & -8)) | (l_v97 << (3 + (l_len99 * 2))));
-          l_x98 = l_kv62;
+        if ((l_op275 == 2)) {
+          const int l_len278 = (l_kv241 & 7);
+          l_kv241 = (((l_len278 + 1) | (l_kv241 & -8)) | (l_v276 << (3 + (l_len278 * 2))));
+          l_x277 = l_kv241;
         }
-        if ((l_op96 == 3)) {
-          l_x98 = (((l_kv62 & 7) != 0) ? l_kv62 : 6);
+        if ((l_op275 == 3)) {
+          l_x277 = (((l_kv241 & 7) != 0) ? l_kv241 : 6);
         }
-        if ((l_c91 != 0)) {
-          l_ls164 = l_q92;
+        if ((l_c270 != 0)) {
+          l_ls1243 = l_q271;
         } else {
-          l_ls063 = l_q92;
+          l_ls0242 = l_q271;
         }
-        if ((l_now94 && (l_act61 != 0))) {
-          ctx.send(Rec{"Reply", {std::to_string(l_q92), std::to_string(l_x98)}}, (first_client(prm) + (l_c91 + 1) - 1));
+        if ((l_now273 && (l_act240 != 0))) {
+          ctx.send(Rec{"Reply", {std::to_string(l_q271), std::to_string(l_x277)}}, (first_client(prm) + (l_c270 + 1) - 1));
         }
       }
-      if (l_now94) {
-        l_so65 = 4;
+      if (l_now273) {
+        l_so244 = 4;
       }
-      const int l_e100 = log[3];
-      const int l_cmd101 = ((l_e100 >> 8) & 7);
-      const int l_c102 = ((l_cmd101 >= 4) ? 1 : 0);
-      const int l_q103 = (l_cmd101 - (((l_cmd101 >= 4) ? 1 : 0) * 3));
-      const int l_before104 = (4 < l_so060);
-      const int l_now105 = (((!l_before104) && (l_run66 != 0)) && ((l_e100 & 3) == 2));
-      l_run66 = (((l_run66 != 0) && (l_before104 || l_now105)) ? 1 : 0);
-      if ((((l_before104 || l_now105) && (l_cmd101 != 0)) && ((l_c102 ? l_ls164 : l_ls063) < l_q103))) {
-        const int l_c106 = ((l_cmd101 >= 4) ? 1 : 0);
-        const int l_op107 = prm.op[l_c106][((l_cmd101 - (((l_cmd101 >= 4) ? 1 : 0) * 3)) - 1)];
-        const int l_v108 = prm.val[l_c106][((l_cmd101 - (((l_cmd101 >= 4) ? 1 : 0) * 3)) - 1)];
-        int l_x109 = 0;
-        if ((l_op107 == 1)) {
-          l_kv62 = (1 | (l_v108 << 3));
-          l_x109 = 7;
+      const int l_e279 = log[3];
+      const int l_cmd280 = ((l_e279 >> 8) & 7);
+      const int l_c281 = ((l_cmd280 >= 4) ? 1 : 0);
+      const int l_q282 = (l_cmd280 - (((l_cmd280 >= 4) ? 1 : 0) * 3));
+      const int l_before283 = (4 < l_so0239);
+      const int l_now284 = (((!l_before283) && (l_run245 != 0)) && ((l_e279 & 3) == 2));
+      l_run245 = (((l_run245 != 0) && (l_before283 || l_now284)) ? 1 : 0);
+      if ((((l_before283 || l_now284) && (l_cmd280 != 0)) && ((l_c281 ? l_ls1243 : l_ls0242) < l_q282))) {
+        const int l_c285 = ((l_cmd280 >= 4) ? 1 : 0);
+        const int l_op286 = prm.op[l_c285][((l_cmd280 - (((l_cmd280 >= 4) ? 1 : 0) * 3)) - 1)];
+        const int l_v287 = prm.val[l_c285][((l_cmd280 - (((l_cmd280 >= 4) ? 1 : 0) * 3)) - 1)];
+        int l_x288 = 0;
+        if ((l_op286 == 1)) {
+          l_kv241 = (1 | (l_v287 << 3));
+          l_x288 = 7;
         }
-        if ((l_op107 == 2)) {
-          const int l_len110 = (l_kv62 & 7);
-          l_kv62 = (((l_len110 + 1) | (l_kv62 & -8)) | (l_v108 << (3 + (l_len110 * 2))));
-          l_x109 = l_kv62;
+        if ((l_op286 == 2)) {
+          const int l_len289 = (l_kv241 & 7);
+          l_kv241 = (((l_len289 + 1) | (l_kv241 & -8)) | (l_v287 << (3 + (l_len289 * 2))));
+          l_x288 = l_kv241;
         }
-        if ((l_op107 == 3)) {
-          l_x109 = (((l_kv62 & 7) != 0) ? l_kv62 : 6);
+        if ((l_op286 == 3)) {
+          l_x288 = (((l_kv241 & 7) != 0) ? l_kv241 : 6);
         }
-        if ((l_c102 != 0)) {
-          l_ls164 = l_q103;
+        if ((l_c281 != 0)) {
+          l_ls1243 = l_q282;
         } else {
-          l_ls063 = l_q103;
+          l_ls0242 = l_q282;
         }
-        if ((l_now105 && (l_act61 != 0))) {
-          ctx.send(Rec{"Reply", {std::to_string(l_q103), std::to_string(l_x109)}}, (first_client(prm) + (l_c102 + 1) - 1));
+        if ((l_now284 && (l_act240 != 0))) {
+          ctx.send(Rec{"Reply", {std::to_string(l_q282), std::to_string(l_x288)}}, (first_client(prm) + (l_c281 + 1) - 1));
         }
       }
-      if (l_now105) {
-        l_so65 = 5;
+      if (l_now284) {
+        l_so244 = 5;
       }
-      slotout = l_so65;
+      slotout = l_so244;
     }
   }
   void onTimer(const Rec& t, Ctx& ctx) override {
@@ -801,40 +801,40 @@ struct N_server : Node {
             votes[3] = 0;
             p1blog[3] = 0;
             p1bvotes = (1 << (self - first_server(prm)));
-            const int l_me111 = log[0];
-            const int l_mm112 = p1blog[0];
-            if (((l_me111 & 3) == 2)) {
-              p1blog[0] = ((2 | (0 << 2)) | (((l_me111 >> 8) & 7) << 8));
+            const int l_me290 = log[0];
+            const int l_mm291 = p1blog[0];
+            if (((l_me290 & 3) == 2)) {
+              p1blog[0] = ((2 | (0 << 2)) | (((l_me290 >> 8) & 7) << 8));
             } else {
-              if (((((l_me111 & 3) == 1) && ((l_mm112 & 3) != 2)) && (((l_mm112 & 3) == 0) || (((l_mm112 >> 2) & 63) < ((l_me111 >> 2) & 63))))) {
-                p1blog[0] = l_me111;
+              if (((((l_me290 & 3) == 1) && ((l_mm291 & 3) != 2)) && (((l_mm291 & 3) == 0) || (((l_mm291 >> 2) & 63) < ((l_me290 >> 2) & 63))))) {
+                p1blog[0] = l_me290;
               }
             }
-            const int l_me113 = log[1];
-            const int l_mm114 = p1blog[1];
-            if (((l_me113 & 3) == 2)) {
-              p1blog[1] = ((2 | (0 << 2)) | (((l_me113 >> 8) & 7) << 8));
+            const int l_me292 = log[1];
+            const int l_mm293 = p1blog[1];
+            if (((l_me292 & 3) == 2)) {
+              p1blog[1] = ((2 | (0 << 2)) | (((l_me292 >> 8) & 7) << 8));
             } else {
-              if (((((l_me113 & 3) == 1) && ((l_mm114 & 3) != 2)) && (((l_mm114 & 3) == 0) || (((l_mm114 >> 2) & 63) < ((l_me113 >> 2) & 63))))) {
-                p1blog[1] = l_me113;
+              if (((((l_me292 & 3) == 1) && ((l_mm293 & 3) != 2)) && (((l_mm293 & 3) == 0) || (((l_mm293 >> 2) & 63) < ((l_me292 >> 2) & 63))))) {
+                p1blog[1] = l_me292;
               }
             }
-            const int l_me115 = log[2];
-            const int l_mm116 = p1blog[2];
-            if (((l_me115 & 3) == 2)) {
-              p1blog[2] = ((2 | (0 << 2)) | (((l_me115 >> 8) & 7) << 8));
+            const int l_me294 = log[2];
+            const int l_mm295 = p1blog[2];
+            if (((l_me294 & 3) == 2)) {
+              p1blog[2] = ((2 | (0 << 2)) | (((l_me294 >> 8) & 7) << 8));
             } else {
-              if (((((l_me115 & 3) == 1) && ((l_mm116 & 3) != 2)) && (((l_mm116 & 3) == 0) || (((l_mm116 >> 2) & 63) < ((l_me115 >> 2) & 63))))) {
-                p1blog[2] = l_me115;
+              if (((((l_me294 & 3) == 1) && ((l_mm295 & 3) != 2)) && (((l_mm295 & 3) == 0) || (((l_mm295 >> 2) & 63) < ((l_me294 >> 2) & 63))))) {
+                p1blog[2] = l_me294;
               }
             }
-            const int l_me117 = log[3];
-            const int l_mm118 = p1blog[3];
-            if (((l_me117 & 3) == 2)) {
-              p1blog[3] = ((2 | (0 << 2)) | (((l_me117 >> 8) & 7) << 8));
+            const int l_me296 = log[3];
+            const int l_mm297 = p1blog[3];
+            if (((l_me296 & 3) == 2)) {
+              p1blog[3] = ((2 | (0 << 2)) | (((l_me296 >> 8) & 7) << 8));
             } else {
-              if (((((l_me117 & 3) == 1) && ((l_mm118 & 3) != 2)) && (((l_mm118 & 3) == 0) || (((l_mm118 >> 2) & 63) < ((l_me117 >> 2) & 63))))) {
-                p1blog[3] = l_me117;
+              if (((((l_me296 & 3) == 1) && ((l_mm297 & 3) != 2)) && (((l_mm297 & 3) == 0) || (((l_mm297 >> 2) & 63) < ((l_me296 >> 2) & 63))))) {
+                p1blog[3] = l_me296;
               }
             }
             if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
@@ -850,308 +850,308 @@ struct N_server : Node {
               active = 1;
               electing = 0;
               p1bvotes = 0;
-              const int l_mg119 = p1blog[0];
-              const int l_mg120 = p1blog[1];
-              const int l_mg121 = p1blog[2];
-              const int l_mg122 = p1blog[3];
-              int l_last123 = 0;
-              if ((((l_mg119 & 3) != 0) || ((log[0] & 3) != 0))) {
-                l_last123 = 1;
+              const int l_mg298 = p1blog[0];
+              const int l_mg299 = p1blog[1];
+              const int l_mg300 = p1blog[2];
+              const int l_mg301 = p1blog[3];
+              int l_last302 = 0;
+              if ((((l_mg298 & 3) != 0) || ((log[0] & 3) != 0))) {
+                l_last302 = 1;
               }
-              if ((((l_mg120 & 3) != 0) || ((log[1] & 3) != 0))) {
-                l_last123 = 2;
+              if ((((l_mg299 & 3) != 0) || ((log[1] & 3) != 0))) {
+                l_last302 = 2;
               }
-              if ((((l_mg121 & 3) != 0) || ((log[2] & 3) != 0))) {
-                l_last123 = 3;
+              if ((((l_mg300 & 3) != 0) || ((log[2] & 3) != 0))) {
+                l_last302 = 3;
               }
-              if ((((l_mg122 & 3) != 0) || ((log[3] & 3) != 0))) {
-                l_last123 = 4;
+              if ((((l_mg301 & 3) != 0) || ((log[3] & 3) != 0))) {
+                l_last302 = 4;
               }
               p1blog[0] = 0;
               p1blog[1] = 0;
               p1blog[2] = 0;
               p1blog[3] = 0;
-              if (((1 <= l_last123) && ((log[0] & 3) != 2))) {
-                if (((l_mg119 & 3) == 2)) {
-                  log[0] = ((2 | (0 << 2)) | (((l_mg119 >> 8) & 7) << 8));
+              if (((1 <= l_last302) && ((log[0] & 3) != 2))) {
+                if (((l_mg298 & 3) == 2)) {
+                  log[0] = ((2 | (0 << 2)) | (((l_mg298 >> 8) & 7) << 8));
                   votes[0] = 0;
                 } else {
-                  log[(1 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg119 & 3) == 1) ? ((l_mg119 >> 8) & 7) : 0) << 8));
+                  log[(1 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg298 & 3) == 1) ? ((l_mg298 >> 8) & 7) : 0) << 8));
                   votes[(1 - 1)] = (1 << (self - first_server(prm)));
                   if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg119 & 3) == 1) ? ((l_mg119 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg298 & 3) == 1) ? ((l_mg298 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
                   }
                   if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg119 & 3) == 1) ? ((l_mg119 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg298 & 3) == 1) ? ((l_mg298 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
                   }
                   if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg119 & 3) == 1) ? ((l_mg119 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(1), std::to_string((((l_mg298 & 3) == 1) ? ((l_mg298 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
                   }
                   if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-                    const int l_ccmd124 = ((log[(1 - 1)] >> 8) & 7);
-                    log[(1 - 1)] = ((2 | (0 << 2)) | (l_ccmd124 << 8));
+                    const int l_ccmd303 = ((log[(1 - 1)] >> 8) & 7);
+                    log[(1 - 1)] = ((2 | (0 << 2)) | (l_ccmd303 << 8));
                     votes[(1 - 1)] = 0;
                     if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd124)}}, (first_server(prm) + 1 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd303)}}, (first_server(prm) + 1 - 1));
                     }
                     if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd124)}}, (first_server(prm) + 2 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd303)}}, (first_server(prm) + 2 - 1));
                     }
                     if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd124)}}, (first_server(prm) + 3 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(1), std::to_string(l_ccmd303)}}, (first_server(prm) + 3 - 1));
                     }
                   }
                 }
               }
-              if (((2 <= l_last123) && ((log[1] & 3) != 2))) {
-                if (((l_mg120 & 3) == 2)) {
-                  log[1] = ((2 | (0 << 2)) | (((l_mg120 >> 8) & 7) << 8));
+              if (((2 <= l_last302) && ((log[1] & 3) != 2))) {
+                if (((l_mg299 & 3) == 2)) {
+                  log[1] = ((2 | (0 << 2)) | (((l_mg299 >> 8) & 7) << 8));
                   votes[1] = 0;
                 } else {
-                  log[(2 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0) << 8));
+                  log[(2 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0) << 8));
                   votes[(2 - 1)] = (1 << (self - first_server(prm)));
                   if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
                   }
                   if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
                   }
                   if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg120 & 3) == 1) ? ((l_mg120 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(2), std::to_string((((l_mg299 & 3) == 1) ? ((l_mg299 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
                   }
                   if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-                    const int l_ccmd125 = ((log[(2 - 1)] >> 8) & 7);
-                    log[(2 - 1)] = ((2 | (0 << 2)) | (l_ccmd125 << 8));
+                    const int l_ccmd304 = ((log[(2 - 1)] >> 8) & 7);
+                    log[(2 - 1)] = ((2 | (0 << 2)) | (l_ccmd304 << 8));
                     votes[(2 - 1)] = 0;
                     if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd125)}}, (first_server(prm) + 1 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd304)}}, (first_server(prm) + 1 - 1));
                     }
                     if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd125)}}, (first_server(prm) + 2 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd304)}}, (first_server(prm) + 2 - 1));
                     }
                     if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd125)}}, (first_server(prm) + 3 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(2), std::to_string(l_ccmd304)}}, (first_server(prm) + 3 - 1));
                     }
                   }
                 }
               }
-              if (((3 <= l_last123) && ((log[2] & 3) != 2))) {
-                if (((l_mg121 & 3) == 2)) {
-                  log[2] = ((2 | (0 << 2)) | (((l_mg121 >> 8) & 7) << 8));
+              if (((3 <= l_last302) && ((log[2] & 3) != 2))) {
+                if (((l_mg300 & 3) == 2)) {
+                  log[2] = ((2 | (0 << 2)) | (((l_mg300 >> 8) & 7) << 8));
                   votes[2] = 0;
                 } else {
-                  log[(3 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0) << 8));
+                  log[(3 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0) << 8));
                   votes[(3 - 1)] = (1 << (self - first_server(prm)));
                   if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
                   }
                   if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
                   }
                   if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg121 & 3) == 1) ? ((l_mg121 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(3), std::to_string((((l_mg300 & 3) == 1) ? ((l_mg300 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
                   }
                   if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-                    const int l_ccmd126 = ((log[(3 - 1)] >> 8) & 7);
-                    log[(3 - 1)] = ((2 | (0 << 2)) | (l_ccmd126 << 8));
+                    const int l_ccmd305 = ((log[(3 - 1)] >> 8) & 7);
+                    log[(3 - 1)] = ((2 | (0 << 2)) | (l_ccmd305 << 8));
                     votes[(3 - 1)] = 0;
                     if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd126)}}, (first_server(prm) + 1 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd305)}}, (first_server(prm) + 1 - 1));
                     }
                     if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd126)}}, (first_server(prm) + 2 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd305)}}, (first_server(prm) + 2 - 1));
                     }
                     if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd126)}}, (first_server(prm) + 3 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(3), std::to_string(l_ccmd305)}}, (first_server(prm) + 3 - 1));
                     }
                   }
                 }
               }
-              if (((4 <= l_last123) && ((log[3] & 3) != 2))) {
-                if (((l_mg122 & 3) == 2)) {
-                  log[3] = ((2 | (0 << 2)) | (((l_mg122 >> 8) & 7) << 8));
+              if (((4 <= l_last302) && ((log[3] & 3) != 2))) {
+                if (((l_mg301 & 3) == 2)) {
+                  log[3] = ((2 | (0 << 2)) | (((l_mg301 >> 8) & 7) << 8));
                   votes[3] = 0;
                 } else {
-                  log[(4 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0) << 8));
+                  log[(4 - 1)] = ((1 | (((round << 2) | leader) << 2)) | ((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0) << 8));
                   votes[(4 - 1)] = (1 << (self - first_server(prm)));
                   if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0))}}, (first_server(prm) + 1 - 1));
                   }
                   if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0))}}, (first_server(prm) + 2 - 1));
                   }
                   if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg122 & 3) == 1) ? ((l_mg122 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
+                    ctx.send(Rec{"P2a", {std::to_string(round), std::to_string(leader), std::to_string(4), std::to_string((((l_mg301 & 3) == 1) ? ((l_mg301 >> 8) & 7) : 0))}}, (first_server(prm) + 3 - 1));
                   }
                   if (((((((1 << (self - first_server(prm))) & 1) + (((1 << (self - first_server(prm))) >> 1) & 1)) + (((1 << (self - first_server(prm))) >> 2) & 1)) * 2) > prm.servers)) {
-                    const int l_ccmd127 = ((log[(4 - 1)] >> 8) & 7);
-                    log[(4 - 1)] = ((2 | (0 << 2)) | (l_ccmd127 << 8));
+                    const int l_ccmd306 = ((log[(4 - 1)] >> 8) & 7);
+                    log[(4 - 1)] = ((2 | (0 << 2)) | (l_ccmd306 << 8));
                     votes[(4 - 1)] = 0;
                     if (((0 < prm.servers) && (0 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd127)}}, (first_server(prm) + 1 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd306)}}, (first_server(prm) + 1 - 1));
                     }
                     if (((1 < prm.servers) && (1 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd127)}}, (first_server(prm) + 2 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd306)}}, (first_server(prm) + 2 - 1));
                     }
                     if (((2 < prm.servers) && (2 != (self - first_server(prm))))) {
-                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd127)}}, (first_server(prm) + 3 - 1));
+                      ctx.send(Rec{"Decision", {std::to_string(4), std::to_string(l_ccmd306)}}, (first_server(prm) + 3 - 1));
                     }
                   }
                 }
               }
-              slotin = (l_last123 + 1);
-              const int l_so0128 = slotout;
-              const int l_act129 = active;
-              int l_kv130 = 0;
-              int l_ls0131 = 0;
-              int l_ls1132 = 0;
-              int l_so133 = l_so0128;
-              int l_run134 = 1;
-              const int l_e135 = log[0];
-              const int l_cmd136 = ((l_e135 >> 8) & 7);
-              const int l_c137 = ((l_cmd136 >= 4) ? 1 : 0);
-              const int l_q138 = (l_cmd136 - (((l_cmd136 >= 4) ? 1 : 0) * 3));
-              const int l_before139 = (1 < l_so0128);
-              const int l_now140 = (((!l_before139) && (l_run134 != 0)) && ((l_e135 & 3) == 2));
-              l_run134 = (((l_run134 != 0) && (l_before139 || l_now140)) ? 1 : 0);
-              if ((((l_before139 || l_now140) && (l_cmd136 != 0)) && ((l_c137 ? l_ls1132 : l_ls0131) < l_q138))) {
-                const int l_c141 = ((l_cmd136 >= 4) ? 1 : 0);
-                const int l_op142 = prm.op[l_c141][((l_cmd136 - (((l_cmd136 >= 4) ? 1 : 0) * 3)) - 1)];
-                const int l_v143 = prm.val[l_c141][((l_cmd136 - (((l_cmd136 >= 4) ? 1 : 0) * 3)) - 1)];
-                int l_x144 = 0;
-                if ((l_op142 == 1)) {
-                  l_kv130 = (1 | (l_v143 << 3));
-                  l_x144 = 7;
+              slotin = (l_last302 + 1);
+              const int l_so0307 = slotout;
+              const int l_act308 = active;
+              int l_kv309 = 0;
+              int l_ls0310 = 0;
+              int l_ls1311 = 0;
+              int l_so312 = l_so0307;
+              int l_run313 = 1;
+              const int l_e314 = log[0];
+              const int l_cmd315 = ((l_e314 >> 8) & 7);
+              const int l_c316 = ((l_cmd315 >= 4) ? 1 : 0);
+              const int l_q317 = (l_cmd315 - (((l_cmd315 >= 4) ? 1 : 0) * 3));
+              const int l_before318 = (1 < l_so0307);
+              const int l_now319 = (((!l_before318) && (l_run313 != 0)) && ((l_e314 & 3) == 2));
+              l_run313 = (((l_run313 != 0) && (l_before318 || l_now319)) ? 1 : 0);
+              if ((((l_before318 || l_now319) && (l_cmd315 != 0)) && ((l_c316 ? l_ls1311 : l_ls0310) < l_q317))) {
+                const int l_c320 = ((l_cmd315 >= 4) ? 1 : 0);
+                const int l_op321 = prm.op[l_c320][((l_cmd315 - (((l_cmd315 >= 4) ? 1 : 0) * 3)) - 1)];
+                const int l_v322 = prm.val[l_c320][((l_cmd315 - (((l_cmd315 >= 4) ? 1 : 0) * 3)) - 1)];
+                int l_x323 = 0;
+                if ((l_op321 == 1)) {
+                  l_kv309 = (1 | (l_v322 << 3));
+                  l_x323 = 7;
                 }
-                if ((l_op142 == 2)) {
-                  const int l_len145 = (l_kv130 & 7);
-                  l_kv130 = (((l_len145 + 1) | (l_kv130 & -8)) | (l_v143 << (3 + (l_len145 * 2))));
-                  l_x144 = l_kv130;
+                if ((l_op321 == 2)) {
+                  const int l_len324 = (l_kv309 & 7);
+                  l_kv309 = (((l_len324 + 1) | (l_kv309 & -8)) | (l_v322 << (3 + (l_len324 * 2))));
+                  l_x323 = l_kv309;
                 }
-                if ((l_op142 == 3)) {
-                  l_x144 = (((l_kv130 & 7) != 0) ? l_kv130 : 6);
+                if ((l_op321 == 3)) {
+                  l_x323 = (((l_kv309 & 7) != 0) ? l_kv309 : 6);
                 }
-                if ((l_c137 != 0)) {
-                  l_ls1132 = l_q138;
+                if ((l_c316 != 0)) {
+                  l_ls1311 = l_q317;
                 } else {
-                  l_ls0131 = l_q138;
+                  l_ls0310 = l_q317;
                 }
-                if ((l_now140 && (l_act129 != 0))) {
-                  ctx.send(Rec{"Reply", {std::to_string(l_q138), std::to_string(l_x144)}}, (first_client(prm) + (l_c137 + 1) - 1));
+                if ((l_now319 && (l_act308 != 0))) {
+                  ctx.send(Rec{"Reply", {std::to_string(l_q317), std::to_string(l_x323)}}, (first_client(prm) + (l_c316 + 1) - 1));
                 }
               }
-              if (l_now140) {
-                l_so133 = 2;
+              if (l_now319) {
+                l_so312 = 2;
               }
-              const int l_e146 = log[1];
-              const int l_cmd147 = ((l_e146 >> 8) & 7);
-              const int l_c148 = ((l_cmd147 >= 4) ? 1 : 0);
-              const int l_q149 = (l_cmd147 - (((l_cmd147 >= 4) ? 1 : 0) * 3));
-              const int l_before150 = (2 < l_so0128);
-              const int l_now151 = (((!l_before150) && (l_run134 != 0)) && ((l_e146 & 3) == 2));
-              l_run134 = (((l_run134 != 0) && (l_before150 || l_now151)) ? 1 : 0);
-              if ((((l_before150 || l_now151) && (l_cmd147 != 0)) && ((l_c148 ? l_ls1132 : l_ls0131) < l_q149))) {
-                const int l_c152 = ((l_cmd147 >= 4) ? 1 : 0);
-                const int l_op153 = prm.op[l_c152][((l_cmd147 - (((l_cmd147 >= 4) ? 1 : 0) * 3)) - 1)];
-                const int l_v154 = prm.val[l_c152][((l_cmd147 - (((l_cmd147 >= 4) ? 1 : 0) * 3)) - 1)];
-                int l_x155 = 0;
-                if ((l_op153 == 1)) {
-                  l_kv130 = (1 | (l_v154 << 3));
-                  l_x155 = 7;
+              const int l_e325 = log[1];
+              const int l_cmd326 = ((l_e325 >> 8) & 7);
+              const int l_c327 = ((l_cmd326 >= 4) ? 1 : 0);
+              const int l_q328 = (l_cmd326 - (((l_cmd326 >= 4) ? 1 : 0) * 3));
+              const int l_before329 = (2 < l_so0307);
+              const int l_now330 = (((!l_before329) && (l_run313 != 0)) && ((l_e325 & 3) == 2));
+              l_run313 = (((l_run313 != 0) && (l_before329 || l_now330)) ? 1 : 0);
+              if ((((l_before329 || l_now330) && (l_cmd326 != 0)) && ((l_c327 ? l_ls1311 : l_ls0310) < l_q328))) {
+                const int l_c331 = ((l_cmd326 >= 4) ? 1 : 0);
+                const int l_op332 = prm.op[l_c331][((l_cmd326 - (((l_cmd326 >= 4) ? 1 : 0) * 3)) - 1)];
+                const int l_v333 = prm.val[l_c331][((l_cmd326 - (((l_cmd326 >= 4) ? 1 : 0) * 3)) - 1)];
+                int l_x334 = 0;
+                if ((l_op332 == 1)) {
+                  l_kv309 = (1 | (l_v333 << 3));
+                  l_x334 = 7;
                 }
-                if ((l_op153 == 2)) {
-                  const int l_len156 = (l_kv130 & 7);
-                  l_kv130 = (((l_len156 + 1) | (l_kv130 & -8)) | (l_v154 << (3 + (l_len156 * 2))));
-                  l_x155 = l_kv130;
+                if ((l_op332 == 2)) {
+                  const int l_len335 = (l_kv309 & 7);
+                  l_kv309 = (((l_len335 + 1) | (l_kv309 & -8)) | (l_v333 << (3 + (l_len335 * 2))));
+                  l_x334 = l_kv309;
                 }
-                if ((l_op153 == 3)) {
-                  l_x155 = (((l_kv130 & 7) != 0) ? l_kv130 : 6);
+                if ((l_op332 == 3)) {
+                  l_x334 = (((l_kv309 & 7) != 0) ? l_kv309 : 6);
                 }
-                if ((l_c148 != 0)) {
-                  l_ls1132 = l_q149;
+                if ((l_c327 != 0)) {
+                  l_ls1311 = l_q328;
                 } else {
-                  l_ls0131 = l_q149;
+                  l_ls0310 = l_q328;
                 }
-                if ((l_now151 && (l_act129 != 0))) {
-                  ctx.send(Rec{"Reply", {std::to_string(l_q149), std::to_string(l_x155)}}, (first_client(prm) + (l_c148 + 1) - 1));
+                if ((l_now330 && (l_act308 != 0))) {
+                  ctx.send(Rec{"Reply", {std::to_string(l_q328), std::to_string(l_x334)}}, (first_client(prm) + (l_c327 + 1) - 1));
                 }
               }
-              if (l_now151) {
-                l_so133 = 3;
+              if (l_now330) {
+                l_so312 = 3;
               }
-              const int l_e157 = log[2];
-              const int l_cmd158 = ((l_e157 >> 8) & 7);
-              const int l_c159 = ((l_cmd158 >= 4) ? 1 : 0);
-              const int l_q160 = (l_cmd158 - (((l_cmd158 >= 4) ? 1 : 0) * 3));
-              const int l_before161 = (3 < l_so0128);
-              const int l_now162 = (((!l_before161) && (l_run134 != 0)) && ((l_e157 & 3) == 2));
-              l_run134 = (((l_run134 != 0) && (l_before161 || l_now162)) ? 1 : 0);
-              if ((((l_before161 || l_now162) && (l_cmd158 != 0)) && ((l_c159 ? l_ls1132 : l_ls0131) < l_q160))) {
-                const int l_c163 = ((l_cmd158 >= 4) ? 1 : 0);
-                const int l_op164 = prm.op[l_c163][((l_cmd158 - (((l_cmd158 >= 4) ? 1 : 0) * 3)) - 1)];
-                const int l_v165 = prm.val[l_c163][((l_cmd158 - (((l_cmd158 >= 4) ? 1 : 0) * 3)) - 1)];
-                int l_x166 = 0;
-                if ((l_op164 == 1)) {
-                  l_kv130 = (1 | (l_v165 << 3));
-                  l_x166 = 7;
+              const int l_e336 = log[2];
+              const int l_cmd337 = ((l_e336 >> 8) & 7);
+              const int l_c338 = ((l_cmd337 >= 4) ? 1 : 0);
+              const int l_q339 = (l_cmd337 - (((l_cmd337 >= 4) ? 1 : 0) * 3));
+              const int l_before340 = (3 < l_so0307);
+              const int l_now341 = (((!l_before340) && (l_run313 != 0)) && ((l_e336 & 3) == 2));
+              l_run313 = (((l_run313 != 0) && (l_before340 || l_now341)) ? 1 : 0);
+              if ((((l_before340 || l_now341) && (l_cmd337 != 0)) && ((l_c338 ? l_ls1311 : l_ls0310) < l_q339))) {
+                const int l_c342 = ((l_cmd337 >= 4) ? 1 : 0);
+                const int l_op343 = prm.op[l_c342][((l_cmd337 - (((l_cmd337 >= 4) ? 1 : 0) * 3)) - 1)];
+                const int l_v344 = prm.val[l_c342][((l_cmd337 - (((l_cmd337 >= 4) ? 1 : 0) * 3)) - 1)];
+                int l_x345 = 0;
+                if ((l_op343 == 1)) {
+                  l_kv309 = (1 | (l_v344 << 3));
+                  l_x345 = 7;
                 }
-                if ((l_op164 == 2)) {
-                  const int l_len167 = (l_kv130 & 7);
-                  l_kv130 = (((l_len167 + 1) | (l_kv130 & -8)) | (l_v165 << (3 + (l_len167 * 2))));
-                  l_x166 = l_kv130;
+                if ((l_op343 == 2)) {
+                  const int l_len346 = (l_kv309 & 7);
+                  l_kv309 = (((l_len346 + 1) | (l_kv309 & -8)) | (l_v344 << (3 + (l_len346 * 2))));
+                  l_x345 = l_kv309;
                 }
-                if ((l_op164 == 3)) {
-                  l_x166 = (((l_kv130 & 7) != 0) ? l_kv130 : 6);
+                if ((l_op343 == 3)) {
+                  l_x345 = (((l_kv309 & 7) != 0) ? l_kv309 : 6);
                 }
-                if ((l_c159 != 0)) {
-                  l_ls1132 = l_q160;
+                if ((l_c338 != 0)) {
+                  l_ls1311 = l_q339;
                 } else {
-                  l_ls0131 = l_q160;
+                  l_ls0310 = l_q339;
                 }
-                if ((l_now162 && (l_act129 != 0))) {
-                  ctx.send(Rec{"Reply", {std::to_string(l_q160), std::to_string(l_x166)}}, (first_client(prm) + (l_c159 + 1) - 1));
+                if ((l_now341 && (l_act308 != 0))) {
+                  ctx.send(Rec{"Reply", {std::to_string(l_q339), std::to_string(l_x345)}}, (first_client(prm) + (l_c338 + 1) - 1));
                 }
               }
-              if (l_now162) {
-                l_so133 = 4;
+              if (l_now341) {
+                l_so312 = 4;
               }
-              const int l_e168 = log[3];
-              const int l_cmd169 = ((l_e168 >> 8) & 7);
-              const int l_c170 = ((l_cmd169 >= 4) ? 1 : 0);
-              const int l_q171 = (l_cmd169 - (((l_cmd169 >= 4) ? 1 : 0) * 3));
-              const int l_before172 = (4 < l_so0128);
-              const int l_now173 = (((!l_before172) && (l_run134 != 0)) && ((l_e168 & 3) == 2));
-              l_run134 = (((l_run134 != 0) && (l_before172 || l_now173)) ? 1 : 0);
-              if ((((l_before172 || l_now173) && (l_cmd169 != 0)) && ((l_c170 ? l_ls1132 : l_ls0131) < l_q171))) {
-                const int l_c174 = ((l_cmd169 >= 4) ? 1 : 0);
-                const int l_op175 = prm.op[l_c174][((l_cmd169 - (((l_cmd169 >= 4) ? 1 : 0) * 3)) - 1)];
-                const int l_v176 = prm.val[l_c174][((l_cmd169 - (((l_cmd169 >= 4) ? 1 : 0) * 3)) - 1)];
-                int l_x177 = 0;
-                if ((l_op175 == 1)) {
-                  l_kv130 = (1 | (l_v176 << 3));
-                  l_x177 = 7;
+              const int l_e347 = log[3];
+              const int l_cmd348 = ((l_e347 >> 8) & 7);
+              const int l_c349 = ((l_cmd348 >= 4) ? 1 : 0);
+              const int l_q350 = (l_cmd348 - (((l_cmd348 >= 4) ? 1 : 0) * 3));
+              const int l_before351 = (4 < l_so0307);
+              const int l_now352 = (((!l_before351) && (l_run313 != 0)) && ((l_e347 & 3) == 2));
+              l_run313 = (((l_run313 != 0) && (l_before351 || l_now352)) ? 1 : 0);
+              if ((((l_before351 || l_now352) && (l_cmd348 != 0)) && ((l_c349 ? l_ls1311 : l_ls0310) < l_q350))) {
+                const int l_c353 = ((l_cmd348 >= 4) ? 1 : 0);
+                const int l_op354 = prm.op[l_c353][((l_cmd348 - (((l_cmd348 >= 4) ? 1 : 0) * 3)) - 1)];
+                const int l_v355 = prm.val[l_c353][((l_cmd348 - (((l_cmd348 >= 4) ? 1 : 0) * 3)) - 1)];
+                int l_x356 = 0;
+                if ((l_op354 == 1)) {
+                  l_kv309 = (1 | (l_v355 << 3));
+                  l_x356 = 7;
                 }
-                if ((l_op175 == 2)) {
-                  const int l_len178 = (l_kv130 & 7);
-                  l_kv130 = (((l_len178 + 1) | (l_kv130 & -8)) | (l_v176 << (3 + (l_len178 * 2))));
-                  l_x177 = l_kv130;
+                if ((l_op354 == 2)) {
+                  const int l_len357 = (l_kv309 & 7);
+                  l_kv309 = (((l_len357 + 1) | (l_kv309 & -8)) | (l_v355 << (3 + (l_len357 * 2))));
+                  l_x356 = l_kv309;
                 }
-                if ((l_op175 == 3)) {
-                  l_x177 = (((l_kv130 & 7) != 0) ? l_kv130 : 6);
+                if ((l_op354 == 3)) {
+                  l_x356 = (((l_kv309 & 7) != 0) ? l_kv309 : 6);
                 }
-                if ((l_c170 != 0)) {
-                  l_ls1132 = l_q171;
+                if ((l_c349 != 0)) {
+                  l_ls1311 = l_q350;
                 } else {
-                  l_ls0131 = l_q171;
+                  l_ls0310 = l_q350;
                 }
-                if ((l_now173 && (l_act129 != 0))) {
-                  ctx.send(Rec{"Reply", {std::to_string(l_q171), std::to_string(l_x177)}}, (first_client(prm) + (l_c170 + 1) - 1));
+                if ((l_now352 && (l_act308 != 0))) {
+                  ctx.send(Rec{"Reply", {std::to_string(l_q350), std::to_string(l_x356)}}, (first_client(prm) + (l_c349 + 1) - 1));
                 }
               }
-              if (l_now173) {
-                l_so133 = 5;
+              if (l_now352) {
+                l_so312 = 5;
               }
-              slotout = l_so133;
+              slotout = l_so312;
             }
           }
         }
@@ -1195,15 +1195,15 @@ struct N_client : Client {
     (void)ctx;
     if (t.type == "ClientTimer") {
       if (((pending != 0) && (std::stoi(t.f[0]) == seq))) {
-        const int l_cid179 = (((self - first_client(prm)) * 3) + std::stoi(t.f[0]));
+        const int l_cid358 = (((self - first_client(prm)) * 3) + std::stoi(t.f[0]));
         if ((0 < prm.servers)) {
-          ctx.send(Rec{"Request", {std::to_string(l_cid179)}}, (first_server(prm) + 1 - 1));
+          ctx.send(Rec{"Request", {std::to_string(l_cid358)}}, (first_server(prm) + 1 - 1));
         }
         if ((1 < prm.servers)) {
-          ctx.send(Rec{"Request", {std::to_string(l_cid179)}}, (first_server(prm) + 2 - 1));
+          ctx.send(Rec{"Request", {std::to_string(l_cid358)}}, (first_server(prm) + 2 - 1));
         }
         if ((2 < prm.servers)) {
-          ctx.send(Rec{"Request", {std::to_string(l_cid179)}}, (first_server(prm) + 3 - 1));
+          ctx.send(Rec{"Request", {std::to_string(l_cid358)}}, (first_server(prm) + 3 - 1));
         }
         ctx.set(Rec{"ClientTimer", {std::to_string(std::stoi(t.f[0]))}}, 100, 100);
       }
@@ -1216,15 +1216,15 @@ struct N_client : Client {
     seq = cmd;
     pending = 1;
     result = 0;
-    const int l_cid180 = (((self - first_client(prm)) * 3) + cmd);
+    const int l_cid359 = (((self - first_client(prm)) * 3) + cmd);
     if ((0 < prm.servers)) {
-      ctx.send(Rec{"Request", {std::to_string(l_cid180)}}, (first_server(prm) + 1 - 1));
+      ctx.send(Rec{"Request", {std::to_string(l_cid359)}}, (first_server(prm) + 1 - 1));
     }
     if ((1 < prm.servers)) {
-      ctx.send(Rec{"Request", {std::to_string(l_cid180)}}, (first_server(prm) + 2 - 1));
+      ctx.send(Rec{"Request", {std::to_string(l_cid359)}}, (first_server(prm) + 2 - 1));
     }
     if ((2 < prm.servers)) {
-      ctx.send(Rec{"Request", {std::to_string(l_cid180)}}, (first_server(prm) + 3 - 1));
+      ctx.send(Rec{"Request", {std::to_string(l_cid359)}}, (first_server(prm) + 3 - 1));
     }
     ctx.set(Rec{"ClientTimer", {std::to_string(cmd)}}, 100, 100);
   }
@@ -1295,236 +1295,236 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
     return Predicate{"Non-empty log slots consistent", [prm, a0_, a1_](const State& s) {
       (void)s; (void)a0_; (void)a1_;
       PredResult res_;
-      int l_isch181 = 0;
-      int l_confl182 = 0;
-      int l_chosen183 = 0;
-      int l_count184 = 0;
+      int l_isch360 = 0;
+      int l_confl361 = 0;
+      int l_chosen362 = 0;
+      int l_count363 = 0;
       if ((0 < prm.servers)) {
-        const int l_e185 = n_server(s, first_server(prm) + 0)->log[0];
-        if (((l_e185 & 3) == 2)) {
-          const int l_x186 = ((((l_e185 >> 8) & 7) != 0) ? ((prm.op[((((l_e185 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e185 >> 8) & 7) - (((((l_e185 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e185 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e185 >> 8) & 7) - (((((l_e185 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch181 != 0) && (l_x186 != l_chosen183))) {
-            l_confl182 = 1;
+        const int l_e364 = n_server(s, first_server(prm) + 0)->log[0];
+        if (((l_e364 & 3) == 2)) {
+          const int l_x365 = ((((l_e364 >> 8) & 7) != 0) ? ((prm.op[((((l_e364 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e364 >> 8) & 7) - (((((l_e364 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e364 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e364 >> 8) & 7) - (((((l_e364 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch360 != 0) && (l_x365 != l_chosen362))) {
+            l_confl361 = 1;
           }
-          l_chosen183 = l_x186;
-          l_isch181 = 1;
+          l_chosen362 = l_x365;
+          l_isch360 = 1;
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e187 = n_server(s, first_server(prm) + 1)->log[0];
-        if (((l_e187 & 3) == 2)) {
-          const int l_x188 = ((((l_e187 >> 8) & 7) != 0) ? ((prm.op[((((l_e187 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e187 >> 8) & 7) - (((((l_e187 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e187 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e187 >> 8) & 7) - (((((l_e187 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch181 != 0) && (l_x188 != l_chosen183))) {
-            l_confl182 = 1;
+        const int l_e366 = n_server(s, first_server(prm) + 1)->log[0];
+        if (((l_e366 & 3) == 2)) {
+          const int l_x367 = ((((l_e366 >> 8) & 7) != 0) ? ((prm.op[((((l_e366 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e366 >> 8) & 7) - (((((l_e366 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e366 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e366 >> 8) & 7) - (((((l_e366 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch360 != 0) && (l_x367 != l_chosen362))) {
+            l_confl361 = 1;
           }
-          l_chosen183 = l_x188;
-          l_isch181 = 1;
+          l_chosen362 = l_x367;
+          l_isch360 = 1;
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e189 = n_server(s, first_server(prm) + 2)->log[0];
-        if (((l_e189 & 3) == 2)) {
-          const int l_x190 = ((((l_e189 >> 8) & 7) != 0) ? ((prm.op[((((l_e189 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e189 >> 8) & 7) - (((((l_e189 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e189 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e189 >> 8) & 7) - (((((l_e189 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch181 != 0) && (l_x190 != l_chosen183))) {
-            l_confl182 = 1;
+        const int l_e368 = n_server(s, first_server(prm) + 2)->log[0];
+        if (((l_e368 & 3) == 2)) {
+          const int l_x369 = ((((l_e368 >> 8) & 7) != 0) ? ((prm.op[((((l_e368 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e368 >> 8) & 7) - (((((l_e368 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e368 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e368 >> 8) & 7) - (((((l_e368 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch360 != 0) && (l_x369 != l_chosen362))) {
+            l_confl361 = 1;
           }
-          l_chosen183 = l_x190;
-          l_isch181 = 1;
+          l_chosen362 = l_x369;
+          l_isch360 = 1;
         }
       }
       if ((0 < prm.servers)) {
-        const int l_e191 = n_server(s, first_server(prm) + 0)->log[0];
-        if ((((l_e191 & 3) != 0) && (((l_e191 & 3) != 1) || (((((l_e191 >> 8) & 7) != 0) ? ((prm.op[((((l_e191 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e191 >> 8) & 7) - (((((l_e191 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e191 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e191 >> 8) & 7) - (((((l_e191 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen183)))) {
-          l_count184 = (l_count184 + 1);
+        const int l_e370 = n_server(s, first_server(prm) + 0)->log[0];
+        if ((((l_e370 & 3) != 0) && (((l_e370 & 3) != 1) || (((((l_e370 >> 8) & 7) != 0) ? ((prm.op[((((l_e370 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e370 >> 8) & 7) - (((((l_e370 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e370 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e370 >> 8) & 7) - (((((l_e370 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen362)))) {
+          l_count363 = (l_count363 + 1);
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e192 = n_server(s, first_server(prm) + 1)->log[0];
-        if ((((l_e192 & 3) != 0) && (((l_e192 & 3) != 1) || (((((l_e192 >> 8) & 7) != 0) ? ((prm.op[((((l_e192 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e192 >> 8) & 7) - (((((l_e192 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e192 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e192 >> 8) & 7) - (((((l_e192 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen183)))) {
-          l_count184 = (l_count184 + 1);
+        const int l_e371 = n_server(s, first_server(prm) + 1)->log[0];
+        if ((((l_e371 & 3) != 0) && (((l_e371 & 3) != 1) || (((((l_e371 >> 8) & 7) != 0) ? ((prm.op[((((l_e371 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e371 >> 8) & 7) - (((((l_e371 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e371 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e371 >> 8) & 7) - (((((l_e371 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen362)))) {
+          l_count363 = (l_count363 + 1);
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e193 = n_server(s, first_server(prm) + 2)->log[0];
-        if ((((l_e193 & 3) != 0) && (((l_e193 & 3) != 1) || (((((l_e193 >> 8) & 7) != 0) ? ((prm.op[((((l_e193 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e193 >> 8) & 7) - (((((l_e193 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e193 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e193 >> 8) & 7) - (((((l_e193 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen183)))) {
-          l_count184 = (l_count184 + 1);
+        const int l_e372 = n_server(s, first_server(prm) + 2)->log[0];
+        if ((((l_e372 & 3) != 0) && (((l_e372 & 3) != 1) || (((((l_e372 >> 8) & 7) != 0) ? ((prm.op[((((l_e372 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e372 >> 8) & 7) - (((((l_e372 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e372 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e372 >> 8) & 7) - (((((l_e372 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen362)))) {
+          l_count363 = (l_count363 + 1);
         }
       }
-      if (((l_isch181 != 0) && ((l_confl182 != 0) || ((l_count184 * 2) <= prm.servers)))) {
+      if (((l_isch360 != 0) && ((l_confl361 != 0) || ((l_count363 * 2) <= prm.servers)))) {
         { res_.value = false; return res_; }
       }
-      int l_isch194 = 0;
-      int l_confl195 = 0;
-      int l_chosen196 = 0;
-      int l_count197 = 0;
+      int l_isch373 = 0;
+      int l_confl374 = 0;
+      int l_chosen375 = 0;
+      int l_count376 = 0;
       if ((0 < prm.servers)) {
-        const int l_e198 = n_server(s, first_server(prm) + 0)->log[1];
-        if (((l_e198 & 3) == 2)) {
-          const int l_x199 = ((((l_e198 >> 8) & 7) != 0) ? ((prm.op[((((l_e198 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e198 >> 8) & 7) - (((((l_e198 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e198 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e198 >> 8) & 7) - (((((l_e198 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch194 != 0) && (l_x199 != l_chosen196))) {
-            l_confl195 = 1;
+        const int l_e377 = n_server(s, first_server(prm) + 0)->log[1];
+        if (((l_e377 & 3) == 2)) {
+          const int l_x378 = ((((l_e377 >> 8) & 7) != 0) ? ((prm.op[((((l_e377 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e377 >> 8) & 7) - (((((l_e377 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e377 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e377 >> 8) & 7) - (((((l_e377 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch373 != 0) && (l_x378 != l_chosen375))) {
+            l_confl374 = 1;
           }
-          l_chosen196 = l_x199;
-          l_isch194 = 1;
+          l_chosen375 = l_x378;
+          l_isch373 = 1;
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e200 = n_server(s, first_server(prm) + 1)->log[1];
-        if (((l_e200 & 3) == 2)) {
-          const int l_x201 = ((((l_e200 >> 8) & 7) != 0) ? ((prm.op[((((l_e200 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e200 >> 8) & 7) - (((((l_e200 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e200 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e200 >> 8) & 7) - (((((l_e200 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch194 != 0) && (l_x201 != l_chosen196))) {
-            l_confl195 = 1;
+        const int l_e379 = n_server(s, first_server(prm) + 1)->log[1];
+        if (((l_e379 & 3) == 2)) {
+          const int l_x380 = ((((l_e379 >> 8) & 7) != 0) ? ((prm.op[((((l_e379 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e379 >> 8) & 7) - (((((l_e379 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e379 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e379 >> 8) & 7) - (((((l_e379 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch373 != 0) && (l_x380 != l_chosen375))) {
+            l_confl374 = 1;
           }
-          l_chosen196 = l_x201;
-          l_isch194 = 1;
+          l_chosen375 = l_x380;
+          l_isch373 = 1;
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e202 = n_server(s, first_server(prm) + 2)->log[1];
-        if (((l_e202 & 3) == 2)) {
-          const int l_x203 = ((((l_e202 >> 8) & 7) != 0) ? ((prm.op[((((l_e202 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e202 >> 8) & 7) - (((((l_e202 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e202 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e202 >> 8) & 7) - (((((l_e202 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch194 != 0) && (l_x203 != l_chosen196))) {
-            l_confl195 = 1;
+        const int l_e381 = n_server(s, first_server(prm) + 2)->log[1];
+        if (((l_e381 & 3) == 2)) {
+          const int l_x382 = ((((l_e381 >> 8) & 7) != 0) ? ((prm.op[((((l_e381 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e381 >> 8) & 7) - (((((l_e381 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e381 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e381 >> 8) & 7) - (((((l_e381 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch373 != 0) && (l_x382 != l_chosen375))) {
+            l_confl374 = 1;
           }
-          l_chosen196 = l_x203;
-          l_isch194 = 1;
+          l_chosen375 = l_x382;
+          l_isch373 = 1;
         }
       }
       if ((0 < prm.servers)) {
-        const int l_e204 = n_server(s, first_server(prm) + 0)->log[1];
-        if ((((l_e204 & 3) != 0) && (((l_e204 & 3) != 1) || (((((l_e204 >> 8) & 7) != 0) ? ((prm.op[((((l_e204 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e204 >> 8) & 7) - (((((l_e204 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e204 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e204 >> 8) & 7) - (((((l_e204 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen196)))) {
-          l_count197 = (l_count197 + 1);
+        const int l_e383 = n_server(s, first_server(prm) + 0)->log[1];
+        if ((((l_e383 & 3) != 0) && (((l_e383 & 3) != 1) || (((((l_e383 >> 8) & 7) != 0) ? ((prm.op[((((l_e383 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e383 >> 8) & 7) - (((((l_e383 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e383 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e383 >> 8) & 7) - (((((l_e383 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen375)))) {
+          l_count376 = (l_count376 + 1);
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e205 = n_server(s, first_server(prm) + 1)->log[1];
-        if ((((l_e205 & 3) != 0) && (((l_e205 & 3) != 1) || (((((l_e205 >> 8) & 7) != 0) ? ((prm.op[((((l_e205 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e205 >> 8) & 7) - (((((l_e205 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e205 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e205 >> 8) & 7) - (((((l_e205 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen196)))) {
-          l_count197 = (l_count197 + 1);
+        const int l_e384 = n_server(s, first_server(prm) + 1)->log[1];
+        if ((((l_e384 & 3) != 0) && (((l_e384 & 3) != 1) || (((((l_e384 >> 8) & 7) != 0) ? ((prm.op[((((l_e384 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e384 >> 8) & 7) - (((((l_e384 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e384 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e384 >> 8) & 7) - (((((l_e384 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen375)))) {
+          l_count376 = (l_count376 + 1);
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e206 = n_server(s, first_server(prm) + 2)->log[1];
-        if ((((l_e206 & 3) != 0) && (((l_e206 & 3) != 1) || (((((l_e206 >> 8) & 7) != 0) ? ((prm.op[((((l_e206 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e206 >> 8) & 7) - (((((l_e206 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e206 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e206 >> 8) & 7) - (((((l_e206 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen196)))) {
-          l_count197 = (l_count197 + 1);
+        const int l_e385 = n_server(s, first_server(prm) + 2)->log[1];
+        if ((((l_e385 & 3) != 0) && (((l_e385 & 3) != 1) || (((((l_e385 >> 8) & 7) != 0) ? ((prm.op[((((l_e385 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e385 >> 8) & 7) - (((((l_e385 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e385 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e385 >> 8) & 7) - (((((l_e385 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen375)))) {
+          l_count376 = (l_count376 + 1);
         }
       }
-      if (((l_isch194 != 0) && ((l_confl195 != 0) || ((l_count197 * 2) <= prm.servers)))) {
+      if (((l_isch373 != 0) && ((l_confl374 != 0) || ((l_count376 * 2) <= prm.servers)))) {
         { res_.value = false; return res_; }
       }
-      int l_isch207 = 0;
-      int l_confl208 = 0;
-      int l_chosen209 = 0;
-      int l_count210 = 0;
+      int l_isch386 = 0;
+      int l_confl387 = 0;
+      int l_chosen388 = 0;
+      int l_count389 = 0;
       if ((0 < prm.servers)) {
-        const int l_e211 = n_server(s, first_server(prm) + 0)->log[2];
-        if (((l_e211 & 3) == 2)) {
-          const int l_x212 = ((((l_e211 >> 8) & 7) != 0) ? ((prm.op[((((l_e211 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e211 >> 8) & 7) - (((((l_e211 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e211 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e211 >> 8) & 7) - (((((l_e211 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch207 != 0) && (l_x212 != l_chosen209))) {
-            l_confl208 = 1;
+        const int l_e390 = n_server(s, first_server(prm) + 0)->log[2];
+        if (((l_e390 & 3) == 2)) {
+          const int l_x391 = ((((l_e390 >> 8) & 7) != 0) ? ((prm.op[((((l_e390 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e390 >> 8) & 7) - (((((l_e390 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e390 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e390 >> 8) & 7) - (((((l_e390 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch386 != 0) && (l_x391 != l_chosen388))) {
+            l_confl387 = 1;
           }
-          l_chosen209 = l_x212;
-          l_isch207 = 1;
+          l_chosen388 = l_x391;
+          l_isch386 = 1;
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e213 = n_server(s, first_server(prm) + 1)->log[2];
-        if (((l_e213 & 3) == 2)) {
-          const int l_x214 = ((((l_e213 >> 8) & 7) != 0) ? ((prm.op[((((l_e213 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e213 >> 8) & 7) - (((((l_e213 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e213 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e213 >> 8) & 7) - (((((l_e213 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch207 != 0) && (l_x214 != l_chosen209))) {
-            l_confl208 = 1;
+        const int l_e392 = n_server(s, first_server(prm) + 1)->log[2];
+        if (((l_e392 & 3) == 2)) {
+          const int l_x393 = ((((l_e392 >> 8) & 7) != 0) ? ((prm.op[((((l_e392 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e392 >> 8) & 7) - (((((l_e392 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e392 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e392 >> 8) & 7) - (((((l_e392 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch386 != 0) && (l_x393 != l_chosen388))) {
+            l_confl387 = 1;
           }
-          l_chosen209 = l_x214;
-          l_isch207 = 1;
+          l_chosen388 = l_x393;
+          l_isch386 = 1;
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e215 = n_server(s, first_server(prm) + 2)->log[2];
-        if (((l_e215 & 3) == 2)) {
-          const int l_x216 = ((((l_e215 >> 8) & 7) != 0) ? ((prm.op[((((l_e215 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e215 >> 8) & 7) - (((((l_e215 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e215 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e215 >> 8) & 7) - (((((l_e215 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch207 != 0) && (l_x216 != l_chosen209))) {
-            l_confl208 = 1;
+        const int l_e394 = n_server(s, first_server(prm) + 2)->log[2];
+        if (((l_e394 & 3) == 2)) {
+          const int l_x395 = ((((l_e394 >> 8) & 7) != 0) ? ((prm.op[((((l_e394 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e394 >> 8) & 7) - (((((l_e394 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e394 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e394 >> 8) & 7) - (((((l_e394 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch386 != 0) && (l_x395 != l_chosen388))) {
+            l_confl387 = 1;
           }
-          l_chosen209 = l_x216;
-          l_isch207 = 1;
+          l_chosen388 = l_x395;
+          l_isch386 = 1;
         }
       }
       if ((0 < prm.servers)) {
-        const int l_e217 = n_server(s, first_server(prm) + 0)->log[2];
-        if ((((l_e217 & 3) != 0) && (((l_e217 & 3) != 1) || (((((l_e217 >> 8) & 7) != 0) ? ((prm.op[((((l_e217 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e217 >> 8) & 7) - (((((l_e217 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e217 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e217 >> 8) & 7) - (((((l_e217 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen209)))) {
-          l_count210 = (l_count210 + 1);
+        const int l_e396 = n_server(s, first_server(prm) + 0)->log[2];
+        if ((((l_e396 & 3) != 0) && (((l_e396 & 3) != 1) || (((((l_e396 >> 8) & 7) != 0) ? ((prm.op[((((l_e396 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e396 >> 8) & 7) - (((((l_e396 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e396 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e396 >> 8) & 7) - (((((l_e396 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen388)))) {
+          l_count389 = (l_count389 + 1);
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e218 = n_server(s, first_server(prm) + 1)->log[2];
-        if ((((l_e218 & 3) != 0) && (((l_e218 & 3) != 1) || (((((l_e218 >> 8) & 7) != 0) ? ((prm.op[((((l_e218 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e218 >> 8) & 7) - (((((l_e218 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e218 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e218 >> 8) & 7) - (((((l_e218 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen209)))) {
-          l_count210 = (l_count210 + 1);
+        const int l_e397 = n_server(s, first_server(prm) + 1)->log[2];
+        if ((((l_e397 & 3) != 0) && (((l_e397 & 3) != 1) || (((((l_e397 >> 8) & 7) != 0) ? ((prm.op[((((l_e397 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e397 >> 8) & 7) - (((((l_e397 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e397 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e397 >> 8) & 7) - (((((l_e397 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen388)))) {
+          l_count389 = (l_count389 + 1);
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e219 = n_server(s, first_server(prm) + 2)->log[2];
-        if ((((l_e219 & 3) != 0) && (((l_e219 & 3) != 1) || (((((l_e219 >> 8) & 7) != 0) ? ((prm.op[((((l_e219 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e219 >> 8) & 7) - (((((l_e219 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e219 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e219 >> 8) & 7) - (((((l_e219 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen209)))) {
-          l_count210 = (l_count210 + 1);
+        const int l_e398 = n_server(s, first_server(prm) + 2)->log[2];
+        if ((((l_e398 & 3) != 0) && (((l_e398 & 3) != 1) || (((((l_e398 >> 8) & 7) != 0) ? ((prm.op[((((l_e398 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e398 >> 8) & 7) - (((((l_e398 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e398 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e398 >> 8) & 7) - (((((l_e398 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen388)))) {
+          l_count389 = (l_count389 + 1);
         }
       }
-      if (((l_isch207 != 0) && ((l_confl208 != 0) || ((l_count210 * 2) <= prm.servers)))) {
+      if (((l_isch386 != 0) && ((l_confl387 != 0) || ((l_count389 * 2) <= prm.servers)))) {
         { res_.value = false; return res_; }
       }
-      int l_isch220 = 0;
-      int l_confl221 = 0;
-      int l_chosen222 = 0;
-      int l_count223 = 0;
+      int l_isch399 = 0;
+      int l_confl400 = 0;
+      int l_chosen401 = 0;
+      int l_count402 = 0;
       if ((0 < prm.servers)) {
-        const int l_e224 = n_server(s, first_server(prm) + 0)->log[3];
-        if (((l_e224 & 3) == 2)) {
-          const int l_x225 = ((((l_e224 >> 8) & 7) != 0) ? ((prm.op[((((l_e224 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e224 >> 8) & 7) - (((((l_e224 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e224 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e224 >> 8) & 7) - (((((l_e224 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch220 != 0) && (l_x225 != l_chosen222))) {
-            l_confl221 = 1;
+        const int l_e403 = n_server(s, first_server(prm) + 0)->log[3];
+        if (((l_e403 & 3) == 2)) {
+          const int l_x404 = ((((l_e403 >> 8) & 7) != 0) ? ((prm.op[((((l_e403 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e403 >> 8) & 7) - (((((l_e403 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e403 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e403 >> 8) & 7) - (((((l_e403 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch399 != 0) && (l_x404 != l_chosen401))) {
+            l_confl400 = 1;
           }
-          l_chosen222 = l_x225;
-          l_isch220 = 1;
+          l_chosen401 = l_x404;
+          l_isch399 = 1;
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e226 = n_server(s, first_server(prm) + 1)->log[3];
-        if (((l_e226 & 3) == 2)) {
-          const int l_x227 = ((((l_e226 >> 8) & 7) != 0) ? ((prm.op[((((l_e226 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e226 >> 8) & 7) - (((((l_e226 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e226 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e226 >> 8) & 7) - (((((l_e226 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch220 != 0) && (l_x227 != l_chosen222))) {
-            l_confl221 = 1;
+        const int l_e405 = n_server(s, first_server(prm) + 1)->log[3];
+        if (((l_e405 & 3) == 2)) {
+          const int l_x406 = ((((l_e405 >> 8) & 7) != 0) ? ((prm.op[((((l_e405 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e405 >> 8) & 7) - (((((l_e405 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e405 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e405 >> 8) & 7) - (((((l_e405 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch399 != 0) && (l_x406 != l_chosen401))) {
+            l_confl400 = 1;
           }
-          l_chosen222 = l_x227;
-          l_isch220 = 1;
+          l_chosen401 = l_x406;
+          l_isch399 = 1;
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e228 = n_server(s, first_server(prm) + 2)->log[3];
-        if (((l_e228 & 3) == 2)) {
-          const int l_x229 = ((((l_e228 >> 8) & 7) != 0) ? ((prm.op[((((l_e228 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e228 >> 8) & 7) - (((((l_e228 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e228 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e228 >> 8) & 7) - (((((l_e228 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch220 != 0) && (l_x229 != l_chosen222))) {
-            l_confl221 = 1;
+        const int l_e407 = n_server(s, first_server(prm) + 2)->log[3];
+        if (((l_e407 & 3) == 2)) {
+          const int l_x408 = ((((l_e407 >> 8) & 7) != 0) ? ((prm.op[((((l_e407 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e407 >> 8) & 7) - (((((l_e407 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e407 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e407 >> 8) & 7) - (((((l_e407 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch399 != 0) && (l_x408 != l_chosen401))) {
+            l_confl400 = 1;
           }
-          l_chosen222 = l_x229;
-          l_isch220 = 1;
+          l_chosen401 = l_x408;
+          l_isch399 = 1;
         }
       }
       if ((0 < prm.servers)) {
-        const int l_e230 = n_server(s, first_server(prm) + 0)->log[3];
-        if ((((l_e230 & 3) != 0) && (((l_e230 & 3) != 1) || (((((l_e230 >> 8) & 7) != 0) ? ((prm.op[((((l_e230 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e230 >> 8) & 7) - (((((l_e230 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e230 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e230 >> 8) & 7) - (((((l_e230 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen222)))) {
-          l_count223 = (l_count223 + 1);
+        const int l_e409 = n_server(s, first_server(prm) + 0)->log[3];
+        if ((((l_e409 & 3) != 0) && (((l_e409 & 3) != 1) || (((((l_e409 >> 8) & 7) != 0) ? ((prm.op[((((l_e409 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e409 >> 8) & 7) - (((((l_e409 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e409 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e409 >> 8) & 7) - (((((l_e409 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen401)))) {
+          l_count402 = (l_count402 + 1);
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e231 = n_server(s, first_server(prm) + 1)->log[3];
-        if ((((l_e231 & 3) != 0) && (((l_e231 & 3) != 1) || (((((l_e231 >> 8) & 7) != 0) ? ((prm.op[((((l_e231 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e231 >> 8) & 7) - (((((l_e231 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e231 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e231 >> 8) & 7) - (((((l_e231 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen222)))) {
-          l_count223 = (l_count223 + 1);
+        const int l_e410 = n_server(s, first_server(prm) + 1)->log[3];
+        if ((((l_e410 & 3) != 0) && (((l_e410 & 3) != 1) || (((((l_e410 >> 8) & 7) != 0) ? ((prm.op[((((l_e410 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e410 >> 8) & 7) - (((((l_e410 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e410 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e410 >> 8) & 7) - (((((l_e410 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen401)))) {
+          l_count402 = (l_count402 + 1);
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e232 = n_server(s, first_server(prm) + 2)->log[3];
-        if ((((l_e232 & 3) != 0) && (((l_e232 & 3) != 1) || (((((l_e232 >> 8) & 7) != 0) ? ((prm.op[((((l_e232 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e232 >> 8) & 7) - (((((l_e232 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e232 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e232 >> 8) & 7) - (((((l_e232 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen222)))) {
-          l_count223 = (l_count223 + 1);
+        const int l_e411 = n_server(s, first_server(prm) + 2)->log[3];
+        if ((((l_e411 & 3) != 0) && (((l_e411 & 3) != 1) || (((((l_e411 >> 8) & 7) != 0) ? ((prm.op[((((l_e411 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e411 >> 8) & 7) - (((((l_e411 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e411 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e411 >> 8) & 7) - (((((l_e411 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen401)))) {
+          l_count402 = (l_count402 + 1);
         }
       }
-      if (((l_isch220 != 0) && ((l_confl221 != 0) || ((l_count223 * 2) <= prm.servers)))) {
+      if (((l_isch399 != 0) && ((l_confl400 != 0) || ((l_count402 * 2) <= prm.servers)))) {
         { res_.value = false; return res_; }
       }
       { res_.value = true; return res_; }
@@ -1547,53 +1547,53 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
       int l_chosen = 0;
       int l_count = 0;
       if ((0 < prm.servers)) {
-        const int l_e233 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
-        if (((l_e233 & 3) == 2)) {
-          const int l_x234 = ((((l_e233 >> 8) & 7) != 0) ? ((prm.op[((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e233 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e233 >> 8) & 7) - (((((l_e233 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch != 0) && (l_x234 != l_chosen))) {
+        const int l_e412 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
+        if (((l_e412 & 3) == 2)) {
+          const int l_x413 = ((((l_e412 >> 8) & 7) != 0) ? ((prm.op[((((l_e412 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e412 >> 8) & 7) - (((((l_e412 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e412 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e412 >> 8) & 7) - (((((l_e412 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x413 != l_chosen))) {
             l_confl = 1;
           }
-          l_chosen = l_x234;
+          l_chosen = l_x413;
           l_isch = 1;
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e235 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
-        if (((l_e235 & 3) == 2)) {
-          const int l_x236 = ((((l_e235 >> 8) & 7) != 0) ? ((prm.op[((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e235 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e235 >> 8) & 7) - (((((l_e235 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch != 0) && (l_x236 != l_chosen))) {
+        const int l_e414 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
+        if (((l_e414 & 3) == 2)) {
+          const int l_x415 = ((((l_e414 >> 8) & 7) != 0) ? ((prm.op[((((l_e414 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e414 >> 8) & 7) - (((((l_e414 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e414 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e414 >> 8) & 7) - (((((l_e414 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x415 != l_chosen))) {
             l_confl = 1;
           }
-          l_chosen = l_x236;
+          l_chosen = l_x415;
           l_isch = 1;
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e237 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
-        if (((l_e237 & 3) == 2)) {
-          const int l_x238 = ((((l_e237 >> 8) & 7) != 0) ? ((prm.op[((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e237 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e237 >> 8) & 7) - (((((l_e237 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
-          if (((l_isch != 0) && (l_x238 != l_chosen))) {
+        const int l_e416 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
+        if (((l_e416 & 3) == 2)) {
+          const int l_x417 = ((((l_e416 >> 8) & 7) != 0) ? ((prm.op[((((l_e416 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e416 >> 8) & 7) - (((((l_e416 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e416 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e416 >> 8) & 7) - (((((l_e416 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0);
+          if (((l_isch != 0) && (l_x417 != l_chosen))) {
             l_confl = 1;
           }
-          l_chosen = l_x238;
+          l_chosen = l_x417;
           l_isch = 1;
         }
       }
       if ((0 < prm.servers)) {
-        const int l_e239 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
-        if ((((l_e239 & 3) != 0) && (((l_e239 & 3) != 1) || (((((l_e239 >> 8) & 7) != 0) ? ((prm.op[((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e239 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e239 >> 8) & 7) - (((((l_e239 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+        const int l_e418 = n_server(s, first_server(prm) + 0)->log[(l_i - 1)];
+        if ((((l_e418 & 3) != 0) && (((l_e418 & 3) != 1) || (((((l_e418 >> 8) & 7) != 0) ? ((prm.op[((((l_e418 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e418 >> 8) & 7) - (((((l_e418 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e418 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e418 >> 8) & 7) - (((((l_e418 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
           l_count = (l_count + 1);
         }
       }
       if ((1 < prm.servers)) {
-        const int l_e240 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
-        if ((((l_e240 & 3) != 0) && (((l_e240 & 3) != 1) || (((((l_e240 >> 8) & 7) != 0) ? ((prm.op[((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e240 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e240 >> 8) & 7) - (((((l_e240 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+        const int l_e419 = n_server(s, first_server(prm) + 1)->log[(l_i - 1)];
+        if ((((l_e419 & 3) != 0) && (((l_e419 & 3) != 1) || (((((l_e419 >> 8) & 7) != 0) ? ((prm.op[((((l_e419 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e419 >> 8) & 7) - (((((l_e419 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e419 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e419 >> 8) & 7) - (((((l_e419 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
           l_count = (l_count + 1);
         }
       }
       if ((2 < prm.servers)) {
-        const int l_e241 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
-        if ((((l_e241 & 3) != 0) && (((l_e241 & 3) != 1) || (((((l_e241 >> 8) & 7) != 0) ? ((prm.op[((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e241 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e241 >> 8) & 7) - (((((l_e241 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
+        const int l_e420 = n_server(s, first_server(prm) + 2)->log[(l_i - 1)];
+        if ((((l_e420 & 3) != 0) && (((l_e420 & 3) != 1) || (((((l_e420 >> 8) & 7) != 0) ? ((prm.op[((((l_e420 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e420 >> 8) & 7) - (((((l_e420 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_e420 >> 8) & 7) >= 4) ? 1 : 0)][((((l_e420 >> 8) & 7) - (((((l_e420 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0) == l_chosen)))) {
           l_count = (l_count + 1);
         }
       }
@@ -1608,16 +1608,16 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
     return Predicate{"Server has status in slot", [prm, a0_, a1_](const State& s) {
       (void)s; (void)a0_; (void)a1_;
       PredResult res_;
-      const int l_k242 = (a0_ - (first_server(prm) + 1 - 1));
-      if (((l_k242 < 0) || (l_k242 >= prm.servers))) {
+      const int l_k421 = (a0_ - (first_server(prm) + 1 - 1));
+      if (((l_k421 < 0) || (l_k421 >= prm.servers))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_slot243 = (a1_ >> 4);
-      int l_se244 = 0;
-      if (((l_slot243 >= 1) && (l_slot243 <= 4))) {
-        l_se244 = n_server(s, first_server(prm) + l_k242)->log[(l_slot243 - 1)];
+      const int l_slot422 = (a1_ >> 4);
+      int l_se423 = 0;
+      if (((l_slot422 >= 1) && (l_slot422 <= 4))) {
+        l_se423 = n_server(s, first_server(prm) + l_k421)->log[(l_slot422 - 1)];
       }
-      if (((l_se244 & 3) == (a1_ & 15))) {
+      if (((l_se423 & 3) == (a1_ & 15))) {
         { res_.value = true; return res_; }
       }
       { res_.value = false; return res_; }
@@ -1628,16 +1628,16 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
     return Predicate{"Server has command in slot", [prm, a0_, a1_](const State& s) {
       (void)s; (void)a0_; (void)a1_;
       PredResult res_;
-      const int l_k245 = (a0_ - (first_server(prm) + 1 - 1));
-      if (((l_k245 < 0) || (l_k245 >= prm.servers))) {
+      const int l_k424 = (a0_ - (first_server(prm) + 1 - 1));
+      if (((l_k424 < 0) || (l_k424 >= prm.servers))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_slot246 = (a1_ >> 8);
-      int l_se247 = 0;
-      if (((l_slot246 >= 1) && (l_slot246 <= 4))) {
-        l_se247 = n_server(s, first_server(prm) + l_k245)->log[(l_slot246 - 1)];
+      const int l_slot425 = (a1_ >> 8);
+      int l_se426 = 0;
+      if (((l_slot425 >= 1) && (l_slot425 <= 4))) {
+        l_se426 = n_server(s, first_server(prm) + l_k424)->log[(l_slot425 - 1)];
       }
-      const int l_cc = (((l_se247 & 3) == 0) ? 0 : ((((l_se247 >> 8) & 7) != 0) ? ((prm.op[((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_se247 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se247 >> 8) & 7) - (((((l_se247 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0));
+      const int l_cc = (((l_se426 & 3) == 0) ? 0 : ((((l_se426 >> 8) & 7) != 0) ? ((prm.op[((((l_se426 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se426 >> 8) & 7) - (((((l_se426 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)] << 2) | prm.val[((((l_se426 >> 8) & 7) >= 4) ? 1 : 0)][((((l_se426 >> 8) & 7) - (((((l_se426 >> 8) & 7) >= 4) ? 1 : 0) * 3)) - 1)]) : 0));
       if ((l_cc == (a1_ & 255))) {
         { res_.value = true; return res_; }
       }
@@ -1649,177 +1649,177 @@ inline std::optional<Predicate> predicate(const std::string& name, const Params&
     return Predicate{"Sequence of appends to the same key is linearizable", [prm, a0_, a1_](const State& s) {
       (void)s; (void)a0_; (void)a1_;
       PredResult res_;
-      const int l_pres248 = ((0 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres248 && (prm.op[0][0] != 2))) {
+      const int l_pres427 = ((0 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres427 && (prm.op[0][0] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res249 = (l_pres248 ? std::stoi(s.cw(first_client(prm) + 0)->results[0].f[0]) : 0);
-      const int l_rlen250 = (l_res249 & 7);
-      if ((l_pres248 && (((l_rlen250 == 0) || (l_rlen250 > 4)) || (((l_res249 >> (1 + (l_rlen250 * 2))) & 3) != prm.val[0][0])))) {
+      const int l_res428 = (l_pres427 ? std::stoi(s.cw(first_client(prm) + 0)->results[0].f[0]) : 0);
+      const int l_rlen429 = (l_res428 & 7);
+      if ((l_pres427 && (((l_rlen429 == 0) || (l_rlen429 > 4)) || (((l_res428 >> (1 + (l_rlen429 * 2))) & 3) != prm.val[0][0])))) {
         { res_.value = false; return res_; }
       }
-      const int l_pres251 = ((0 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres251 && (prm.op[0][1] != 2))) {
+      const int l_pres430 = ((0 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres430 && (prm.op[0][1] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res252 = (l_pres251 ? std::stoi(s.cw(first_client(prm) + 0)->results[1].f[0]) : 0);
-      const int l_rlen253 = (l_res252 & 7);
-      if ((l_pres251 && (((l_rlen253 == 0) || (l_rlen253 > 4)) || (((l_res252 >> (1 + (l_rlen253 * 2))) & 3) != prm.val[0][1])))) {
+      const int l_res431 = (l_pres430 ? std::stoi(s.cw(first_client(prm) + 0)->results[1].f[0]) : 0);
+      const int l_rlen432 = (l_res431 & 7);
+      if ((l_pres430 && (((l_rlen432 == 0) || (l_rlen432 > 4)) || (((l_res431 >> (1 + (l_rlen432 * 2))) & 3) != prm.val[0][1])))) {
         { res_.value = false; return res_; }
       }
-      const int l_pres254 = ((0 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 0)->results.size()));
-      if ((l_pres254 && (prm.op[0][2] != 2))) {
+      const int l_pres433 = ((0 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 0)->results.size()));
+      if ((l_pres433 && (prm.op[0][2] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res255 = (l_pres254 ? std::stoi(s.cw(first_client(prm) + 0)->results[2].f[0]) : 0);
-      const int l_rlen256 = (l_res255 & 7);
-      if ((l_pres254 && (((l_rlen256 == 0) || (l_rlen256 > 4)) || (((l_res255 >> (1 + (l_rlen256 * 2))) & 3) != prm.val[0][2])))) {
+      const int l_res434 = (l_pres433 ? std::stoi(s.cw(first_client(prm) + 0)->results[2].f[0]) : 0);
+      const int l_rlen435 = (l_res434 & 7);
+      if ((l_pres433 && (((l_rlen435 == 0) || (l_rlen435 > 4)) || (((l_res434 >> (1 + (l_rlen435 * 2))) & 3) != prm.val[0][2])))) {
         { res_.value = false; return res_; }
       }
-      const int l_pres257 = ((1 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres257 && (prm.op[1][0] != 2))) {
+      const int l_pres436 = ((1 < prm.clients) && (0 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres436 && (prm.op[1][0] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res258 = (l_pres257 ? std::stoi(s.cw(first_client(prm) + 1)->results[0].f[0]) : 0);
-      const int l_rlen259 = (l_res258 & 7);
-      if ((l_pres257 && (((l_rlen259 == 0) || (l_rlen259 > 4)) || (((l_res258 >> (1 + (l_rlen259 * 2))) & 3) != prm.val[1][0])))) {
+      const int l_res437 = (l_pres436 ? std::stoi(s.cw(first_client(prm) + 1)->results[0].f[0]) : 0);
+      const int l_rlen438 = (l_res437 & 7);
+      if ((l_pres436 && (((l_rlen438 == 0) || (l_rlen438 > 4)) || (((l_res437 >> (1 + (l_rlen438 * 2))) & 3) != prm.val[1][0])))) {
         { res_.value = false; return res_; }
       }
-      const int l_pres260 = ((1 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres260 && (prm.op[1][1] != 2))) {
+      const int l_pres439 = ((1 < prm.clients) && (1 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres439 && (prm.op[1][1] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res261 = (l_pres260 ? std::stoi(s.cw(first_client(prm) + 1)->results[1].f[0]) : 0);
-      const int l_rlen262 = (l_res261 & 7);
-      if ((l_pres260 && (((l_rlen262 == 0) || (l_rlen262 > 4)) || (((l_res261 >> (1 + (l_rlen262 * 2))) & 3) != prm.val[1][1])))) {
+      const int l_res440 = (l_pres439 ? std::stoi(s.cw(first_client(prm) + 1)->results[1].f[0]) : 0);
+      const int l_rlen441 = (l_res440 & 7);
+      if ((l_pres439 && (((l_rlen441 == 0) || (l_rlen441 > 4)) || (((l_res440 >> (1 + (l_rlen441 * 2))) & 3) != prm.val[1][1])))) {
         { res_.value = false; return res_; }
       }
-      const int l_pres263 = ((1 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 1)->results.size()));
-      if ((l_pres263 && (prm.op[1][2] != 2))) {
+      const int l_pres442 = ((1 < prm.clients) && (2 < (int)s.cw(first_client(prm) + 1)->results.size()));
+      if ((l_pres442 && (prm.op[1][2] != 2))) {
         throw std::runtime_error("predicate threw");
       }
-      const int l_res264 = (l_pres263 ? std::stoi(s.cw(first_client(prm) + 1)->results[2].f[0]) : 0);
-      const int l_rlen265 = (l_res264 & 7);
-      if ((l_pres263 && (((l_rlen265 == 0) || (l_rlen265 > 4)) || (((l_res264 >> (1 + (l_rlen265 * 2))) & 3) != prm.val[1][2])))) {
+      const int l_res443 = (l_pres442 ? std::stoi(s.cw(first_client(prm) + 1)->results[2].f[0]) : 0);
+      const int l_rlen444 = (l_res443 & 7);
+      if ((l_pres442 && (((l_rlen444 == 0) || (l_rlen444 > 4)) || (((l_res443 >> (1 + (l_rlen444 * 2))) & 3) != prm.val[1][2])))) {
         { res_.value = false; return res_; }
       }
-      if ((l_pres248 && l_pres251)) {
-        if ((l_rlen250 == l_rlen253)) {
+      if ((l_pres427 && l_pres430)) {
+        if ((l_rlen429 == l_rlen432)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)) != ((l_res252 >> 3) & ((1 << (((l_rlen250 < l_rlen253) ? l_rlen250 : l_rlen253) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres248 && l_pres254)) {
-        if ((l_rlen250 == l_rlen256)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen250 < l_rlen256) ? l_rlen250 : l_rlen256) * 2)) - 1)))) {
+        if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen432) ? l_rlen429 : l_rlen432) * 2)) - 1)) != ((l_res431 >> 3) & ((1 << (((l_rlen429 < l_rlen432) ? l_rlen429 : l_rlen432) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres248 && l_pres257)) {
-        if ((l_rlen250 == l_rlen259)) {
+      if ((l_pres427 && l_pres433)) {
+        if ((l_rlen429 == l_rlen435)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen250 < l_rlen259) ? l_rlen250 : l_rlen259) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres248 && l_pres260)) {
-        if ((l_rlen250 == l_rlen262)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen250 < l_rlen262) ? l_rlen250 : l_rlen262) * 2)) - 1)))) {
+        if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen435) ? l_rlen429 : l_rlen435) * 2)) - 1)) != ((l_res434 >> 3) & ((1 << (((l_rlen429 < l_rlen435) ? l_rlen429 : l_rlen435) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres248 && l_pres263)) {
-        if ((l_rlen250 == l_rlen265)) {
+      if ((l_pres427 && l_pres436)) {
+        if ((l_rlen429 == l_rlen438)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res249 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen250 < l_rlen265) ? l_rlen250 : l_rlen265) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres251 && l_pres254)) {
-        if ((l_rlen253 == l_rlen256)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)) != ((l_res255 >> 3) & ((1 << (((l_rlen253 < l_rlen256) ? l_rlen253 : l_rlen256) * 2)) - 1)))) {
+        if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen438) ? l_rlen429 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen429 < l_rlen438) ? l_rlen429 : l_rlen438) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres251 && l_pres257)) {
-        if ((l_rlen253 == l_rlen259)) {
+      if ((l_pres427 && l_pres439)) {
+        if ((l_rlen429 == l_rlen441)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen253 < l_rlen259) ? l_rlen253 : l_rlen259) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres251 && l_pres260)) {
-        if ((l_rlen253 == l_rlen262)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen253 < l_rlen262) ? l_rlen253 : l_rlen262) * 2)) - 1)))) {
+        if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen441) ? l_rlen429 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen429 < l_rlen441) ? l_rlen429 : l_rlen441) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres251 && l_pres263)) {
-        if ((l_rlen253 == l_rlen265)) {
+      if ((l_pres427 && l_pres442)) {
+        if ((l_rlen429 == l_rlen444)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res252 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen253 < l_rlen265) ? l_rlen253 : l_rlen265) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres254 && l_pres257)) {
-        if ((l_rlen256 == l_rlen259)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)) != ((l_res258 >> 3) & ((1 << (((l_rlen256 < l_rlen259) ? l_rlen256 : l_rlen259) * 2)) - 1)))) {
+        if ((((l_res428 >> 3) & ((1 << (((l_rlen429 < l_rlen444) ? l_rlen429 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen429 < l_rlen444) ? l_rlen429 : l_rlen444) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres254 && l_pres260)) {
-        if ((l_rlen256 == l_rlen262)) {
+      if ((l_pres430 && l_pres433)) {
+        if ((l_rlen432 == l_rlen435)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen256 < l_rlen262) ? l_rlen256 : l_rlen262) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres254 && l_pres263)) {
-        if ((l_rlen256 == l_rlen265)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res255 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen256 < l_rlen265) ? l_rlen256 : l_rlen265) * 2)) - 1)))) {
+        if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen435) ? l_rlen432 : l_rlen435) * 2)) - 1)) != ((l_res434 >> 3) & ((1 << (((l_rlen432 < l_rlen435) ? l_rlen432 : l_rlen435) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres257 && l_pres260)) {
-        if ((l_rlen259 == l_rlen262)) {
+      if ((l_pres430 && l_pres436)) {
+        if ((l_rlen432 == l_rlen438)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)) != ((l_res261 >> 3) & ((1 << (((l_rlen259 < l_rlen262) ? l_rlen259 : l_rlen262) * 2)) - 1)))) {
-          { res_.value = false; return res_; }
-        }
-      }
-      if ((l_pres257 && l_pres263)) {
-        if ((l_rlen259 == l_rlen265)) {
-          { res_.value = false; return res_; }
-        }
-        if ((((l_res258 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen259 < l_rlen265) ? l_rlen259 : l_rlen265) * 2)) - 1)))) {
+        if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen438) ? l_rlen432 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen432 < l_rlen438) ? l_rlen432 : l_rlen438) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }
-      if ((l_pres260 && l_pres263)) {
-        if ((l_rlen262 == l_rlen265)) {
+      if ((l_pres430 && l_pres439)) {
+        if ((l_rlen432 == l_rlen441)) {
           { res_.value = false; return res_; }
         }
-        if ((((l_res261 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)) != ((l_res264 >> 3) & ((1 << (((l_rlen262 < l_rlen265) ? l_rlen262 : l_rlen265) * 2)) - 1)))) {
+        if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen441) ? l_rlen432 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen432 < l_rlen441) ? l_rlen432 : l_rlen441) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres430 && l_pres442)) {
+        if ((l_rlen432 == l_rlen444)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res431 >> 3) & ((1 << (((l_rlen432 < l_rlen444) ? l_rlen432 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen432 < l_rlen444) ? l_rlen432 : l_rlen444) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres433 && l_pres436)) {
+        if ((l_rlen435 == l_rlen438)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen438) ? l_rlen435 : l_rlen438) * 2)) - 1)) != ((l_res437 >> 3) & ((1 << (((l_rlen435 < l_rlen438) ? l_rlen435 : l_rlen438) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres433 && l_pres439)) {
+        if ((l_rlen435 == l_rlen441)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen441) ? l_rlen435 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen435 < l_rlen441) ? l_rlen435 : l_rlen441) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres433 && l_pres442)) {
+        if ((l_rlen435 == l_rlen444)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res434 >> 3) & ((1 << (((l_rlen435 < l_rlen444) ? l_rlen435 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen435 < l_rlen444) ? l_rlen435 : l_rlen444) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres436 && l_pres439)) {
+        if ((l_rlen438 == l_rlen441)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res437 >> 3) & ((1 << (((l_rlen438 < l_rlen441) ? l_rlen438 : l_rlen441) * 2)) - 1)) != ((l_res440 >> 3) & ((1 << (((l_rlen438 < l_rlen441) ? l_rlen438 : l_rlen441) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres436 && l_pres442)) {
+        if ((l_rlen438 == l_rlen444)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res437 >> 3) & ((1 << (((l_rlen438 < l_rlen444) ? l_rlen438 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen438 < l_rlen444) ? l_rlen438 : l_rlen444) * 2)) - 1)))) {
+          { res_.value = false; return res_; }
+        }
+      }
+      if ((l_pres439 && l_pres442)) {
+        if ((l_rlen441 == l_rlen444)) {
+          { res_.value = false; return res_; }
+        }
+        if ((((l_res440 >> 3) & ((1 << (((l_rlen441 < l_rlen444) ? l_rlen441 : l_rlen444) * 2)) - 1)) != ((l_res443 >> 3) & ((1 << (((l_rlen441 < l_rlen444) ? l_rlen441 : l_rlen444) * 2)) - 1)))) {
           { res_.value = false; return res_; }
         }
       }

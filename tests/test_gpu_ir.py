@@ -71,12 +71,10 @@ MP = json.load(open(os.path.join(HERE, "golden", "multipaxos.json")))
 def test_ir_multipaxos_matches_golden(name, shards):
     """BASELINE C5's protocol generated from the IR (dslabs_amd/ir/specs/multipaxos.py) on the
     MI355X engine: every multipaxos.json fixture of the hand-written protocol -- C5 to depth 12
-    included -- per depth, also hash-sharded over 3 virtual shards; terminal traces replay on the
+    included -- per depth, also hash-sharded over 3 virtual shards (C5 d12 too); terminal traces replay on the
     IR-generated oracle form."""
     from test_ir import _mp_ir
     case = MP[name]
-    if shards and name == "mp_c5_d12":
-        pytest.skip("the sharded form runs C5 at depth 8 (mp_c5_d8)")
     proto, rest = _mp_ir(case["args"])
     e = Engine(proto, virtual_shards=shards, replicate_below=0 if shards else -1)
     try:
