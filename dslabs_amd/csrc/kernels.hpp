@@ -249,9 +249,14 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 // compiled to ~1,300 exec-mask instructions per Multi-Paxos row). Stores go through
 // address-space-1 pointers: a pointer that came through v_readlane would otherwise be a FLAT
 // store, which also counts in lgkmcnt. Must be called by all lanes of the wave.
+// Returns true (wave-uniform) when two kept sends of one row were equal: they would share a rank
+// and leave a record slot unwritten. Only a protocol whose Sender skips its duplicate check
+// (P::kSendsDistinct, asserted on the explored steps of tests/hostcheck) can get there; the caller
+// raises an error instead of writing a wrong row silently.
 template <class P>
-__device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
+__device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
                                           uint32_t* dst) {
+  bool collision = false;
   using L = Layout<P>;
   using Rec = typename P::Rec;
   typedef __attribute__((address_space(1))) uint32_t g32;
@@ -323,6 +328,12 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
           int pos = 0;  // elements below r: its slot (free lanes hold ~0, never below)
 #pragma unroll
           for (int t = 0; t < TR; t++) pos += __popcll(__ballot(e[t] < r));
+          if constexpr (SendsDistinct<P>::value) {  // r itself is the one element equal to it
+            int eq = 0;
+#pragma unroll
+            for (int t = 0; t < TR; t++) eq += __popcll(__ballot(e[t] == r));
+            collision |= eq != 1;
+          }
 #pragma unroll
           for (int t = 0; t < TR; t++) {
             const int q = lane + 64 * t;
@@ -341,6 +352,7 @@ __device__ __forceinline__ void wave_emit(bool active, const uint32_t* base, uin
     }
     if (TAIL0 < NW && lane < NW - TAIL0) ow[TAIL0 + lane] = 0u;
   }
+  return collision;
 }
 
 template <class P>
@@ -872,7 +884,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             a.next_event[idx] = (uint32_t)k;
             c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
           }
-          wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+          if (wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW) && lane == 0)
+            atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
           PH_MARK(6);  // history + row emission
           // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
           const bool spill = is_valid && !fits;
@@ -948,7 +961,8 @@ __global__ void __launch_bounds__(kBlock) k_unspill(const uint64_t* items, uint6
       next_event[idx] = (uint32_t)k;
       ne = (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
-    wave_emit<P>(ok, cur, parent, d, next + (base_idx + i) * NW);
+    if (wave_emit<P>(ok, cur, parent, d, next + (base_idx + i) * NW) && __lane_id() == 0)
+      atomicAdd(&ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
     c_next_work += ne;
   }
   block_flush(s_red, &ctr->next_work, c_next_work);
@@ -1193,7 +1207,8 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       a.next_event[idx] = (uint32_t)k;
       c_next_work += (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
-    wave_emit<P>(fits, a.cur, parent, d, a.next + idx * NW);
+    if (wave_emit<P>(fits, a.cur, parent, d, a.next + idx * NW) && __lane_id() == 0)
+      atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
   }
   block_flush(s_red, &a.ctr->next_work, c_next_work);
 }
