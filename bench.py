@@ -217,7 +217,32 @@ def roofline(stats: dict, workload: str, depth: int) -> dict:
     prof = pmc_profile(workload, depth)
     if prof and prof.get("atomics_per_step") is not None:
         out["pmc_atomics_per_search"] = int(prof["atomics_per_step"])
+    ra = random_access_roofline(out["table_bytes"], out["probes_per_s"], out["atomics_per_s"])
+    if ra:
+        out["random_access"] = ra
     return out
+
+
+def random_access_roofline(table_bytes: int, probes_per_s: float, inserts_per_s: float):
+    """The probes' own ceiling: the chip-wide rates of independent random 64-B line loads and of
+    random 8-byte agent-scope CAS on a table of about this size (tools/rand_calib.hip, committed
+    as profiles/r04_random_access_calibration.jsonl; 16 waves per CU, 8 in flight per lane).
+    A table beyond 1 GiB is probed by a load and only a new state's slot is CAS'd (fingerprint.hpp
+    load_first), a smaller one by a CAS per probe. `time_share` = the fraction of the kernel's time
+    those accesses alone would take at their ceilings (1.0 = at the random-access roofline)."""
+    f = os.path.join(ROOT, "profiles", "r04_random_access_calibration.jsonl")
+    if not os.path.exists(f):
+        return None
+    rows = [json.loads(x) for x in open(f) if x.strip()]
+    rows = [r for r in rows if r.get("waves_per_cu") == 16] or rows
+    import math
+    r = min(rows, key=lambda r: abs(math.log2(r["table_bytes"]) - math.log2(max(1, table_bytes))))
+    lc, cc = r["random_line_loads_per_s"], r["random_cas_per_s"]
+    load_first = table_bytes > (1 << 30)
+    share = (probes_per_s / lc + inserts_per_s / cc) if load_first else probes_per_s / cc
+    return {"load_ceiling_per_s": lc, "cas_ceiling_per_s": cc, "calibrated_table_bytes": r["table_bytes"],
+            "probe_mode": "load, then CAS if empty" if load_first else "CAS", "time_share": round(share, 4),
+            "source": os.path.relpath(f, ROOT)}
 
 
 def main():
