@@ -35,6 +35,8 @@ constexpr int kMaxShards = 16;
 #define DSL_KWIN 1024
 #endif
 constexpr int kWin = DSL_KWIN;  // work items per class-sorted window of k_level
+// a located event in 16 bits: record indices < kNetCap, timers -1 - (node * 256 + j) >= -4096
+constexpr int kEvNone = -32768;
 // The next frontier is written into up to kSegs segments, one reservation counter each (a
 // workgroup appends to segment blockIdx % nseg), so every wavefront reserves its rows with one
 // returning atomic and no workgroup barrier, and no counter word carries more than 1/kSegs of
@@ -510,6 +512,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   // handler classes: messages, timers, then the events whose handler surely changes nothing
   // (NoopFilter: counted as successors and never run; they sort last and the passes stop before them)
   constexpr int NC = P::kMsgClasses + 2;
+  static_assert(P::kNodes * 256 < 32768 && P::kNetCap < 32768, "a located event fits s_ev's 16 bits");
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                    // a.PB (max) * NW
   Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
@@ -527,6 +530,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ int s_cbase[kWin / 64][NC];
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
+  __shared__ int16_t s_ev[kWin];  // each item's located event (locate_event code; kEvNone: none)
   __shared__ int s_stop, s_weff, s_gnext, s_tup;
   __shared__ uint64_t s_t0;
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
@@ -672,8 +676,10 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
           const uint32_t* w = rows + j * NW;
           for (int q = lo + sub; q < hi; q += tpp) {
+            int ev;
             s_par[q - w0] = (uint8_t)j;
-            s_cls[q - w0] = (uint8_t)event_class_skip<P>(w, prm, set, q - e0);
+            s_cls[q - w0] = (uint8_t)event_class_skip<P>(w, prm, set, q - e0, &ev);
+            s_ev[q - w0] = (int16_t)(ev == INT32_MIN ? kEvNone : ev);
           }
         }
       }
@@ -801,7 +807,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           // often) leads back to the parent, which is in the visited set: no probe
           {
             PH_CLS_T0
-            rc = delta_step<P>(w, k, d, prm, set);
+            const int ev = s_ev[u];
+            rc = delta_step_located<P>(w, ev == kEvNone ? INT32_MIN : ev, d, prm, set);
             PH_CLS_ADD(s_cls[u], true);
             PH_MARK(1);  // decode + handler + canonical sends
             if (rc == STEP_OK) {

@@ -301,8 +301,10 @@ struct NoopTimerFilter<P, std::void_t<decltype(&P::surely_noop_timer)>> {
 };
 
 template <class P>
-DSL_HD int event_class_skip(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
+DSL_HD int event_class_skip(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k,
+                            int* located = nullptr) {
   const int e = locate_event<P>(w, prm, set, k);
+  if (located) *located = e;  // k_level keeps it for delta_step_located (no second walk)
   if (e < 0) {
     if (e == INT32_MIN) return P::kMsgClasses;
     const int x = -1 - e;
@@ -367,8 +369,16 @@ DSL_HD int delta_sends(const Delta<P>& d, typename P::Rec* out) {
 
 // Applies event k of parent w: fills the delta (its send list canonical); returns a StepRc.
 template <class P>
+DSL_HD int delta_step_located(const uint32_t* w, int e, Delta<P>& d, const typename P::Params& prm,
+                              const DevSettings& set);
+template <class P>
 DSL_HD int delta_step(const uint32_t* w, int k, Delta<P>& d, const typename P::Params& prm, const DevSettings& set) {
-  const int e = locate_event<P>(w, prm, set, k);
+  return delta_step_located<P>(w, locate_event<P>(w, prm, set, k), d, prm, set);
+}
+// The same for an event already located (locate_event's code e).
+template <class P>
+DSL_HD int delta_step_located(const uint32_t* w, int e, Delta<P>& d, const typename P::Params& prm,
+                              const DevSettings& set) {
   if (e == INT32_MIN) return STEP_NULL;
   d.out.n = 0;
   d.out.overflow = false;
