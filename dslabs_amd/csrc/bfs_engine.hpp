@@ -896,6 +896,11 @@ struct BfsEngine : EngineBase {
     while ((2ull << tbl.b0) <= buckets) tbl.b0++;  // log2(buckets): the key layout of this search
     inserted = 1;
     uint64_t prev_new = 0, prev_work = 0;  // the last level's new states and work items (est_new_states)
+    // the last level's frontier growth (next frontier / frontier, all shards): the next frontier's
+    // rows are reserved for 1.25x that growth (at least 4x), so a protocol that grows faster than
+    // 4 new states per parent (the synthetic C3: ~5) does not spill every large level
+    uint64_t prev_front = 1;
+    double front_growth = 0;
 
     // Seed: the initial state lives on its owner shard (BFS.initSearch, Search.java:434-440).
     const Fp init_fp = full_fingerprint<P>(init.w);
@@ -1072,7 +1077,8 @@ struct BfsEngine : EngineBase {
           for (size_t q = 0; q < S.seg_cnt.size(); q++) nchunks += (S.seg_cnt[q] + PB - 1) / PB;
           const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)lslots));
           S.nseg = (int)std::min<uint64_t>(kSegs, blocks);
-          const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(4 * S.F, 8192)) + 1;
+          const uint64_t grown = (uint64_t)(1.25 * front_growth * (double)S.F);
+          const uint64_t want = std::min<uint64_t>(S.work, std::max<uint64_t>(std::max<uint64_t>(4 * S.F, grown), 8192)) + 1;
           S.segcap = (want + S.nseg - 1) / S.nseg + 1;
           const uint64_t rows = S.segcap * S.nseg;
           DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
@@ -1497,6 +1503,10 @@ struct BfsEngine : EngineBase {
         inserted += route ? max_new : gsum[0];  // per shard (an upper bound)
         prev_new = gsum[0];
         prev_work = gsum[6];
+        if (gsum[1]) {  // the level's parents: gsum[7] when counted, else the last frontier
+          front_growth = (double)gsum[1] / (double)(gsum[7] ? gsum[7] : prev_front);
+          prev_front = gsum[1];
+        }
         if (gsum[0]) per_depth.push_back(gsum[0]);
         max_front = std::max(max_front, gsum[1]);
         progress_states = total_states;

@@ -423,10 +423,12 @@ __host__ __device__ inline int balanced_chunk(uint64_t F, int pbmax, int slots) 
 }
 
 // New states a level of `work` work items may insert, from the previous level's new / work ratio
-// (x2, plus a floor): the growth rule's estimate (BfsEngine::ensure_table). At most `work`.
+// (x1.25, plus a floor): the growth rule's estimate (BfsEngine::ensure_table). At most `work`.
 __host__ __device__ inline uint64_t est_new_states(uint64_t work, uint64_t prev_new, uint64_t prev_work) {
+  // the last level's new states per work item, with a 25 % margin (the ratio falls with depth in
+  // every protocol here; the table is then kept at most half full of the estimate)
   const double r = prev_work ? (double)prev_new / (double)prev_work : 1.0;
-  const double e = 2.0 * r * (double)work + 1024.0;
+  const double e = 1.25 * r * (double)work + 1024.0;
   return e < (double)work ? (uint64_t)e : work;
 }
 
