@@ -255,9 +255,12 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 // and leave a record slot unwritten. Only a protocol whose Sender skips its duplicate check
 // (P::kSendsDistinct, asserted on the explored steps of tests/hostcheck) can get there; the caller
 // raises an error instead of writing a wrong row silently.
+// nw_lds (k_level): the changed nodes' words already in LDS, kNodeWords per lane of the workgroup
+// (s_nodew; `lane0` = the wave's first lane there): a header word then comes from one LDS read
+// instead of kNodeWords readlanes and selects per row.
 template <class P>
 __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
-                                          uint32_t* dst) {
+                                          uint32_t* dst, const uint32_t* nw_lds = nullptr) {
   bool collision = false;
   using L = Layout<P>;
   using Rec = typename P::Rec;
@@ -280,7 +283,19 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
     const int m = __builtin_popcount(keep);
     const int n = Net<P>::size(pw);
     // header
-    {
+    if (nw_lds) {
+      const uint32_t* nws = nw_lds + src * P::kNodeWords;
+#pragma unroll
+      for (int t = 0; t < TH; t++) {
+        const int o = lane + 64 * t;
+        if (o < L::kRecBase) {
+          const int rel = o - node * P::kNodeWords;
+          const uint32_t v = o < L::kNetCount ? ((unsigned)rel < (unsigned)P::kNodeWords ? nws[rel] : pw[o])
+                                              : o == L::kNetCount ? (uint32_t)(n + m) : 0u;
+          ow[o] = v;
+        }
+      }
+    } else {
       uint32_t nw[P::kNodeWords];
 #pragma unroll
       for (int i = 0; i < P::kNodeWords; i++) nw[i] = rl32(d.nw[i], src);
@@ -346,13 +361,15 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
         }
       }
     }
+    // only the row's n + m records are stored: the free slots after them (and the padding) keep
+    // whatever the buffer held, since every reader of a row reads its records below the count
+    // (Net::at for j < size; rows never leave the device: host states are rebuilt by replay)
     grec* orec = (grec*)(ow + L::kRecBase);
 #pragma unroll
     for (int t = 0; t < TR; t++) {
       const int q = lane + 64 * t;
-      if (q < P::kNetCap) orec[rk[t]] = q < n + m ? e[t] : (Rec)0;
+      if (q < n + m) orec[rk[t]] = e[t];
     }
-    if (TAIL0 < NW && lane < NW - TAIL0) ow[TAIL0 + lane] = 0u;
   }
   return collision;
 }
@@ -893,8 +910,12 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             a.next_event[idx] = (uint32_t)k;
             c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
           }
-          if (wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW) && lane == 0)
+          if (wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW, s_nodew + (tid - lane) * P::kNodeWords) &&
+              lane == 0)
             atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
+#ifdef DSL_X2_EMIT  // cost probe (measurement builds): the same rows written twice
+          wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+#endif
           PH_MARK(6);  // history + row emission
           // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
           const bool spill = is_valid && !fits;
