@@ -28,12 +28,6 @@
 #include "kernels.hpp"
 #include "replay.hpp"
 
-// LDS budget for a k_level chunk's parent rows: with the kernel's ~11 KB of static LDS, 4
-// resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
-#ifndef DSL_ROWS_LDS_KB
-#define DSL_ROWS_LDS_KB 24
-#endif
-
 namespace dsl {
 
 void set_error(const std::string& msg);
@@ -446,7 +440,8 @@ struct BfsEngine : EngineBase {
   // Parents per chunk at most: about three passes of 256 lanes at the observed branching, within
   // the LDS budget of the staged rows.
   // LDS per staged parent: its row, fingerprint, node hashes (kernels.hpp k_level step 2) and offset
-  static constexpr size_t kRowLds = (size_t)NW * 4 + sizeof(Fp) * (1 + P::kNodes) + 4;
+  // (+16 per chunk: LdsRow::image rounds the padded row image up to 16 bytes)
+  static constexpr size_t kRowLds = (size_t)LdsRow<P>::kStride * 4 + sizeof(Fp) * (1 + P::kNodes) + 4;
   int pb_max() const {
     const int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / kRowLds);
     const int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));

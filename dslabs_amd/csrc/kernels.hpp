@@ -43,6 +43,34 @@ constexpr int kEvNone = -32768;
 // the level's reservations. A frontier is then a short list of row ranges: the segments, the
 // spill range and (multi-shard) the received range.
 constexpr int kSegs = 32;
+// LDS budget for a k_level chunk's staged parent rows: with the kernel's ~11 KB of static LDS, 4
+// resident workgroups per CU (the 4 waves/SIMD the register budget allows) fit in 160 KB.
+#ifndef DSL_ROWS_LDS_KB
+#define DSL_ROWS_LDS_KB 24
+#endif
+// Row stride of the staged parents in LDS (dwords). A packed row is a multiple of 16 B, and
+// Multi-Paxos's is 160 dwords = 0 mod 32: at stride kWords every lane-per-parent access of word c
+// (node hashes, event counts, classification, the handlers' parent reads) hits bank c mod 32, a
+// 32-way conflict per ds_read_b32 group (2.9 extra LDS cycles per LDS instruction on
+// C5). A row stride padded by DSL_LDS_PAD dwords spreads consecutive parents over the banks:
+//   pad 4 (16-B aligned rows): staged by LDS-DMA, one global_load_lds_dwordx4 per row (lanes over
+//     the row's 16-byte units), 8 distinct banks per 32 parents;
+//   pad 1 / 2: 32 / 16 distinct banks, staged through registers (LDS-DMA writes lane x 16 B);
+//   pad 0: the rows back to back, one DMA instruction per 1 KiB.
+// Default: pad 4 for a protocol whose row is 0 mod 32 dwords and has at least 64 words (one DMA
+// instruction per row is then at least 16 active lanes), else 0.
+template <class P>
+struct LdsRow {
+  static constexpr int kWords = Layout<P>::kWords;
+#ifdef DSL_LDS_PAD
+  static constexpr int kPad = DSL_LDS_PAD;
+#else
+  static constexpr int kPad = (kWords % 32 == 0 && kWords >= 64) ? 4 : 0;
+#endif
+  static constexpr int kStride = kWords + kPad;
+  // dwords of a chunk's row image (rounded to 16 B, so the fingerprints after it stay aligned)
+  static constexpr int image(int pb) { return (pb * kStride + 3) / 4 * 4; }
+};
 constexpr int kMaxSegs = kSegs + 2;
 constexpr int kSegStride = 16;  // u64 words between segment counters (one 128-byte line each)
 constexpr int kCtrSegOff = 4096;                                  // segment counters inside a counter set
@@ -235,7 +263,7 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 }
 
 // Wave-cooperative row emission: every lane with `active` has a successor (its parent row
-// `base + pidx * NW`, its canonical delta `d`) to be written to `dst`. The rows are written one
+// `base + pidx * STRIDE`, its canonical delta `d`) to be written to `dst`. The rows are written one
 // after another by the whole wavefront; the destination is never read back. Per row:
 //   - header words (node words, the record count, padding): lane o copies parent word o, or the
 //     replaced node's word, and writes it -- one coalesced 4-byte store per 64 words;
@@ -258,7 +286,7 @@ __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned lo
 // nw_lds (k_level): the changed nodes' words already in LDS, kNodeWords per lane of the workgroup
 // (s_nodew; `lane0` = the wave's first lane there): a header word then comes from one LDS read
 // instead of kNodeWords readlanes and selects per row.
-template <class P>
+template <class P, int STRIDE = Layout<P>::kWords>
 __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uint64_t pidx, const Delta<P>& d,
                                           uint32_t* dst, const uint32_t* nw_lds = nullptr) {
   bool collision = false;
@@ -276,7 +304,7 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
   while (mask) {
     const int src = __ffsll((long long)mask) - 1;
     mask &= mask - 1;
-    const uint32_t* pw = base + rl64(pidx, src) * NW;
+    const uint32_t* pw = base + rl64(pidx, src) * STRIDE;
     g32* ow = (g32*)(rl64((uint64_t)(uintptr_t)dst, src));
     const int node = (int)rl32((uint32_t)d.node, src);
     const uint32_t keep = rl32(d.keep, src);
@@ -472,6 +500,55 @@ __device__ __forceinline__ void stage_lds(const uint4* src, uint4* dst, int n16)
   }
 }
 
+// Copies a chunk's rows (pb rows of NW dwords, contiguous in global memory) into an LDS image of
+// row stride SP (a multiple of 4 dwords) with LDS-DMA: wave w stages rows w, w + 4, ..., one
+// wave-instruction per 64 16-byte units of a row. No wait here (as stage_lds).
+template <int NW, int SP>
+__device__ __forceinline__ void stage_rows_dma(const uint4* src, uint32_t* dst, int pb) {
+  constexpr int U = NW / 4;
+  const int lane = __lane_id();
+  for (int j = (int)(threadIdx.x >> 6); j < pb; j += (int)(blockDim.x >> 6)) {
+#pragma unroll
+    for (int b = 0; b < U; b += 64)
+      if (b + lane < U)
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + j * U + b + lane),
+                                         (__attribute__((address_space(3))) void*)(dst + j * SP + 4 * b), 16, 0, 0);
+  }
+}
+
+// Copies a chunk's rows (pb rows of NW dwords, contiguous in global memory) into an LDS image of
+// row stride SP > NW through registers: every thread issues all its 16-byte loads before its first
+// LDS store (the chunk is at most DSL_ROWS_LDS_KB, i.e. a fixed number of units per thread).
+template <int NW, int SP>
+__device__ __forceinline__ void stage_rows_padded(const uint4* src, uint32_t* dst, int pb) {
+  constexpr int U = NW / 4;  // 16-byte units per row
+  constexpr int kIt = (DSL_ROWS_LDS_KB * 1024 / 16 + kLevelBlock - 1) / kLevelBlock;
+  const int n16 = pb * U;
+  uint4 v[kIt];
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    const int u = (int)threadIdx.x + it * kLevelBlock;
+    if (u < n16) v[it] = src[u];
+  }
+#pragma unroll
+  for (int it = 0; it < kIt; it++) {
+    const int u = (int)threadIdx.x + it * kLevelBlock;
+    if (u < n16) {
+      const int j = u / U, c = u - j * U;
+      uint32_t* o = dst + j * SP + 4 * c;
+      if constexpr (SP % 2 == 0) {
+        reinterpret_cast<uint2*>(o)[0] = make_uint2(v[it].x, v[it].y);
+        reinterpret_cast<uint2*>(o)[1] = make_uint2(v[it].z, v[it].w);
+      } else {
+        o[0] = v[it].x;
+        o[1] = v[it].y;
+        o[2] = v[it].z;
+        o[3] = v[it].w;
+      }
+    }
+  }
+}
+
 // Terminal candidates of a level are reduced EXACTLY by priority (EXCEPTION > INVARIANT > GOAL,
 // Search.java:370-385), then by the successor's fingerprint (a deterministic tie-break): a wave
 // takes the minimum key of its candidates and folds it into LevelCounters::term_best with one
@@ -527,14 +604,15 @@ struct LevelWaves<P, std::void_t<decltype(P::kLevelWaves)>> : std::integral_cons
 template <class P, bool ROUTE>
 __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
+  constexpr int SP = LdsRow<P>::kStride;  // row stride of the staged parents in LDS
   constexpr int NWAVE = kLevelBlock / 64;
   // handler classes: messages, timers, then the events whose handler surely changes nothing
   // (NoopFilter: counted as successors and never run; they sort last and the passes stop before them)
   constexpr int NC = P::kMsgClasses + 2;
   static_assert(P::kNodes * 256 < 32768 && P::kNetCap < 32768, "a located event fits s_ev's 16 bits");
   extern __shared__ __align__(16) uint32_t lds[];
-  uint32_t* rows = lds;                                    // a.PB (max) * NW
-  Fp* fps = reinterpret_cast<Fp*>(rows + a.PB * NW);       // a.PB
+  uint32_t* rows = lds;                                           // a.PB (max) rows, stride SP
+  Fp* fps = reinterpret_cast<Fp*>(rows + LdsRow<P>::image(a.PB));  // a.PB
   Fp* nh = fps + a.PB;                                     // a.PB * kNodes: the parents' node hashes
   int* off = reinterpret_cast<int*>(nh + a.PB * P::kNodes);  // a.PB + 1
   __shared__ SegTable s_segs;
@@ -629,7 +707,12 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     // 1. stage the parents (contiguous rows) and their fingerprints in LDS: LDS-DMA
     //    (global_load_lds_dwordx4, 1 KiB per wave-instruction, no VGPRs), every load in flight
     //    before the one wait
-    stage_lds(reinterpret_cast<const uint4*>(a.cur + p0 * NW), reinterpret_cast<uint4*>(rows), pb * NW / 4);
+    if constexpr (SP == NW)
+      stage_lds(reinterpret_cast<const uint4*>(a.cur + p0 * NW), reinterpret_cast<uint4*>(rows), pb * NW / 4);
+    else if constexpr (SP % 4 == 0)
+      stage_rows_dma<NW, SP>(reinterpret_cast<const uint4*>(a.cur + p0 * NW), rows, pb);
+    else
+      stage_rows_padded<NW, SP>(reinterpret_cast<const uint4*>(a.cur + p0 * NW), rows, pb);
     stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -640,7 +723,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     //    exclusive scan (wave scans); the scan's barrier also publishes the hashes
     for (int x = tid; x < pb * P::kNodes; x += kLevelBlock) {
       const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
-      nh[x] = node_hash<P>(ii, rows + jj * NW + ii * P::kNodeWords);
+      nh[x] = node_hash<P>(ii, rows + jj * SP + ii * P::kNodeWords);
     }
     int total;
     if (pb <= 64) {  // one wave's worth of parents: wave 0 scans them alone, one barrier
@@ -648,7 +731,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         int x = 0;
         if (lane < pb)
           x = (ROUTE && a.owner_filter && owner_of(fps[lane], a.W) != a.me) ? 0
-                                                                           : count_events<P>(rows + lane * NW, prm, set);
+                                                                           : count_events<P>(rows + lane * SP, prm, set);
         x = (int)wave_incl_sum((uint32_t)x);
         if (lane < pb) off[lane + 1] = x;
         if (lane == 0) off[0] = 0;
@@ -661,7 +744,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
       int x = 0;
       if (tid < pb)
         x = (ROUTE && a.owner_filter && owner_of(fps[tid], a.W) != a.me) ? 0
-                                                                        : count_events<P>(rows + tid * NW, prm, set);
+                                                                        : count_events<P>(rows + tid * SP, prm, set);
       x = (int)wave_incl_sum((uint32_t)x);
       if (lane == 63) s_wsum[wid] = x;
       __syncthreads();
@@ -693,7 +776,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         if (j < pb) {
           const int e0 = off[j];
           const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
-          const uint32_t* w = rows + j * NW;
+          const uint32_t* w = rows + j * SP;
           for (int q = lo + sub; q < hi; q += tpp) {
             int ev;
             s_par[q - w0] = (uint8_t)j;
@@ -818,7 +901,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const int u = s_perm[t];
           j = s_par[u];
           k = w0 + u - off[j];
-          const uint32_t* w = rows + j * NW;
+          const uint32_t* w = rows + j * SP;
           uint32_t* my_nw = s_nodew + tid * P::kNodeWords;  // the changed node's words, for the judge
           int rc, dnode = 0, dn = 0;
           bool noop = false;
@@ -904,17 +987,17 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const bool fits = is_valid && li < a.segcap;
           const uint64_t idx = (uint64_t)seg * a.segcap + li;
           if (fits) {
-            const uint32_t* w = rows + j * NW;
+            const uint32_t* w = rows + j * SP;
             a.next_fp[idx] = f;
             a.next_parent[idx] = ((uint64_t)a.me << 48) | (p0 + j);
             a.next_event[idx] = (uint32_t)k;
             c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
           }
-          if (wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW, s_nodew + (tid - lane) * P::kNodeWords) &&
+          if (wave_emit<P, SP>(fits, rows, (uint64_t)j, d, a.next + idx * NW, s_nodew + (tid - lane) * P::kNodeWords) &&
               lane == 0)
             atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
 #ifdef DSL_X2_EMIT  // cost probe (measurement builds): the same rows written twice
-          wave_emit<P>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
+          wave_emit<P, SP>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
 #endif
           PH_MARK(6);  // history + row emission
           // beyond the segment's rows: spill (parent, event); materialized after the level (rare)
