@@ -272,6 +272,40 @@ def gen_deep(names=None):
         json.dump(out, f, indent=1)
 
 
+# Deep vectors of the multithreaded host BFS (tools/cpu_bfs.cpp): another engine than the kernels
+# (a host visited set and host frontiers) over the same packed transition functions, for depths the
+# oracle cannot reach in this container. The whole C3 bench configuration (BASELINE C3, maxDepth 10,
+# 780,909,037 states: a 2^31-slot host table of 16 GiB plus the depth-9 frontier) runs on the build
+# container's 8 cores in minutes; its depth-0..8 prefix is the oracle's synth_c3_d8.
+# python tests/golden/make_golden.py deep-cpu
+DEEP_CPU = {
+    "synth_c3_d10_cpu_bfs": dict(workload="synthetic", depth=10, table_log2=31),
+}
+
+
+def gen_deep_cpu(names=None):
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    import bench
+    from tools import cpu_baseline
+    path = os.path.join(HERE, "deep.json")
+    out = json.load(open(path)) if os.path.exists(path) else {}
+    for name, c in DEEP_CPU.items():
+        if names and name not in names:
+            continue
+        proto, s, _ = bench.build_search(c["workload"], c["depth"])
+        t0 = time.time()
+        r = cpu_baseline.run(proto, s, table_log2=c["table_log2"], timeout=6 * 3600)
+        out[name] = {"source": "tools/cpu_bfs.cpp via tools/cpu_baseline.run (bench.build_search(%r, %d))"
+                               % (c["workload"], c["depth"]),
+                     "end": r["end"], "states": r["states"], "max_depth": len(r["per_depth"]) - 1,
+                     "per_depth": r["per_depth"], "threads": r["threads"], "table_log2": c["table_log2"],
+                     "elapsed_s": round(time.time() - t0, 1)}
+        print(name, r["end"], r["states"], out[name]["elapsed_s"])
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+
+
 if __name__ == "__main__":
     which = set(sys.argv[1:]) or {"lab0", "sipaxos", "multipaxos", "synthetic", "amokv", "pb"}
     if "lab0" in which or "sipaxos" in which:
@@ -290,6 +324,8 @@ if __name__ == "__main__":
                        "results": vs["results"]}, f, indent=1)
     if "deep" in which:
         gen_deep()
+    if "deep-cpu" in which:
+        gen_deep_cpu()
     deep = {w[len("deep:"):] for w in which if w.startswith("deep:")}  # e.g. deep:synth_c3_d7
     if deep:
         gen_deep(deep)

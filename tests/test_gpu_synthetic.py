@@ -49,16 +49,16 @@ def test_synthetic_sharded(shards, rep):
 
 def test_synthetic_c3_bench_config_depth10(monkeypatch):
     """The C3 bench configuration itself (bench.py --workload synthetic: maxDepth 10, 780,909,037
-    states, a 2^31-slot table far beyond the Infinity Cache): its depth-0..8 counts equal the
-    oracle's deepest pin (tests/golden/deep.json synth_c3_d8), depth 9 equals the multithreaded host
-    BFS over the same transition functions (tools/cpu_bfs.cpp: another engine, not the kernels),
-    and both probe modes (load-first, the default at this table size; CAS-only) give the same
-    vector at full size."""
+    states, a 2^31-slot table far beyond the Infinity Cache), whole per-depth vector pinned
+    independently of the kernels: equal to the multithreaded host BFS over the same transition
+    functions run to the full depth in the build container (tests/golden/deep.json
+    synth_c3_d10_cpu_bfs, `python tests/golden/make_golden.py deep-cpu`: a host visited set and host
+    frontiers, not the device's), whose depth-0..8 prefix is the oracle's deepest pin (synth_c3_d8);
+    both probe modes (load-first, the default at this table size; CAS-only) give that vector."""
     import sys
     deep = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "deep.json")))
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
-    from tools import cpu_baseline
     proto, s, _ = bench.build_search("synthetic", 10)
     e = Engine(proto)
     try:
@@ -67,10 +67,7 @@ def test_synthetic_c3_bench_config_depth10(monkeypatch):
         r0 = e.bfs(proto.initial_state(), s)
     finally:
         e.close()
-    assert r.per_depth == r0.per_depth
-    assert r.states == sum(r.per_depth) == 780909037
-    assert r.per_depth[:9] == deep["synth_c3_d8"]["per_depth"]
-    s9 = s.clone()
-    s9.maxDepth(9)
-    c = cpu_baseline.run(proto, s9, table_log2=29)
-    assert c["per_depth"] == r.per_depth[:10], c["per_depth"]
+    cpu = deep["synth_c3_d10_cpu_bfs"]
+    assert cpu["per_depth"][:9] == deep["synth_c3_d8"]["per_depth"]
+    assert r.per_depth == r0.per_depth == cpu["per_depth"]
+    assert r.states == cpu["states"] == 780909037
