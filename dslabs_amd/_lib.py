@@ -40,7 +40,7 @@ EXPORTED = [
     "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
     "dsl_run_dfs", "dsl_replay", "dsl_human_readable_trace", "dsl_set_dropped",
 ]
-DSL_ABI_VERSION = 3  # include/dslabs_hip.h; load() refuses a library of another layout
+DSL_ABI_VERSION = 4  # include/dslabs_hip.h; load() refuses a library of another layout
 
 
 class dsl_protocol_desc(ctypes.Structure):
@@ -68,7 +68,11 @@ class dsl_settings(ctypes.Structure):
         ("table_log2_slots", ctypes.c_int32), ("n_pool", ctypes.c_int32),
         ("max_frontier_states", ctypes.c_uint64), ("memory_budget_bytes", ctypes.c_uint64),
         ("pool", dsl_predicate * DSL_MAX_POOL),
+        ("do_checks", ctypes.c_int32), ("check_sample", ctypes.c_int32),
     ]
+
+
+DSL_CHECKS_NONE, DSL_CHECKS_ERRORS, DSL_CHECKS_ALL = 0, 1, 2  # dsl_settings.do_checks
 
 
 class dsl_engine_config(ctypes.Structure):
@@ -104,6 +108,8 @@ class dsl_result(ctypes.Structure):
         ("initial_depth", ctypes.c_int32), ("elapsed_s", ctypes.c_double),
         ("successors", ctypes.c_uint64), ("new_states_inserted", ctypes.c_uint64),
         ("exchanged_states", ctypes.c_uint64), ("level_ms_max", ctypes.c_double),
+        ("checks_run", ctypes.c_uint64), ("not_deterministic", ctypes.c_uint64), ("not_idempotent", ctypes.c_uint64),
+        ("first_not_deterministic", dsl_event), ("first_not_idempotent", dsl_event),
     ]
 
 
@@ -116,7 +122,8 @@ class dsl_stats(ctypes.Structure):
                 ("sharded_levels", ctypes.c_uint64), ("probes", ctypes.c_uint64),
                 ("host_syncs", ctypes.c_uint64), ("table_rehashes", ctypes.c_uint64),
                 ("rccl_version", ctypes.c_int32), ("level_slots", ctypes.c_int32),
-                ("cost_c_ns", ctypes.c_double), ("cost_x_us", ctypes.c_double), ("shard_work_min", ctypes.c_uint64)]
+                ("cost_c_ns", ctypes.c_double), ("cost_x_us", ctypes.c_double), ("shard_work_min", ctypes.c_uint64),
+                ("exchange_rounds", ctypes.c_uint64), ("fast_levels", ctypes.c_uint64), ("completions", ctypes.c_uint64)]
 
 
 _lib = None

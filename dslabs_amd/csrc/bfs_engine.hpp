@@ -64,6 +64,12 @@ struct Comm {
   virtual bool device_collectives() const { return false; }
   virtual int allgather_dev(const uint64_t*, int, uint64_t*, hipStream_t) { return DSL_ERR_COMM; }
   virtual int version() const { return 0; }
+  // RCCL: the communicator's asynchronous error (ncclCommGetAsyncError: a peer that died, a
+  // network failure), polled while the host waits on the stream; abort() ends every outstanding
+  // operation of the communicator (ncclCommAbort), so a failed rank ends the search on every rank
+  // with DSL_ERR_COMM instead of leaving the others blocked in a collective.
+  virtual int async_error() { return DSL_OK; }
+  virtual void abort() {}
 };
 
 struct EngineBase {
@@ -130,6 +136,17 @@ struct BfsEngine : EngineBase {
     int nseg = 1;
     std::vector<uint64_t> level_size;  // rows of each level's frontier (history entries)
     uint64_t cap_fp = 0;
+    uint64_t* rspill = nullptr;  // route-spilled successors (k_level ROUTE past a region)
+    uint64_t rspill_cap = 0;
+    FpRec* out2 = nullptr;       // completion phase: re-routed route spills, W regions
+    uint64_t out2_cap = 0;
+    uint8_t* rep2 = nullptr;     // ... and the owners' answers to them
+    uint64_t rep2_cap = 0;
+    uint64_t rs_cap = 0;         // records per out2 / rep2 region
+    // a sharded level's next-frontier layout (rows): [0, seg_span) the segments, [seg_span,
+    // + uns_room) rows k_unspill appends (fast path), [seg_span + uns_room, + mat_room) rows
+    // k_materialize appends, [ovf_base, + ovf_cnt) spills past uns_room (completion phase)
+    uint64_t seg_span = 0, uns_room = 0, mat_room = 0, ovf_base = 0, ovf_cnt = 0;
     LevelCounters lc{};
   };
 
@@ -151,7 +168,9 @@ struct BfsEngine : EngineBase {
   unsigned long long* rehash_err = nullptr;
   // multi-rank exchange scratch: the route-count matrix and the level records (kernels.hpp
   // k_level_record), on the device and pinned on the host
-  static constexpr int kXWords = kMaxShards * kMaxShards + (kMaxShards + 1) * kRecWords;
+  // [0, kMaxShards * kRecWords): the local shards' records; then the gathered records (RCCL);
+  // then the completion phase's route-spill counts (kMaxShards x kMaxShards)
+  static constexpr int kXWords = 2 * kMaxShards * kRecWords + kMaxShards * kMaxShards;
   uint64_t* xdev = nullptr;
   // the device-side deadline of a time-limited search (LevelArgs::budget_rt): the device clock at
   // the search's start (k_clock) and the budget in its ticks; not used in a replicated level of a
@@ -163,19 +182,44 @@ struct BfsEngine : EngineBase {
   uint64_t* xhost = nullptr;
   uint64_t* segs_dev = nullptr;   // virtual shards: the segment tables of the two exchange rounds
   uint64_t* segs_host = nullptr;
-  uint64_t seg_round = 0;
+  uint64_t seg_round = 0, seg_since_sync = 0;
+  static constexpr int kSegTables = 8;
   // One host round trip (counted in dsl_stats.host_syncs). The host polls the stream instead of
   // blocking in hipStreamSynchronize: a search is ~1 ms of device work with one or two waits, and a
   // blocked thread's wake-up latency (tens of microseconds, varying by host) is paid per search.
   // DSL_BLOCKING_SYNC=1 restores the blocking wait.
   bool spin_sync = !getenv("DSL_BLOCKING_SYNC");
+  // With a communicator the wait also polls its asynchronous error and a deadline
+  // (DSL_COMM_TIMEOUT_MS, default 300 s): either aborts the communicator and fails the search.
+  const double comm_timeout_ms = getenv("DSL_COMM_TIMEOUT_MS") ? atof(getenv("DSL_COMM_TIMEOUT_MS")) : 300000.0;
+  bool comm_failed = false;
+  int comm_fail(const std::string& why) {
+    comm_failed = true;
+    if (comm) comm->abort();
+    set_error("multi-GPU exchange failed on rank " + std::to_string(comm ? comm->rank() : 0) + ": " + why +
+              " (communicator aborted)");
+    return DSL_ERR_COMM;
+  }
   int hsync() {
-    if (spin_sync) {
+    if (comm) {
+      const auto t0 = std::chrono::steady_clock::now();
+      hipError_t e;
+      for (uint64_t it = 0; (e = hipStreamQuery(stream)) == hipErrorNotReady; it++) {
+        if ((it & 1023) == 1023) {
+          if (comm->async_error() != DSL_OK) return comm_fail("asynchronous communicator error");
+          if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > comm_timeout_ms)
+            return comm_fail("no progress within DSL_COMM_TIMEOUT_MS");
+        }
+      }
+      if (e != hipSuccess) DSL_HIP(e);
+    } else if (spin_sync) {
+      seg_since_sync = 0;
       hipError_t e;
       while ((e = hipStreamQuery(stream)) == hipErrorNotReady) {
       }
       if (e != hipSuccess) DSL_HIP(e);
     } else {
+      seg_since_sync = 0;
       DSL_HIP(hipStreamSynchronize(stream));
     }
     stats.host_syncs++;
@@ -257,7 +301,7 @@ struct BfsEngine : EngineBase {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,
                       s.out_fp,    s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
-                      s.find_ctr};
+                      s.find_ctr,  s.rspill,   s.out2,    s.rep2};
       for (void* q : ptrs) (void)hipFree(q);
       for (auto* q : s.hpar) (void)hipFree(q);
       for (auto* q : s.hev) (void)hipFree(q);
@@ -389,12 +433,16 @@ struct BfsEngine : EngineBase {
     // virtual shards: the round's segments as one table, copied by one launch (k_copy_segments)
     const int L = (int)sh.size();
     if (!segs_dev) {
-      DSL_HIP(hipMalloc(&segs_dev, 2 * 3 * kMaxShards * kMaxShards * 8));
-      DSL_HIP(hipHostMalloc(&segs_host, 2 * 3 * kMaxShards * kMaxShards * 8));
+      DSL_HIP(hipMalloc(&segs_dev, kSegTables * 3 * kMaxShards * kMaxShards * 8));
+      DSL_HIP(hipHostMalloc(&segs_host, kSegTables * 3 * kMaxShards * kMaxShards * 8));
     }
-    uint64_t* h = segs_host + (seg_round & 1) * 3 * kMaxShards * kMaxShards;  // rounds alternate halves
-    uint64_t* dv = segs_dev + (seg_round & 1) * 3 * kMaxShards * kMaxShards;
+    // rounds take the pinned tables in turn; the host rewrites a table only after a host round
+    // trip has drained the copy that read it
+    if (seg_since_sync >= kSegTables) DSL_TRY(hsync());
+    uint64_t* h = segs_host + (seg_round % kSegTables) * 3 * kMaxShards * kMaxShards;
+    uint64_t* dv = segs_dev + (seg_round % kSegTables) * 3 * kMaxShards * kMaxShards;
     seg_round++;
+    seg_since_sync++;
     int n = 0;
     uint64_t maxlen = 0;
     for (int s = 0; s < L; s++)
@@ -776,6 +824,445 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
+  // ---- sharded levels: the fast path ----------------------------------------------
+  // A sharded level moves its routed fingerprints in fixed-size SLABS: source -> owner, `slab`
+  // records (plus a header record holding the count) per pair, sized before the level from the
+  // global work and the last measured routed fraction (route_frac, x1.3). No count crosses to the
+  // host before the exchange, so the level is ONE host round trip: k_level<ROUTE> ->
+  // k_route_headers -> round A (slabs) -> k_probe_slab (owners) -> round B (one answer byte per
+  // record) -> k_materialize (sources) -> k_unspill -> k_level_record -> gather of the records ->
+  // the one synchronization. The maxDepth level has no round B and no k_materialize (its routed
+  // successors were judged at the source: LevelArgs::judge_routed). Whatever did not fit (a
+  // region past its slab, records past a region, spills past their room) is flagged in the
+  // records, and every rank then runs the completion phase (complete_sharded) with host-known
+  // counts. DSL_SLAB=0 sends everything through the completion phase (the two-round-trip
+  // exchange of round 4).
+  const bool slab_mode = !(getenv("DSL_SLAB") && atoi(getenv("DSL_SLAB")) == 0);
+  double route_frac = 0;  // routed records / work items of the last sharded level (0: none yet)
+  uint64_t max_rank_work = 0;  // the next level's work of the busiest rank (0: no sharded level yet)
+
+  int sharded_capacity(Shard& S, uint64_t slab, bool last) {
+    // out_fp: W regions of cap_fp records, record 0 the header; the same cap on every rank
+    // (DSL_SLAB=0: the shard's work, the exact bound)
+    S.cap_fp = slab ? 2 * slab + 2 : std::max<uint64_t>(S.work, 1) + 1;
+    DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
+    DSL_TRY(grow(&S.rspill, &S.rspill_cap, std::max<uint64_t>(S.work, 1), false, 0));
+    DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>((slab + 1) * W, 1), false, 0));
+    DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(slab * W, 1), false, 0));
+    DSL_TRY(grow(&S.rep_in, &S.rep_in_cap, std::max<uint64_t>(S.cap_fp * W, 1), false, 0));
+    // rows: the segments, room for spills (a quarter of the segments), room for the successors
+    // the owners find new (every record of this shard's slabs, W - 1 of them)
+    S.seg_span = S.segcap * S.nseg;
+    S.uns_room = last || !slab ? 0 : S.seg_span / 4;
+    S.mat_room = last ? 0 : slab * (W - 1);
+    S.ovf_base = S.ovf_cnt = 0;
+    const uint64_t rows = S.seg_span + S.uns_room + S.mat_room;
+    DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
+    DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
+    DSL_TRY(hist_grow(S, S.level_size.size(), rows, 0));
+    return DSL_OK;
+  }
+
+  // One all-to-all round where every (source, owner) pair moves `bytes[s][d]` bytes: local shard
+  // l sends from send[l] + soff[l][d], receives at recv[l] + roff[l][s].
+  int xround(const std::vector<const uint8_t*>& snd, const Mat& so, const Mat& sb, const std::vector<uint8_t*>& rcv,
+             const Mat& ro, const Mat& rb) {
+    stats.exchange_rounds++;
+    return xfer(snd, so, sb, rcv, ro, rb);
+  }
+
+  // Every local shard's level record (k_level_record) computed on the device, gathered by every
+  // rank, read with the shards' counters in ONE host round trip; recs = W records.
+  int gather_records(const std::vector<uint64_t>& extra_rows, uint64_t slab, uint64_t time_up,
+                     std::vector<uint64_t>& recs) {
+    const int L = (int)sh.size();
+    const bool dev_gather = comm && comm->device_collectives();
+    for (int l = 0; l < L; l++) {
+      Shard& S = sh[l];
+      RecordArgs ra{};
+      ra.c = S.ctr;
+      ra.seg_ctr = S.seg_ctr;
+      ra.nseg = S.nseg;
+      ra.segcap = S.segcap;
+      ra.extra_rows = extra_rows[l];
+      ra.uns_cap = S.uns_room;
+      ra.mat_cap = S.mat_room;
+      ra.parents = S.F;
+      ra.time_up = time_up;
+      ra.gid = S.gid;
+      ra.W = W;
+      ra.rc = S.rc;
+      ra.slab = slab;
+      ra.cap_fp = S.cap_fp;
+      ra.out = xdev + (size_t)l * kRecWords;
+      hipLaunchKernelGGL(k_level_record, dim3(1), dim3(64), 0, stream, ra);
+      DSL_HIP(hipGetLastError());
+    }
+    uint64_t* gdev = xdev + (size_t)kMaxShards * kRecWords;
+    if (dev_gather) {
+      DSL_TRY(comm->allgather_dev(xdev, kRecWords, gdev, stream));
+      DSL_HIP(hipMemcpyAsync(xhost, gdev, (size_t)W * kRecWords * 8, hipMemcpyDeviceToHost, stream));
+    } else {
+      DSL_HIP(hipMemcpyAsync(xhost, xdev, (size_t)L * kRecWords * 8, hipMemcpyDeviceToHost, stream));
+    }
+    for (auto& S : sh)
+      DSL_HIP(hipMemcpyAsync(S.hctr, S.ctr, kCtrSegOff + 8 * S.nseg * kSegStride, hipMemcpyDeviceToHost, stream));
+    DSL_TRY(hsync());
+    recs.assign((size_t)W * kRecWords, 0);
+    if (comm && !dev_gather) {
+      stats.host_syncs++;
+      DSL_TRY(comm->allgather_u64(xhost, kRecWords, recs.data(), stream));
+    } else if (comm) {
+      std::memcpy(recs.data(), xhost, recs.size() * 8);
+    } else {
+      for (int l = 0; l < L; l++)
+        std::memcpy(recs.data() + (size_t)sh[l].gid * kRecWords, xhost + (size_t)l * kRecWords, kRecWords * 8);
+    }
+    for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
+    return DSL_OK;
+  }
+
+  int sharded_fast(int depth, bool last, uint64_t slab, uint64_t time_up, std::vector<uint64_t>& recs,
+                   std::vector<std::vector<uint64_t>>& nbase, std::vector<std::vector<uint64_t>>& ncnt,
+                   std::vector<uint64_t>& span) {
+    const int L = (int)sh.size();
+    Mat so(L, std::vector<uint64_t>(W, 0)), sb = so, ro = so, rb = so;
+    std::vector<const uint8_t*> snd(L);
+    std::vector<uint8_t*> rcv(L);
+    const size_t R = sizeof(FpRec);
+    if (slab) {
+      for (auto& S : sh) {
+        hipLaunchKernelGGL(k_route_headers, dim3(1), dim3(64), 0, stream, (const RouteCounters*)S.rc, S.out_fp,
+                           S.cap_fp, W);
+        DSL_HIP(hipGetLastError());
+      }
+      // round A: the slabs (header + slab records) of every (source, owner) pair
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        for (int d = 0; d < W; d++) {
+          const uint64_t n = d == S.gid ? 0 : (slab + 1) * R;
+          so[l][d] = (uint64_t)d * S.cap_fp * R;
+          sb[l][d] = n;
+          ro[l][d] = (uint64_t)d * (slab + 1) * R;
+          rb[l][d] = n;
+        }
+        snd[l] = reinterpret_cast<const uint8_t*>(S.out_fp);
+        rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
+      }
+      DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
+      for (auto& S : sh) {
+        ProbeSlabArgs pa{};
+        pa.in = S.in_fp;
+        pa.slab = slab;
+        pa.W = W;
+        pa.me = S.gid;
+        pa.table = tbl;
+        pa.table.slots = S.table;
+        pa.reply = last ? nullptr : S.rep_out;
+        pa.ctr = S.ctr;
+        const int blocks = (int)std::min<uint64_t>((slab * W + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(k_probe_slab, dim3(std::max(1, blocks)), dim3(kBlock), 0, stream, pa);
+        DSL_HIP(hipGetLastError());
+      }
+      if (!last) {
+        // round B: one answer byte per record, back to its source (the slab's layout, reversed)
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          for (int d = 0; d < W; d++) {
+            const uint64_t n = d == S.gid ? 0 : slab;
+            so[l][d] = (uint64_t)d * slab;
+            sb[l][d] = n;
+            ro[l][d] = (uint64_t)d * S.cap_fp;
+            rb[l][d] = n;
+          }
+          snd[l] = S.rep_out;
+          rcv[l] = S.rep_in;
+        }
+        DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
+        for (auto& S : sh) DSL_TRY(launch_materialize(S, depth, slab, 0, nullptr));
+      }
+    }
+    for (auto& S : sh) {
+      if (!S.uns_room) continue;
+      const size_t lv = S.level_size.size();
+      const int blocks = (int)std::min<uint64_t>((S.uns_room + kBlock - 1) / kBlock, 8192);
+      hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, S.uns_room, S.cur, S.cur_fp,
+                         S.next, S.next_fp, S.hpar[lv], S.hev[lv], S.seg_span, S.gid, S.ctr, prm, dset,
+                         (const unsigned long long*)&S.ctr->spilled);
+      DSL_HIP(hipGetLastError());
+    }
+    std::vector<uint64_t> extra(L, 0);
+    DSL_TRY(gather_records(extra, slab, time_up, recs));
+    bool incomplete = false, errors = false;
+    for (int x = 0; x < W; x++) {
+      const uint64_t* r = recs.data() + (size_t)x * kRecWords;
+      incomplete |= r[kRecIncomplete] != 0;
+      errors |= (r[kRecErrOverflow] | r[kRecErrTable] | r[kRecErrFrontier]) != 0;
+    }
+    if (getenv("DSL_LEVEL_TRACE")) {
+      fprintf(stderr, "[shard] depth %d slab %llu last %d:", depth + 1, (unsigned long long)slab, last ? 1 : 0);
+      for (int x = 0; x < W; x++) {
+        const uint64_t* r = recs.data() + (size_t)x * kRecWords;
+        uint64_t mx = 0;
+        for (int d = 0; d < W; d++)
+          if (d != x) mx = std::max<uint64_t>(mx, r[kRecRoute + d]);
+        fprintf(stderr, " [%d: work %llu max_route %llu inc %llu]", x, (unsigned long long)r[kRecWork],
+                (unsigned long long)mx, (unsigned long long)r[kRecIncomplete]);
+      }
+      fprintf(stderr, "\n");
+    }
+    if (incomplete && !errors) {
+      stats.completions++;
+      DSL_TRY(complete_sharded(depth, last, slab, time_up, recs));
+    } else {
+      stats.fast_levels++;
+    }
+    for (auto& S : sh) DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
+    // the next frontier of every local shard: segments, unspilled rows, materialized rows, and
+    // the completion phase's spills
+    for (int l = 0; l < L; l++) {
+      Shard& S = sh[l];
+      std::vector<unsigned long long> seg(kSegs * kSegStride);
+      std::memcpy(seg.data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
+      for (int q = 0; q < S.nseg; q++) {
+        const uint64_t c = std::min<uint64_t>(seg[(size_t)q * kSegStride], S.segcap);
+        if (c) {
+          nbase[l].push_back((uint64_t)q * S.segcap);
+          ncnt[l].push_back(c);
+        }
+      }
+      const uint64_t un = std::min<uint64_t>(S.lc.spilled, S.uns_room);
+      if (un) {
+        nbase[l].push_back(S.seg_span);
+        ncnt[l].push_back(un);
+      }
+      const uint64_t mat = std::min<uint64_t>(S.lc.next_size, S.mat_room);
+      if (mat) {
+        nbase[l].push_back(S.seg_span + S.uns_room);
+        ncnt[l].push_back(mat);
+      }
+      if (S.ovf_cnt) {
+        nbase[l].push_back(S.ovf_base);
+        ncnt[l].push_back(S.ovf_cnt);
+      }
+      span[l] = std::max(S.seg_span + S.uns_room + S.mat_room, S.ovf_base + S.ovf_cnt);
+    }
+    return DSL_OK;
+  }
+
+  // k_materialize of shard S: the fast path's slabs (dev counts, off == null) or host-known
+  // counts off[] of region `skip` onwards (the completion phase), appended at seg_span + uns_room.
+  int launch_materialize(Shard& S, int depth, uint64_t slab, uint64_t skip, const uint64_t* off,
+                         const FpRec* sent = nullptr, const uint8_t* reply = nullptr, uint64_t cap = 0, int hdr = 1) {
+    const size_t lv = S.level_size.size();
+    MaterializeArgs<P> ma{};
+    ma.sent = sent ? sent : S.out_fp;
+    ma.reply = reply ? reply : S.rep_in;
+    ma.cap = cap ? cap : S.cap_fp;
+    ma.hdr = hdr;
+    ma.skip = skip;
+    ma.W = W;
+    uint64_t total = 0;
+    if (off) {
+      for (int d = 0; d <= kMaxShards; d++) ma.off[d] = off[d];
+      total = off[kMaxShards];
+    } else {
+      ma.dev_cnt = S.rc;
+      ma.slab = slab;
+      total = slab * (W - 1);
+    }
+    if (!total) return DSL_OK;
+    ma.cur = S.cur;
+    ma.cur_fp = S.cur_fp;
+    ma.me = S.gid;
+    ma.depth = depth + 1;
+    ma.incremental = depth > init_depth ? 1 : 0;
+    ma.next = S.next;
+    ma.next_fp = S.next_fp;
+    ma.next_parent = S.hpar[lv];
+    ma.next_event = S.hev[lv];
+    ma.next_base = S.seg_span + S.uns_room;
+    ma.next_cap = S.mat_room;
+    ma.ctr = S.ctr;
+    ma.terms = S.terms;
+    ma.term_cap = term_cap;
+    const int blocks = (int)std::min<uint64_t>((total + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
+    DSL_HIP(hipGetLastError());
+    return DSL_OK;
+  }
+
+  // The completion phase of a sharded level (every rank, when any record is incomplete): with the
+  // gathered route counts, (1) the route-spilled successors are re-fingerprinted per owner
+  // (k_respill; their counts gathered: a host round trip), (2) the records past each slab and (3)
+  // the re-routed ones go through a host-sized exchange round each (probe, answers,
+  // materialization), (4) spills past their room are materialized, then the records are gathered
+  // again. Rare: the slab is 1.3x the expected records per pair.
+  int complete_sharded(int depth, bool last, uint64_t slab, uint64_t time_up, std::vector<uint64_t>& recs) {
+    const int L = (int)sh.size();
+    const size_t R = sizeof(FpRec);
+    const size_t lv = sh[0].level_size.size();
+    auto route = [&](int s, int d) { return recs[(size_t)s * kRecWords + kRecRoute + d]; };
+    auto cap_of = [&](int s) { return recs[(size_t)s * kRecWords + kRecCap]; };
+    // (1) route spills -> out2, per owner; the count matrix gathered
+    Mat rs(W, std::vector<uint64_t>(W, 0));
+    {
+      std::vector<uint64_t> nrs(L);
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        nrs[l] = std::min<uint64_t>(S.lc.route_spilled, S.rspill_cap);
+        S.rs_cap = std::max<uint64_t>(nrs[l], 1);
+        DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
+        if (!nrs[l]) continue;
+        DSL_TRY(grow(&S.out2, &S.out2_cap, nrs[l] * W, false, 0));
+        const int blocks = (int)std::min<uint64_t>((nrs[l] + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(k_respill<P>, dim3(blocks), dim3(kBlock), 0, stream, (const uint64_t*)S.rspill, nrs[l],
+                           (const uint32_t*)S.cur, (const Fp*)S.cur_fp, W, S.out2, S.rs_cap, S.rc, S.ctr, prm, dset);
+        DSL_HIP(hipGetLastError());
+      }
+      uint64_t* h = xhost + 2 * (size_t)kMaxShards * kRecWords;
+      for (int l = 0; l < L; l++)
+        DSL_HIP(hipMemcpyAsync(h + (size_t)l * kMaxShards, sh[l].rc, kMaxShards * 8, hipMemcpyDeviceToHost, stream));
+      DSL_TRY(hsync());
+      std::vector<uint64_t> mine((size_t)L * W), all((size_t)W * W);
+      for (int l = 0; l < L; l++)
+        for (int d = 0; d < W; d++) mine[(size_t)l * W + d] = h[(size_t)l * kMaxShards + d];
+      if (comm) {
+        stats.host_syncs++;
+        DSL_TRY(comm->allgather_u64(mine.data(), W, all.data(), stream));
+      } else {
+        for (int l = 0; l < L; l++)
+          for (int d = 0; d < W; d++) all[(size_t)sh[l].gid * W + d] = mine[(size_t)l * W + d];
+      }
+      for (int x = 0; x < W; x++)
+        for (int d = 0; d < W; d++) rs[x][d] = all[(size_t)x * W + d];
+      for (int l = 0; l < L; l++) DSL_HIP(hipMemsetAsync(sh[l].rc, 0, sizeof(RouteCounters), stream));
+    }
+    // rows: the materialized room grows by everything this shard may still get back
+    for (int l = 0; l < L; l++) {
+      Shard& S = sh[l];
+      const int g = S.gid;
+      uint64_t more = 0;
+      for (int d = 0; d < W; d++) {
+        if (d == g) continue;
+        const uint64_t in_region = std::min<uint64_t>(route(g, d), cap_of(g) - 1);
+        more += (in_region > slab ? in_region - slab : 0) + rs[g][d];
+      }
+      const uint64_t used = S.seg_span + S.uns_room + S.mat_room;
+      const uint64_t ovf = S.lc.spilled > S.uns_room ? std::min<uint64_t>(S.lc.spilled, S.spill_cap) - S.uns_room : 0;
+      const uint64_t need = used + more + ovf;
+      if (need > used) {
+        DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, used));
+        DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, used));
+        DSL_TRY(hist_grow(S, lv, need, used));
+      }
+      S.mat_room += more;
+      S.ovf_base = S.seg_span + S.uns_room + S.mat_room;
+      S.ovf_cnt = ovf;
+    }
+    // (2) the records past each slab, (3) the re-routed ones: two host-sized rounds
+    for (int pass = 0; pass < 2; pass++) {
+      Mat cnt(W, std::vector<uint64_t>(W, 0));
+      for (int x = 0; x < W; x++)
+        for (int d = 0; d < W; d++) {
+          if (d == x) continue;
+          if (pass == 0) {
+            const uint64_t in_region = std::min<uint64_t>(route(x, d), cap_of(x) - 1);
+            cnt[x][d] = in_region > slab ? in_region - slab : 0;
+          } else {
+            cnt[x][d] = rs[x][d];
+          }
+        }
+      bool any = false;
+      for (int x = 0; x < W; x++)
+        for (int d = 0; d < W; d++) any |= cnt[x][d] != 0;
+      if (!any) continue;
+      Mat so(L, std::vector<uint64_t>(W, 0)), sb = so, ro = so, rb = so;
+      std::vector<const uint8_t*> snd(L);
+      std::vector<uint8_t*> rcv(L);
+      std::vector<uint64_t> nin(L, 0);
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        const int g = S.gid;
+        uint64_t roff = 0;
+        for (int d = 0; d < W; d++) {
+          const uint64_t rcap = pass == 0 ? S.cap_fp : S.rs_cap;
+          so[l][d] = pass == 0 ? ((uint64_t)d * S.cap_fp + 1 + slab) * R : (uint64_t)d * rcap * R;
+          sb[l][d] = cnt[g][d] * R;
+          ro[l][d] = roff * R;
+          rb[l][d] = cnt[d][g] * R;
+          roff += cnt[d][g];
+        }
+        nin[l] = roff;
+        DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>(roff, 1), false, 0));
+        DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(roff, 1), false, 0));
+        snd[l] = reinterpret_cast<const uint8_t*>(pass == 0 ? S.out_fp : S.out2);
+        rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
+      }
+      DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        if (!nin[l]) continue;
+        ProbeArgs pa;
+        pa.in = S.in_fp;
+        pa.n = nin[l];
+        pa.table = tbl;
+        pa.table.slots = S.table;
+        pa.reply = S.rep_out;
+        pa.ctr = S.ctr;
+        const int blocks = (int)std::min<uint64_t>((nin[l] + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(k_probe_remote, dim3(blocks), dim3(kBlock), 0, stream, pa);
+        DSL_HIP(hipGetLastError());
+      }
+      if (last) continue;  // the maxDepth level: judged at the source, nothing comes back
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        const int g = S.gid;
+        if (pass == 1) DSL_TRY(grow(&S.rep2, &S.rep2_cap, S.rs_cap * W, false, 0));
+        const uint64_t rcap = pass == 0 ? S.cap_fp : S.rs_cap;
+        uint64_t soff = 0;
+        for (int d = 0; d < W; d++) {
+          so[l][d] = soff;
+          sb[l][d] = cnt[d][g];
+          soff += cnt[d][g];
+          ro[l][d] = (uint64_t)d * rcap + (pass == 0 ? slab : 0);
+          rb[l][d] = cnt[g][d];
+        }
+        snd[l] = S.rep_out;
+        rcv[l] = pass == 0 ? S.rep_in : S.rep2;
+      }
+      DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
+      for (int l = 0; l < L; l++) {
+        Shard& S = sh[l];
+        const int g = S.gid;
+        uint64_t off[kMaxShards + 1] = {0};
+        for (int d = 0; d < kMaxShards; d++) off[d + 1] = off[d] + (d < W ? cnt[g][d] : 0);
+        if (pass == 0)
+          DSL_TRY(launch_materialize(S, depth, slab, slab, off));
+        else
+          DSL_TRY(launch_materialize(S, depth, slab, 0, off, S.out2, S.rep2, S.rs_cap, 0));
+      }
+    }
+    // (4) spills past their room
+    std::vector<uint64_t> extra(L, 0);
+    for (int l = 0; l < L; l++) {
+      Shard& S = sh[l];
+      if (!S.ovf_cnt) continue;
+      const int blocks = (int)std::min<uint64_t>((S.ovf_cnt + kBlock - 1) / kBlock, 8192);
+      hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, (const uint64_t*)(S.spill + S.uns_room),
+                         S.ovf_cnt, (const uint32_t*)S.cur, (const Fp*)S.cur_fp, S.next, S.next_fp, S.hpar[lv], S.hev[lv],
+                         S.ovf_base, S.gid, S.ctr, prm, dset, nullptr);
+      DSL_HIP(hipGetLastError());
+      extra[l] = S.ovf_cnt;
+    }
+    // the route counts of the records stay the level's (rc was reused by k_respill)
+    std::vector<uint64_t> keep(recs);
+    DSL_TRY(gather_records(extra, ~0ull, time_up, recs));
+    for (int x = 0; x < W; x++)
+      for (int d = 0; d < kMaxShards; d++) recs[(size_t)x * kRecWords + kRecRoute + d] = keep[(size_t)x * kRecWords + kRecRoute + d];
+    return DSL_OK;
+  }
+
   // Search.run for BFS. A search whose visited table ran out of room (est_new_states far off:
   // more new states in one level than twice the estimate) is run again from a first table twice
   // the size it reached -- the table grows instead of failing, up to the memory budget.
@@ -806,6 +1293,10 @@ struct BfsEngine : EngineBase {
 
   int run_once(dsl_result** out) {
     const auto t_start = t_run0;
+    if (comm_failed) {
+      set_error("the engine's communicator was aborted by an earlier failure: create a new engine");
+      return DSL_ERR_COMM;
+    }
     (void)hipGetLastError();  // the per-thread sticky error must not blame this search for an older call
     if (!stream) {
       if (cfg.device >= 0) DSL_HIP(hipSetDevice(cfg.device));
@@ -908,6 +1399,7 @@ struct BfsEngine : EngineBase {
     // hash-sharded. Per-level latency of a sharded level is ~3 exchange rounds, so sharding a
     // level pays only once it has enough work.
     bool rep_active = W > 1 && rep_threshold() > 0;
+    max_rank_work = 0;
     bool first_sharded = W > 1 && !rep_active;
     // checkState of the initial state: the same judge, on the host (no round trip before the
     // first level); k_setup only inserts its fingerprint
@@ -972,7 +1464,7 @@ struct BfsEngine : EngineBase {
       fprintf(stderr, "[setup] %.4f ms\n",
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
 
-    if (comm && !xdev) {
+    if (W > 1 && !xdev) {
       DSL_HIP(hipMalloc(&xdev, kXWords * 8));
       DSL_HIP(hipHostMalloc(&xhost, kXWords * 8));
     }
@@ -1062,6 +1554,21 @@ struct BfsEngine : EngineBase {
         uint64_t Fmax = 0;
         for (auto& S : sh) Fmax = std::max(Fmax, S.F);
         const int PB = chunk_parents(Fmax, route);
+        // a sharded level: the slab (records per source -> owner pair the fast path moves without
+        // the host reading any count), from the global work and the last measured routed fraction;
+        // identical on every rank (its inputs are). The maxDepth level expands nothing further.
+        const bool last_level = hset.max_depth >= 0 && depth + 1 >= hset.max_depth;
+        uint64_t slab = 0;
+        if (route && slab_mode) {
+          // the most work one rank has: from the last sharded level's records; after replicated
+          // levels every rank expands the parents it owns (hash-balanced, g/W); a search sharded
+          // from its first level starts on the initial state's owner alone
+          const double per_rank = max_rank_work ? (double)max_rank_work
+                                  : rep_threshold() > 0 ? (double)g[2] / W : (double)g[2];
+          const double frac = route_frac > 0 ? route_frac : 1.0;
+          slab = (uint64_t)(1.3 * frac * per_rank / (W - 1)) + 64;
+          if (const char* m = getenv("DSL_SLAB_MAX")) slab = std::min<uint64_t>(slab, std::max(1, atoi(m)));  // tests
+        }
         const int lslots = level_slots((size_t)pb_max() * kRowLds + 16, route);
         if (queued) {
           sh[0].nseg = kSegs;
@@ -1084,10 +1591,7 @@ struct BfsEngine : EngineBase {
           S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + S.cset * kCtrSet + kCtrSegOff);
           // a shard that launches no k_level this level zeroes its next set here
           if (S.F == 0) DSL_HIP(hipMemsetAsync(S.ctrbuf + (S.cset ^ 1) * kCtrSet, 0, kCtrSet, stream));
-          if (route) {
-            S.cap_fp = std::max<uint64_t>(S.work, 1);
-            DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
-          }
+          if (route) DSL_TRY(sharded_capacity(S, slab, last_level));
         }
         }  // !queued (capacity)
         const size_t lds = (size_t)PB * kRowLds + 16;
@@ -1129,6 +1633,9 @@ struct BfsEngine : EngineBase {
           a.out_fp = S.out_fp;
           a.cap_fp = S.cap_fp;
           a.rc = S.rc;
+          a.rspill = S.rspill;
+          a.rspill_cap = S.rspill_cap;
+          a.judge_routed = route && last_level ? 1 : 0;
           a.qprev = nullptr;
           a.qprev_seg = nullptr;
           a.segs.pb = PB;
@@ -1145,43 +1652,55 @@ struct BfsEngine : EngineBase {
         }
         DSL_HIP(hipEventRecord(ev1, stream));
         }  // !queued (launch)
-        // spilled VALID states: grow the next frontier and materialize them after the local rows
+        // The level's counters. A sharded level runs its exchange first (sharded_fast): the
+        // owners' probes, the materialization and every shard's level record, then ONE host round
+        // trip; a single-shard or replicated level reads its counters right after k_level.
         std::vector<std::vector<unsigned long long>> segc(L, std::vector<unsigned long long>(kSegs * kSegStride));
-        Mat rcnt(L, std::vector<uint64_t>(W, 0));  // routed records per destination shard
-        const bool dev_gather = route && comm && comm->device_collectives();
+        std::vector<std::vector<uint64_t>> nbase(L), ncnt(L);
+        std::vector<uint64_t> span(L);
+        std::vector<uint64_t> recs;  // sharded: W records of kRecWords (k_level_record), every rank's
+        const auto tx0 = std::chrono::steady_clock::now();
+        if (route) {
+          stats.sharded_levels++;
+          uint64_t time_up = 0;
+          if (hset.max_time_ms > 0 &&
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count() >
+                  hset.max_time_ms)
+            time_up = 1;
+          DSL_TRY(sharded_fast(depth, last_level, slab, time_up, recs, nbase, ncnt, span));
+          // the routed fraction of this level (all shards), for the next level's slab
+          uint64_t routed = 0, lw = 0;
+          for (int x = 0; x < W; x++) {
+            const uint64_t* r = recs.data() + (size_t)x * kRecWords;
+            lw += r[kRecWork];
+            for (int d = 0; d < W; d++)
+              if (d != x) routed += r[kRecRoute + d];
+          }
+          if (lw) route_frac = std::max(0.05, (double)routed / (double)lw);
+          max_rank_work = 0;
+          for (int x = 0; x < W; x++) max_rank_work = std::max<uint64_t>(max_rank_work, recs[(size_t)x * kRecWords + kRecNextWork]);
+          for (int l = 0; l < L; l++)
+            for (int d = 0; d < W; d++)
+              if (d != sh[l].gid) exchanged += recs[(size_t)sh[l].gid * kRecWords + kRecRoute + d];
+        } else {
         if (queued) {  // this level's counters came back with the queue
           const unsigned char* set = hq + (size_t)q_pos * kCtrSet;
           std::memcpy(&sh[0].lc, set, sizeof(LevelCounters));
           std::memcpy(segc[0].data(), set + kCtrSegOff, 8 * kSegs * kSegStride);
         } else {
-        for (int l = 0; l < L; l++) {
-          Shard& S = sh[l];
-          DSL_HIP(hipMemcpyAsync(S.hctr, S.ctrbuf + S.cset * kCtrSet, kCtrSegOff + 8 * S.nseg * kSegStride,
-                                 hipMemcpyDeviceToHost, stream));
-          if (route) {  // the level's route counts come with the same synchronization
-            if (dev_gather) {  // every rank's counts, gathered on the device: the count matrix
-              DSL_TRY(comm->allgather_dev(reinterpret_cast<const uint64_t*>(S.rc), W, xdev, stream));
-              DSL_HIP(hipMemcpyAsync(xhost, xdev, (size_t)W * W * 8, hipMemcpyDeviceToHost, stream));
-            }
-            DSL_HIP(hipMemcpyAsync(S.hctr + kCtrSet, S.rc, sizeof(RouteCounters), hipMemcpyDeviceToHost, stream));
-            DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
+          for (int l = 0; l < L; l++) {
+            Shard& S = sh[l];
+            DSL_HIP(hipMemcpyAsync(S.hctr, S.ctrbuf + S.cset * kCtrSet, kCtrSegOff + 8 * S.nseg * kSegStride,
+                                   hipMemcpyDeviceToHost, stream));
+          }
+          DSL_TRY(hsync());
+          for (int l = 0; l < L; l++) {
+            Shard& S = sh[l];
+            std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
+            std::memcpy(segc[l].data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
           }
         }
-        DSL_TRY(hsync());
-        for (int l = 0; l < L; l++) {
-          Shard& S = sh[l];
-          std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
-          std::memcpy(segc[l].data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
-          if (route) {
-            RouteCounters rcs;
-            std::memcpy(&rcs, S.hctr + kCtrSet, sizeof(rcs));
-            rcnt[l].assign(rcs.out, rcs.out + W);
-          }
-        }
-        }
-        // next frontier: the filled part of each segment, then the spill range (then received)
-        std::vector<std::vector<uint64_t>> nbase(L), ncnt(L);
-        std::vector<uint64_t> span(L);
+        // next frontier: the filled part of each segment, then the spill range
         bool unspilled = false;
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
@@ -1204,155 +1723,12 @@ struct BfsEngine : EngineBase {
           const int blocks = (int)std::min<uint64_t>((ns + kBlock - 1) / kBlock, 256ull * 32);
           LevelCounters* uctr = queued ? reinterpret_cast<LevelCounters*>(qctr + (size_t)q_pos * kCtrSet) : S.ctr;
           hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, ns, S.cur, S.cur_fp, S.next,
-                             S.next_fp, S.hpar[lv], S.hev[lv], keep, S.gid, uctr, prm, dset);
+                             S.next_fp, S.hpar[lv], S.hev[lv], keep, S.gid, uctr, prm, dset, nullptr);
           nbase[l].push_back(keep);
           ncnt[l].push_back(ns);
           span[l] = need;
         }
-
-        std::vector<uint64_t> mat_keep(L, 0), mat_total(L, 0);
-        const auto tx0 = std::chrono::steady_clock::now();
-        if (route) {
-          stats.sharded_levels++;
-          Mat matrix(W, std::vector<uint64_t>(W, 0));  // [source][owner] records
-          if (comm) {
-            std::vector<uint64_t> flat((size_t)W * W);
-            if (dev_gather) {
-              std::memcpy(flat.data(), xhost, flat.size() * 8);
-            } else {
-              stats.host_syncs++;
-              DSL_TRY(comm->allgather_u64(rcnt[0].data(), W, flat.data(), stream));
-            }
-            for (int x = 0; x < W; x++)
-              for (int d = 0; d < W; d++) matrix[x][d] = flat[(size_t)x * W + d];
-          } else {
-            for (int l = 0; l < L; l++) matrix[sh[l].gid] = rcnt[l];
-          }
-          for (int l = 0; l < L; l++)
-            for (int d = 0; d < W; d++) exchanged += rcnt[l][d];
-          // round A: fingerprints to their owners
-          Mat so(L, std::vector<uint64_t>(W)), sb = so, ro = so, rb = so, src_off(L, std::vector<uint64_t>(W + 1, 0));
-          std::vector<const uint8_t*> snd(L);
-          std::vector<uint8_t*> rcv(L);
-          for (int l = 0; l < L; l++) {
-            Shard& S = sh[l];
-            const int g = S.gid;
-            for (int x = 0; x < W; x++) src_off[l][x + 1] = src_off[l][x] + matrix[x][g];
-            const uint64_t nin = src_off[l][W];
-            DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>(nin, 1), false, 0));
-            DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(nin, 1), false, 0));
-            for (int d = 0; d < W; d++) {
-              so[l][d] = (uint64_t)d * S.cap_fp * sizeof(FpRec);
-              sb[l][d] = rcnt[l][d] * sizeof(FpRec);
-              ro[l][d] = src_off[l][d] * sizeof(FpRec);
-              rb[l][d] = matrix[d][g] * sizeof(FpRec);
-            }
-            snd[l] = reinterpret_cast<const uint8_t*>(S.out_fp);
-            rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
-          }
-          DSL_TRY(xfer(snd, so, sb, rcv, ro, rb));
-          for (int l = 0; l < L; l++) {
-            Shard& S = sh[l];
-            const uint64_t nin = src_off[l][W];
-            if (!nin) continue;
-            ProbeArgs pa;
-            pa.in = S.in_fp;
-            pa.n = nin;
-            pa.table = tbl;
-            pa.table.slots = S.table;
-            pa.reply = S.rep_out;
-            pa.ctr = S.ctr;
-            const int blocks = (int)std::min<uint64_t>((nin + kBlock - 1) / kBlock, 256ull * 32);
-            hipLaunchKernelGGL(k_probe_remote, dim3(blocks), dim3(kBlock), 0, stream, pa);
-          }
-          // round B: one answer byte per record back to its source, in the order the source sent
-          for (int l = 0; l < L; l++) {
-            Shard& S = sh[l];
-            const int g = S.gid;
-            DSL_TRY(grow(&S.rep_in, &S.rep_in_cap, std::max<uint64_t>(S.cap_fp * W, 1), false, 0));
-            for (int x = 0; x < W; x++) {
-              so[l][x] = src_off[l][x];
-              sb[l][x] = matrix[x][g];
-              ro[l][x] = (uint64_t)x * S.cap_fp;
-              rb[l][x] = rcnt[l][x];
-            }
-            snd[l] = S.rep_out;
-            rcv[l] = S.rep_in;
-          }
-          DSL_TRY(xfer(snd, so, sb, rcv, ro, rb));
-          // the new ones are materialized, judged and appended where they were generated
-          for (int l = 0; l < L; l++) {
-            Shard& S = sh[l];
-            uint64_t total = 0;
-            for (int d = 0; d < W; d++) total += rcnt[l][d];
-            if (!total) continue;
-            const uint64_t keep = span[l], need = keep + total;
-            DSL_TRY(grow_rows(&S.next, &S.next_cap, need, true, keep));
-            DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, keep));
-            const size_t lv = S.level_size.size();
-            DSL_TRY(hist_grow(S, lv, need, keep));
-            MaterializeArgs<P> ma{};
-            ma.sent = S.out_fp;
-            ma.reply = S.rep_in;
-            ma.cap = S.cap_fp;
-            for (int d = 0; d < kMaxShards; d++) ma.off[d + 1] = ma.off[d] + (d < W ? rcnt[l][d] : 0);
-            ma.cur = S.cur;
-            ma.cur_fp = S.cur_fp;
-            ma.me = S.gid;
-            ma.depth = depth + 1;
-            ma.incremental = depth > init_depth ? 1 : 0;
-            ma.next = S.next;
-            ma.next_fp = S.next_fp;
-            ma.next_parent = S.hpar[lv];
-            ma.next_event = S.hev[lv];
-            ma.next_base = keep;
-            ma.next_cap = total;
-            ma.ctr = S.ctr;
-            ma.terms = S.terms;
-            ma.term_cap = term_cap;
-            const int blocks = (int)std::min<uint64_t>((total + kBlock - 1) / kBlock, 256ull * 32);
-            hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
-            mat_keep[l] = keep;
-            mat_total[l] = total;
-            span[l] = need;
-          }
-        }
-        // A sharded level of several ranks closes with ONE exchange: every rank's level record
-        // (k_level_record: counts, errors, its best terminal key, its next frontier and work, its
-        // time-up flag) gathered by every rank, on the device with RCCL, in the same round trip as
-        // the final counters.
-        std::vector<uint64_t> recs;
-        if (route && comm) {
-          Shard& S = sh[0];
-          uint64_t base_rows = 0;
-          for (uint64_t c : ncnt[0]) base_rows += c;
-          uint64_t time_up = 0;
-          if (hset.max_time_ms > 0 &&
-              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count() >
-                  hset.max_time_ms)
-            time_up = 1;
-          uint64_t* drec = xdev + kMaxShards * kMaxShards;
-          uint64_t* hrec = xhost + kMaxShards * kMaxShards;
-          hipLaunchKernelGGL(k_level_record, dim3(1), dim3(64), 0, stream, S.ctr, base_rows, mat_total[0], S.F, time_up,
-                             S.gid, drec);
-          DSL_HIP(hipGetLastError());
-          if (dev_gather) {
-            DSL_TRY(comm->allgather_dev(drec, kRecWords, drec + kRecWords, stream));
-            DSL_HIP(hipMemcpyAsync(hrec, drec, (size_t)(W + 1) * kRecWords * 8, hipMemcpyDeviceToHost, stream));
-          } else {
-            DSL_HIP(hipMemcpyAsync(hrec, drec, kRecWords * 8, hipMemcpyDeviceToHost, stream));
-          }
-          DSL_HIP(hipMemcpyAsync(S.hctr, S.ctr, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
-          DSL_TRY(hsync());
-          std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
-          recs.resize((size_t)W * kRecWords);
-          if (dev_gather) {
-            std::memcpy(recs.data(), hrec + kRecWords, recs.size() * 8);
-          } else {
-            stats.host_syncs++;
-            DSL_TRY(comm->allgather_u64(hrec, kRecWords, recs.data(), stream));
-          }
-        } else if (route || unspilled) {  // counters changed after the first read
+        if (unspilled) {  // counters changed after the first read (next_work)
           for (auto& S : sh) {
             const void* src = queued ? (const void*)(qctr + (size_t)q_pos * kCtrSet) : (const void*)S.ctr;
             DSL_HIP(hipMemcpyAsync(S.hctr, src, sizeof(LevelCounters), hipMemcpyDeviceToHost, stream));
@@ -1360,14 +1736,9 @@ struct BfsEngine : EngineBase {
           DSL_TRY(hsync());
           for (auto& S : sh) std::memcpy(&S.lc, S.hctr, sizeof(LevelCounters));
         }
-        if (route)  // both rounds, the owners' probes and the materialization, up to the counters
+        }  // !route
+        if (route)  // the exchange rounds, the owners' probes and the materialization, up to the counters
           stats.exchange_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tx0).count();
-        for (int l = 0; l < L; l++) {  // the rows k_materialize appended
-          const uint64_t c = std::min<uint64_t>(sh[l].lc.next_size, mat_total[l]);
-          if (!c) continue;
-          nbase[l].push_back(mat_keep[l]);
-          ncnt[l].push_back(c);
-        }
         float kms = 0;
         if (!queued || q_pos == 0) {  // a queue is timed as a whole (its dispatches counted there)
           if (queued) kms = (float)q_ms_total;
@@ -1454,9 +1825,11 @@ struct BfsEngine : EngineBase {
             g_next[2] += r[kRecNextWork];
           }
           have_g = true;
-          Shard& S = sh[0];
-          if (enc != ~0ull && (int)(enc & 0xff) == S.gid)  // this rank holds the level's best terminal
-            DSL_TRY(resolve_terminal(S, ~(uint64_t)S.lc.term_best, depth + 1, depth > init_depth, &local_best[0]));
+          for (int l = 0; l < L; l++) {
+            Shard& S = sh[l];
+            if (enc != ~0ull && (int)(enc & 0xff) == S.gid)  // this shard holds the level's best terminal
+              DSL_TRY(resolve_terminal(S, ~(uint64_t)S.lc.term_best, depth + 1, depth > init_depth, &local_best[l]));
+          }
         } else if (!rep) {
           DSL_TRY(global_sum(gsum));
           if (comm) {

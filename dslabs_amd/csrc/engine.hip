@@ -23,9 +23,45 @@ struct RcclComm : Comm {
   int r = 0, n = 1;
   uint64_t* dbuf = nullptr;  // 2 * (kMaxShards * 64) u64
   static constexpr int kScratch = 2 * kMaxShards * 64;
+  const double timeout_ms = getenv("DSL_COMM_TIMEOUT_MS") ? atof(getenv("DSL_COMM_TIMEOUT_MS")) : 300000.0;
   ~RcclComm() override {
     if (c) ncclCommDestroy(c);
     hipFree(dbuf);
+  }
+  int async_error() override {
+    if (!c) return DSL_ERR_COMM;
+    ncclResult_t st = ncclSuccess;
+    if (ncclCommGetAsyncError(c, &st) != ncclSuccess) return DSL_ERR_COMM;
+    if (st != ncclSuccess && st != ncclInProgress) {
+      set_error(std::string("RCCL asynchronous error: ") + ncclGetErrorString(st));
+      return DSL_ERR_COMM;
+    }
+    return DSL_OK;
+  }
+  void abort() override {
+    if (c) (void)ncclCommAbort(c);
+    c = nullptr;
+  }
+  // The small host-read collectives wait for their result polling the communicator's error and a
+  // deadline (a dead peer aborts the communicator instead of blocking this rank forever).
+  int wait(hipStream_t st) {
+    const auto t0 = std::chrono::steady_clock::now();
+    hipError_t e;
+    for (uint64_t it = 0; (e = hipStreamQuery(st)) == hipErrorNotReady; it++) {
+      if ((it & 1023) == 1023) {
+        if (async_error() != DSL_OK ||
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
+          abort();
+          set_error("RCCL collective failed or timed out on rank " + std::to_string(r) + " (communicator aborted)");
+          return DSL_ERR_COMM;
+        }
+      }
+    }
+    if (e != hipSuccess) {
+      set_error(std::string("HIP error ") + hipGetErrorString(e) + " in an RCCL collective");
+      return DSL_ERR_HIP;
+    }
+    return DSL_OK;
   }
   int rank() const override { return r; }
   int size() const override { return n; }
@@ -37,40 +73,42 @@ struct RcclComm : Comm {
     return DSL_OK;
   }
   int allgather_u64(const uint64_t* in, int k, uint64_t* out, hipStream_t st) override {
+    if (!c) return DSL_ERR_COMM;
     if (k * (n + 1) > kScratch) return DSL_ERR_ARG;
     DSL_HIP(hipMemcpyAsync(dbuf, in, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclAllGather(dbuf, dbuf + k, k, ncclUint64, c, st), "allgather");
     if (rc) return rc;
     DSL_HIP(hipMemcpyAsync(out, dbuf + k, (size_t)k * n * 8, hipMemcpyDeviceToHost, st));
-    DSL_HIP(hipStreamSynchronize(st));
-    return DSL_OK;
+    return wait(st);
   }
   int allreduce_u64(uint64_t* v, int k, bool min, hipStream_t st) override {
+    if (!c) return DSL_ERR_COMM;
     if (k > kScratch) return DSL_ERR_ARG;
     DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclAllReduce(dbuf, dbuf, k, ncclUint64, min ? ncclMin : ncclSum, c, st), "allreduce");
     if (rc) return rc;
     DSL_HIP(hipMemcpyAsync(v, dbuf, k * 8, hipMemcpyDeviceToHost, st));
-    DSL_HIP(hipStreamSynchronize(st));
-    return DSL_OK;
+    return wait(st);
   }
   int bcast_u64(uint64_t* v, int k, int root, hipStream_t st) override {
+    if (!c) return DSL_ERR_COMM;
     if (k > kScratch) return DSL_ERR_ARG;
     DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclBroadcast(dbuf, dbuf, k, ncclUint64, root, c, st), "broadcast");
     if (rc) return rc;
     DSL_HIP(hipMemcpyAsync(v, dbuf, k * 8, hipMemcpyDeviceToHost, st));
-    DSL_HIP(hipStreamSynchronize(st));
-    return DSL_OK;
+    return wait(st);
   }
   bool device_collectives() const override { return true; }
   int allgather_dev(const uint64_t* d_in, int k, uint64_t* d_out, hipStream_t st) override {
+    if (!c) return DSL_ERR_COMM;
     return ck(ncclAllGather(d_in, d_out, k, ncclUint64, c, st), "allgather");
   }
   int ver = 0;
   int version() const override { return ver; }
   int alltoallv(const uint8_t* send, const uint64_t* so, const uint64_t* sb, uint8_t* recv, const uint64_t* ro,
                 const uint64_t* rb, hipStream_t st) override {
+    if (!c) return DSL_ERR_COMM;
     int rc = ck(ncclGroupStart(), "group start");
     if (rc) return rc;
     for (int p = 0; p < n; p++) {

@@ -100,6 +100,8 @@ struct LevelCounters {
   unsigned long long probes;        // visited-table probes (successors that are not no-ops)
   unsigned long long cum_before;    // queued levels: new states of the queue's earlier levels
   unsigned long long time_up;       // the search's deadline passed during this level (it is partial)
+  unsigned long long route_spilled; // routed successors past their destination region (rspill list)
+  unsigned long long unspilled;     // rows k_unspill appended (multi-shard fast path: device count)
   unsigned long long phase[12];     // DSL_PHASES builds only: shader cycles per k_level phase
   unsigned long long phcls[32];     // DSL_PHASES: handler cycles per class [0, 16), wave-passes [16, 32)
 };
@@ -425,9 +427,12 @@ struct LevelArgs {
   uint64_t spill_cap;
   int32_t W, me;             // shards (ROUTE only)
   int32_t owner_filter;      // expand only parents this shard owns (first hash-sharded level)
-  FpRec* out_fp;             // W regions of cap_fp records (ROUTE only)
+  FpRec* out_fp;             // W regions of cap_fp records, record 0 of each the header (ROUTE only)
   uint64_t cap_fp;
   RouteCounters* rc;
+  uint64_t* rspill;          // routed successors past their region: (parent << 20 | event)
+  uint64_t rspill_cap;
+  int32_t judge_routed;      // the maxDepth level: routed successors are judged at the source
   // Queued levels (single shard, BfsEngine::enqueue_queue): the frontier's table is derived from
   // the previous queued level's counters instead of `segs`, by the rule the host applies.
   const LevelCounters* qprev;        // null: the table is `segs`
@@ -930,14 +935,27 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           if (rc == STEP_OK && !noop) {
             PH_MARK(2);  // fingerprint
             if (ROUTE) dest = owner_of(f, a.W);
+            bool judge = false;
             if (ROUTE && dest != a.me) {
               route = true;
+              // the maxDepth level (no successor is expanded): judged here, at the source, so the
+              // owner only answers nothing -- no round B, no k_materialize (a routed successor that
+              // is not new was judged when it was first inserted, and checkState is a function of
+              // the state: its verdict cannot be terminal, Search.java:468-504)
+              judge = a.judge_routed != 0;
             } else {
               c_probe++;
               const int ins = find ? INS_NEW : table_insert(a.table, f);
               PH_MARK(3);  // visited-table probe / insert
               if (ins == INS_NEW) {
                 c_new++;
+                judge = true;
+              } else if (ins == INS_FULL) {
+                atomicAdd(&a.ctr->err_table, 1ull);
+              }
+            }
+            if (judge) {
+              {
                 int pi = -1;
                 NodeView view{w, P::kNodeWords, dnode, my_nw};
                 if constexpr (NetPreds<P>::value) {  // the new records through LDS (no register addresses)
@@ -951,15 +969,17 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
                 }
                 const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
                 if (v == V_VALID) {
-                  if (Net<P>::size(w) + dn <= P::kNetCap) is_valid = !find;
-                  else atomicAdd(&a.ctr->err_overflow, 1ull);
+                  if (route) {
+                  } else if (Net<P>::size(w) + dn <= P::kNetCap) {
+                    is_valid = !find;
+                  } else {
+                    atomicAdd(&a.ctr->err_overflow, 1ull);
+                  }
                 } else if (v >= V_TERM_EXCEPTION) {
                   tv = v;
                   tpi = pi;
                   tkey = term_key(v, f.hi);
                 }
-              } else if (ins == INS_FULL) {
-                atomicAdd(&a.ctr->err_table, 1ull);
               }
             }
           } else if (rc == STEP_EXCEPTION) {
@@ -1011,8 +1031,20 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           }
         }
         if (ROUTE) {
+          // region `dest` of out_fp: record 0 is the header (k_route_headers), then the records; a
+          // record past the region's capacity goes to the route-spill list (parent, event), which
+          // the host re-routes after the level (BfsEngine::complete_sharded; rare)
           const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out, route, dest, a.W);
-          if (route) a.out_fp[(uint64_t)dest * a.cap_fp + ridx] = FpRec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
+          if (route) {
+            const FpRec rec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
+            if (ridx + 1 < a.cap_fp) {
+              a.out_fp[(uint64_t)dest * a.cap_fp + 1 + ridx] = rec;
+            } else {
+              const unsigned long long x = atomicAdd(&a.ctr->route_spilled, 1ull);
+              if (x < a.rspill_cap) a.rspill[x] = rec.item;
+              else atomicAdd(&a.ctr->err_frontier, 1ull);
+            }
+          }
         }
       }
       PH_MARK(10);  // the pass loop's exit
@@ -1043,15 +1075,17 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 }
 
 // Materializes spilled VALID states (already inserted, counted and judged) at next_size.
+// n_dev (multi-shard fast path, the host has not read the counters): n = min(*n_dev, n).
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_unspill(const uint64_t* items, uint64_t n, const uint32_t* cur,
                                                     const Fp* cur_fp, uint32_t* next, Fp* next_fp,
                                                     uint64_t* next_parent, uint32_t* next_event, uint64_t base_idx,
                                                     int32_t me, LevelCounters* ctr, typename P::Params prm,
-                                                    DevSettings set) {
+                                                    DevSettings set, const unsigned long long* n_dev = nullptr) {
   constexpr int NW = Layout<P>::kWords;
   __shared__ unsigned long long s_red[kBlock / 64];
   unsigned long long c_next_work = 0;
+  if (n_dev) n = min<uint64_t>(*n_dev, n);
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -1182,29 +1216,120 @@ __global__ void __launch_bounds__(kBlock) k_copy_segments(const uint64_t* seg, i
   }
 }
 
-// A sharded level's closing record (one per rank, gathered by every rank in ONE collective,
-// BfsEngine::run): what the next level and the level's bookkeeping need from every shard.
+// A sharded level's closing record (one per shard, gathered by every rank in ONE collective,
+// BfsEngine::run): what the next level and the level's bookkeeping need from every shard. It is
+// computed on the device from the shard's counters, so the host reads nothing before it.
 enum : int {
   kRecNew = 0, kRecRows, kRecSucc, kRecErrOverflow, kRecErrTable, kRecErrFrontier, kRecWork, kRecParents,
-  kRecNextWork, kRecTerm, kRecTimeUp, kRecProbes, kRecLevelTimeUp, kRecWords
+  kRecNextWork, kRecTerm, kRecTimeUp, kRecProbes, kRecLevelTimeUp,
+  kRecIncomplete,   // the fast path left work for the host (a region past its slab, spills past their room)
+  kRecCap,          // the records one out_fp region of the shard holds (+1: its header)
+  kRecRoute,        // kMaxShards words: records routed to each shard this level
+  kRecWords = kRecRoute + kMaxShards
 };
-__global__ void k_level_record(const LevelCounters* c, uint64_t base_rows, uint64_t mat_total, uint64_t parents,
-                               uint64_t time_up, int gid, uint64_t* out) {
+struct RecordArgs {
+  const LevelCounters* c;
+  const unsigned long long* seg_ctr;  // nseg counters, kSegStride apart
+  int32_t nseg;
+  uint64_t segcap;
+  uint64_t extra_rows;     // host-known rows beyond the segments (the completion phase), else 0
+  uint64_t uns_cap;        // fast path: unspilled rows = min(spilled, uns_cap)
+  uint64_t mat_cap;        // materialized rows = min(next_size, mat_cap)
+  uint64_t parents, time_up;
+  int32_t gid, W;
+  const RouteCounters* rc;  // null: no routing this level
+  uint64_t slab;            // data records per slab (fast path), 0 = none
+  uint64_t cap_fp;
+  uint64_t* out;
+};
+__global__ void k_level_record(RecordArgs a) {
   if (threadIdx.x) return;
-  const uint64_t mat = c->next_size < mat_total ? c->next_size : mat_total;  // rows k_materialize appended
+  const LevelCounters* c = a.c;
+  uint64_t rows = a.extra_rows;
+  for (int q = 0; q < a.nseg; q++) rows += min<uint64_t>(a.seg_ctr[q * kSegStride], a.segcap);
+  rows += min<uint64_t>(c->spilled, a.uns_cap) + min<uint64_t>(c->next_size, a.mat_cap);
+  uint64_t* out = a.out;
   out[kRecNew] = c->new_states;
-  out[kRecRows] = base_rows + mat;
+  out[kRecRows] = rows;
   out[kRecSucc] = c->successors;
   out[kRecErrOverflow] = c->err_overflow;
   out[kRecErrTable] = c->err_table;
   out[kRecErrFrontier] = c->err_frontier;
   out[kRecWork] = c->work_items;
-  out[kRecParents] = parents;
+  out[kRecParents] = a.parents;
   out[kRecNextWork] = c->next_work;
-  out[kRecTerm] = c->term_best ? ((~(uint64_t)c->term_best) & ~(uint64_t)0xff) | (uint64_t)gid : ~0ull;
-  out[kRecTimeUp] = time_up;
+  out[kRecTerm] = c->term_best ? ((~(uint64_t)c->term_best) & ~(uint64_t)0xff) | (uint64_t)a.gid : ~0ull;
+  out[kRecTimeUp] = a.time_up;
   out[kRecProbes] = c->probes;
   out[kRecLevelTimeUp] = c->time_up;  // the level itself stopped at the deadline (partial)
+  uint64_t inc = (c->spilled > a.uns_cap ? 1 : 0) | (c->route_spilled ? 2 : 0);
+  for (int d = 0; d < kMaxShards; d++) {
+    const uint64_t r = a.rc && d < a.W ? a.rc->out[d] : 0;
+    out[kRecRoute + d] = r;
+    if (d != a.gid && r > a.slab) inc |= 4;
+  }
+  out[kRecIncomplete] = inc;
+  out[kRecCap] = a.cap_fp;
+}
+
+// The header of every destination region of a shard's out_fp (record 0): the records routed there
+// (at most the region's capacity); the owner reads it from the slab it receives (k_probe_slab).
+__global__ void k_route_headers(const RouteCounters* rc, FpRec* out_fp, uint64_t cap_fp, int W) {
+  const int d = threadIdx.x;
+  if (d < W) out_fp[(uint64_t)d * cap_fp] = FpRec{min<uint64_t>(rc->out[d], cap_fp - 1), 0ull, 0ull};
+}
+
+// Owner side of the fast path: W received slabs of `slab` + 1 records (header first) at
+// in[s * (slab + 1)]; record j of source s is probed and answered at reply[s * slab + j].
+struct ProbeSlabArgs {
+  const FpRec* in;
+  uint64_t slab;
+  int32_t W, me;
+  Table table;
+  uint8_t* reply;  // null: no answers (the maxDepth level)
+  LevelCounters* ctr;
+};
+__global__ void __launch_bounds__(kBlock) k_probe_slab(ProbeSlabArgs a) {
+  __shared__ unsigned long long s_red[kBlock / 64];
+  __shared__ uint64_t s_n[kMaxShards];
+  if ((int)threadIdx.x < a.W)
+    s_n[threadIdx.x] = (int)threadIdx.x == a.me ? 0ull : min<uint64_t>(a.in[threadIdx.x * (a.slab + 1)].hi, a.slab);
+  __syncthreads();
+  unsigned long long c_new = 0;
+  const uint64_t n = (uint64_t)a.W * a.slab, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t src = i / a.slab, j = i - src * a.slab;
+    if (j >= s_n[src]) continue;
+    const FpRec r = a.in[src * (a.slab + 1) + 1 + j];
+    const int ins = table_insert(a.table, Fp{r.hi, r.lo});
+    if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
+    c_new += ins == INS_NEW;
+    if (a.reply) a.reply[i] = ins == INS_NEW ? 1 : 0;
+  }
+  block_flush(s_red, &a.ctr->new_states, c_new);
+}
+
+// Route-spilled successors (k_level's rspill list) re-fingerprinted and laid out per destination
+// (completion phase): region d of `out` (cap records, no header) gets those owned by d.
+template <class P>
+__global__ void __launch_bounds__(kBlock) k_respill(const uint64_t* items, uint64_t n, const uint32_t* cur,
+                                                    const Fp* cur_fp, int32_t W, FpRec* out, uint64_t cap,
+                                                    RouteCounters* rc, LevelCounters* ctr, typename P::Params prm,
+                                                    DevSettings set) {
+  constexpr int NW = Layout<P>::kWords;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t parent = items[i] >> 20;
+    const int k = (int)(items[i] & 0xfffff);
+    const uint32_t* w = cur + parent * NW;
+    Delta<P> d;
+    delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
+    const Fp f = delta_fingerprint<P>(w, cur_fp[parent], d);
+    const int dest = owner_of(f, W);
+    const unsigned long long x = atomicAdd(&rc->out[dest], 1ull);
+    if (x < cap) out[(uint64_t)dest * cap + x] = FpRec{f.hi, f.lo, items[i]};
+    else atomicAdd(&ctr->err_frontier, 1ull);
+  }
 }
 
 // A sharded level keeps every new state at the shard that generated it; only the visited set is
@@ -1240,6 +1365,14 @@ struct MaterializeArgs {
   const uint8_t* reply;              // W regions of cap bytes (the owners' answers)
   uint64_t cap;
   uint64_t off[kMaxShards + 1];      // flattened index: records to shard d are [off[d], off[d+1])
+  // the fast path (the host has not read the route counts): the records to shard d are the first
+  // min(rc->out[d], slab) of region d (off[] is then derived on the device); otherwise `off` is
+  // the host's. Record i of region d is sent[d * cap + hdr + skip + i], its answer
+  // reply[d * cap + skip + i] (hdr = 1: the region starts with its header record)
+  const RouteCounters* dev_cnt;
+  uint64_t slab;
+  int32_t W, hdr;
+  uint64_t skip;
   const uint32_t* cur;
   const Fp* cur_fp;
   int32_t me, depth, incremental;
@@ -1259,8 +1392,19 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[kBlock / 64];
+  __shared__ uint64_t s_off[kMaxShards + 1];
+  if (threadIdx.x == 0) {
+    if (a.dev_cnt) {
+      s_off[0] = 0;
+      for (int d = 0; d < kMaxShards; d++)
+        s_off[d + 1] = s_off[d] + (d < a.W && d != a.me ? min<uint64_t>(a.dev_cnt->out[d], a.slab) : 0ull);
+    } else {
+      for (int d = 0; d <= kMaxShards; d++) s_off[d] = a.off[d];
+    }
+  }
+  __syncthreads();
   unsigned long long c_next_work = 0;
-  const uint64_t n = a.off[kMaxShards];
+  const uint64_t n = s_off[kMaxShards];
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -1274,10 +1418,10 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
     Fp f{0, 0};
     if (i < n) {
       int dst = 0;
-      while (dst + 1 < kMaxShards && a.off[dst + 1] <= i) dst++;
-      const uint64_t slot = (uint64_t)dst * a.cap + (i - a.off[dst]);
+      while (dst + 1 < kMaxShards && s_off[dst + 1] <= i) dst++;
+      const uint64_t slot = (uint64_t)dst * a.cap + a.skip + (i - s_off[dst]);
       if (a.reply[slot]) {
-        const FpRec r = a.sent[slot];
+        const FpRec r = a.sent[slot + a.hdr];
         parent = r.item >> 20;
         k = (int)(r.item & 0xfffff);
         const uint32_t* w = a.cur + parent * NW;

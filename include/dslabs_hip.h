@@ -34,8 +34,10 @@
 extern "C" {
 #endif
 
-#define DSL_ABI_VERSION 3 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version;
-                            3: dsl_engine_config.flags, dsl_host_comm.flags */
+#define DSL_ABI_VERSION 4 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version;
+                            3: dsl_engine_config.flags, dsl_host_comm.flags;
+                            4: dsl_settings.do_checks / check_sample, dsl_result check counts,
+                               dsl_stats exchange_rounds / fast_levels / completions */
 #define DSL_MAX_NODES 32
 #define DSL_MAX_PREDICATES 16
 #define DSL_MAX_POOL 48          /* operands of combinator predicates (dsl_settings.pool) */
@@ -154,7 +156,19 @@ typedef struct {
   uint64_t memory_budget_bytes; /* device memory the visited table may grow to, per shard (0: no cap;
                                    a search that needs more ends with DSL_ERR_TABLE_FULL) */
   dsl_predicate pool[DSL_MAX_POOL]; /* operands of DSL_PRED_AND / _OR / _IMPLIES predicates */
+  /* GlobalSettings.doErrorChecks / doAllChecks (T/search/Search.java:201-220): after every level,
+     up to check_sample of its new VALID states (0: 256) are re-derived on the host from their
+     parent and event (stepEvent, SearchState.java:282-359) and compared with the device's row
+     (determinism); with DSL_CHECKS_ALL a delivered message is also stepped a second time on the
+     successor (idempotence, not necessarily an error). Counts in dsl_result. */
+  int32_t do_checks;        /* DSL_CHECKS_* */
+  int32_t check_sample;
 } dsl_settings;
+
+/* dsl_settings.do_checks */
+#define DSL_CHECKS_NONE 0
+#define DSL_CHECKS_ERRORS 1 /* GlobalSettings.doErrorChecks: determinism */
+#define DSL_CHECKS_ALL 2    /* GlobalSettings.doAllChecks: + idempotence of message handlers */
 
 typedef struct {
   int32_t device;           /* HIP device ordinal, -1 = current */
@@ -201,6 +215,14 @@ typedef struct {
   uint64_t new_states_inserted;
   uint64_t exchanged_states;/* states routed to another shard (multi-GPU) */
   double level_ms_max;
+  /* dsl_settings.do_checks (CheckLogger.notDeterministic / notIdempotent, T/utils/CheckLogger.java:104-121):
+     successors re-checked, and how many of them were not deterministic / not idempotent; the first
+     offending event (its parent's depth and the event, decoded) of each kind */
+  uint64_t checks_run;
+  uint64_t not_deterministic;
+  uint64_t not_idempotent;
+  dsl_event first_not_deterministic;
+  dsl_event first_not_idempotent;
 } dsl_result;
 
 typedef struct dsl_engine dsl_engine;
@@ -307,6 +329,11 @@ typedef struct {
   double cost_c_ns;
   double cost_x_us;
   uint64_t shard_work_min;
+  /* sharded levels: all-to-all rounds run, levels completed in ONE host round trip (the slab fast
+     path), and levels that needed the completion phase (a slab or a region overflowed) */
+  uint64_t exchange_rounds;
+  uint64_t fast_levels;
+  uint64_t completions;
 } dsl_stats;
 
 int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);

@@ -24,11 +24,13 @@ public final class Dsl {
   public static final long SIZE_PREDICATE = 24, OFF_PRED_ID = 0, OFF_PRED_NEGATE = 4, OFF_PRED_ARG0 = 8,
       OFF_PRED_ARG1 = 16;
   // dsl_settings
-  public static final long SIZE_SETTINGS = 3480, OFF_MAX_DEPTH = 0, OFF_MAX_TIME_MS = 4, OFF_NETWORK_ACTIVE = 8,
+  public static final long SIZE_SETTINGS = 3488, OFF_MAX_DEPTH = 0, OFF_MAX_TIME_MS = 4, OFF_NETWORK_ACTIVE = 8,
       OFF_DELIVER_TIMERS = 12, OFF_LINK_ACTIVE = 16, OFF_SENDER_ACTIVE = 1040, OFF_RECEIVER_ACTIVE = 1072,
       OFF_TIMERS_ACTIVE = 1104, OFF_N_INVARIANTS = 1136, OFF_N_GOALS = 1140, OFF_N_PRUNES = 1144,
       OFF_INVARIANTS = 1152, OFF_GOALS = 1536, OFF_PRUNES = 1920, OFF_TABLE_LOG2 = 2304, OFF_N_POOL = 2308,
-      OFF_MAX_FRONTIER = 2312, OFF_MEMORY_BUDGET = 2320, OFF_POOL = 2328;
+      OFF_MAX_FRONTIER = 2312, OFF_MEMORY_BUDGET = 2320, OFF_POOL = 2328, OFF_DO_CHECKS = 3480,
+      OFF_CHECK_SAMPLE = 3484;
+  public static final int CHECKS_NONE = 0, CHECKS_ERRORS = 1, CHECKS_ALL = 2;
   public static final int MAX_NODES = 32, MAX_PREDICATES = 16, MAX_POOL = 48;
   // dsl_engine_config
   public static final long SIZE_ENGINE_CONFIG = 160, OFF_CFG_DEVICE = 0, OFF_CFG_RANK = 4, OFF_CFG_WORLD = 8,
@@ -37,13 +39,14 @@ public final class Dsl {
   public static final long SIZE_EVENT = 96, OFF_EV_IS_TIMER = 0, OFF_EV_FROM = 4, OFF_EV_TO = 8, OFF_EV_TYPE = 12,
       OFF_EV_N_FIELDS = 16, OFF_EV_TIMER_MIN = 20, OFF_EV_TIMER_MAX = 24, OFF_EV_FIELDS = 32;
   // dsl_result
-  public static final long SIZE_RESULT = 104, OFF_RES_END = 0, OFF_RES_TERMINAL_DEPTH = 4, OFF_RES_PRED_INDEX = 8,
+  public static final long SIZE_RESULT = 320, OFF_RES_END = 0, OFF_RES_TERMINAL_DEPTH = 4, OFF_RES_PRED_INDEX = 8,
       OFF_RES_MAX_DEPTH = 12, OFF_RES_STATES = 16, OFF_RES_N_LEVELS = 24, OFF_RES_TRACE_LEN = 28,
       OFF_RES_PER_DEPTH = 32, OFF_RES_TRACE = 40, OFF_RES_TERMINAL_STATE = 48, OFF_RES_STATE_BYTES = 56,
-      OFF_RES_INITIAL_DEPTH = 60, OFF_RES_ELAPSED = 64;
+      OFF_RES_INITIAL_DEPTH = 60, OFF_RES_ELAPSED = 64, OFF_RES_CHECKS_RUN = 104, OFF_RES_NOT_DETERMINISTIC = 112,
+      OFF_RES_NOT_IDEMPOTENT = 120, OFF_RES_FIRST_NOT_DETERMINISTIC = 128, OFF_RES_FIRST_NOT_IDEMPOTENT = 224;
 
   // DSL_ABI_VERSION: the struct layout above; a library of another version is refused
-  public static final int ABI_VERSION = 3;
+  public static final int ABI_VERSION = 4;
   public static final int MAX_EVENT_FIELDS = 8;
 
   // dsl_protocol_id (include/dslabs_hip.h)
@@ -301,7 +304,8 @@ public final class Dsl {
 
   /** dsl_result, copied. */
   public record Result(int endCondition, int terminalDepth, int predicateIndex, int maxDepth, long states,
-                       long[] perDepth, Event[] trace, byte[] terminalState, int initialDepth, double elapsedSecs) {
+                       long[] perDepth, Event[] trace, byte[] terminalState, int initialDepth, double elapsedSecs,
+                       long checksRun, long notDeterministic, long notIdempotent) {
     static Result copyOf(MemorySegment r) {
       int nl = r.get(ValueLayout.JAVA_INT, OFF_RES_N_LEVELS), tl = r.get(ValueLayout.JAVA_INT, OFF_RES_TRACE_LEN);
       long[] pd = new long[nl];
@@ -317,7 +321,8 @@ public final class Dsl {
       return new Result(r.get(ValueLayout.JAVA_INT, OFF_RES_END), r.get(ValueLayout.JAVA_INT, OFF_RES_TERMINAL_DEPTH),
           r.get(ValueLayout.JAVA_INT, OFF_RES_PRED_INDEX), r.get(ValueLayout.JAVA_INT, OFF_RES_MAX_DEPTH),
           r.get(ValueLayout.JAVA_LONG, OFF_RES_STATES), pd, tr, st, r.get(ValueLayout.JAVA_INT, OFF_RES_INITIAL_DEPTH),
-          r.get(ValueLayout.JAVA_DOUBLE, OFF_RES_ELAPSED));
+          r.get(ValueLayout.JAVA_DOUBLE, OFF_RES_ELAPSED), r.get(ValueLayout.JAVA_LONG, OFF_RES_CHECKS_RUN),
+          r.get(ValueLayout.JAVA_LONG, OFF_RES_NOT_DETERMINISTIC), r.get(ValueLayout.JAVA_LONG, OFF_RES_NOT_IDEMPOTENT));
     }
   }
 }

@@ -82,6 +82,8 @@ def main():
         st = eng.kernel_stats()
         res.update(end=r.endCondition().name, per_depth=r.per_depth, states=r.states, exchanged=st["exchanged"],
                    host_syncs=st["host_syncs"], sharded_levels=st["sharded_levels"], first=first,
+                   fast_levels=st["fast_levels"], completions=st["completions"],
+                   exchange_rounds=st["exchange_rounds"],
                    cost_c_ns=st["cost_c_ns"], cost_x_us=st["cost_x_us"], shard_work_min=st["shard_work_min"])
         t = r.invariantViolatingState() or r.goalMatchingState()
         if t is not None:

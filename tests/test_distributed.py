@@ -18,18 +18,19 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_workers(mode, world, timeout=300, replicate_below=0, device_collectives=False):
+def run_workers(mode, world, timeout=300, replicate_below=0, device_collectives=False, env=None):
     port = _free_port()
     outs, procs = [], []
     with tempfile.TemporaryDirectory() as d:
         for r in range(world):
             out = os.path.join(d, f"r{r}.json")
             outs.append(out)
-            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                       MASTER_PORT=str(port), LOCAL_RANK="0", DSL_TEST_REPLICATE_BELOW=str(replicate_below),
-                       DSL_TEST_DEVICE_COLLECTIVES="1" if device_collectives else "0")
+            wenv = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                        MASTER_PORT=str(port), LOCAL_RANK="0", DSL_TEST_REPLICATE_BELOW=str(replicate_below),
+                        DSL_TEST_DEVICE_COLLECTIVES="1" if device_collectives else "0")
+            wenv.update(env or {})
             procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_shard_worker.py"), mode, out],
-                                          env=env))
+                                          env=wenv))
         for p in procs:
             assert p.wait(timeout=timeout) == 0
         return [json.load(open(o)) for o in outs]

@@ -84,10 +84,11 @@ def test_multiprocess_shards_one_gpu(mode, world, rep):
 @pytest.mark.parametrize("world", [2, 3])
 def test_multiprocess_device_collectives_c5(world):
     """The RCCL engine's bookkeeping on gloo: with DSL_HOST_COMM_DEVICE_COLLECTIVES the engine takes
-    its device-collective branches (the route-count matrix and the level records gathered on the
-    device, bfs_engine.hpp dev_gather), each gather emulated by the transport. C5 d12 with every
-    level hash-sharded, then with the default threshold: per-depth counts equal the golden vector,
-    states are routed, and a sharded level costs at most two host round trips."""
+    its device-collective branches (the level records gathered on the device, bfs_engine.hpp
+    gather_records), each gather emulated by the transport. C5 d12 with every level hash-sharded,
+    then with the default threshold: per-depth counts equal the golden vector, states are routed,
+    and (the second search, buffers grown) every sharded level is ONE host round trip on the slab
+    fast path, the maxDepth level without round B."""
     want = MPX["mp_c5_d12"]["per_depth"]
     for rep in (0, -1):
         res = run_workers("mp_c5", world, replicate_below=rep, device_collectives=True)
@@ -97,11 +98,28 @@ def test_multiprocess_device_collectives_c5(world):
             assert r["first"]["sharded_levels"] > 0
         assert sum(r["first"]["exchanged"] for r in res) > 0
         # every rank took the same decisions (the cost model is agreed in one collective)
-        assert len({(r["sharded_levels"], r["shard_work_min"]) for r in res}) == 1
+        assert len({(r["sharded_levels"], r["shard_work_min"], r["fast_levels"]) for r in res}) == 1
         if rep == 0:
             for r in res:
                 assert r["sharded_levels"] == 12
-                assert r["host_syncs"] <= 2 * r["sharded_levels"] + 1, r
+                assert r["fast_levels"] == 12 and r["completions"] == 0, r
+                assert r["host_syncs"] <= r["sharded_levels"] + 1, r
+                assert r["exchange_rounds"] == 2 * r["sharded_levels"] - 1, r  # no round B at maxDepth
+
+
+@pytest.mark.parametrize("world,slab_max", [(2, 0), (3, 24)])
+def test_multiprocess_sharded_completion_c5(world, slab_max):
+    """The completion phase over gloo (device-collective branches): DSL_SLAB=0 sends every record
+    through the host-sized rounds (round 4's two-round-trip exchange), DSL_SLAB_MAX=24 overflows
+    every slab and region (records past the slab, route spills re-fingerprinted by k_respill):
+    per-depth counts still equal the golden vector on every rank."""
+    want = MPX["mp_c5_d12"]["per_depth"]
+    env = {"DSL_SLAB": "0"} if slab_max == 0 else {"DSL_SLAB_MAX": str(slab_max)}
+    res = run_workers("mp_c5", world, replicate_below=0, device_collectives=True, env=env)
+    for r in res:
+        assert r["errors"] == []
+        assert r["per_depth"] == r["first"]["per_depth"] == want
+        assert r["completions"] > 0, r
 
 
 def test_rccl_engine_at_world_1():
@@ -143,9 +161,10 @@ def test_virtual_shards_c5_default_settings(shards):
 
 @pytest.mark.parametrize("shards", [2, 8])
 def test_sharded_level_host_round_trips(shards):
-    """Every level hash-sharded (replicate_below = 0): a sharded level costs two host round trips
-    (the counters after k_level with the route counts; the counters after the exchange), and the
-    exchange rounds of virtual shards are one launch each (k_copy_segments)."""
+    """Every level hash-sharded (replicate_below = 0): on the slab fast path a sharded level is ONE
+    host round trip (the gathered level records with the counters), the exchange rounds of virtual
+    shards are one launch each (k_copy_segments), and the maxDepth level skips round B and
+    k_materialize (its routed successors are judged at the source)."""
     import argmap
     case = MPX["mp_c5_d12"]
     proto = argmap.protocol(case["args"])
@@ -159,4 +178,36 @@ def test_sharded_level_host_round_trips(shards):
         eng.close()
     assert r.per_depth == case["per_depth"]
     assert st["sharded_levels"] == 12
-    assert st["host_syncs"] <= 2 * st["sharded_levels"], st
+    assert st["fast_levels"] == 12 and st["completions"] == 0, st
+    assert st["host_syncs"] <= st["sharded_levels"] + 1, st
+    assert st["exchange_rounds"] == 2 * st["sharded_levels"] - 1, st
+
+
+@pytest.mark.parametrize("shards,env", [(4, {"DSL_SLAB": "0"}), (4, {"DSL_SLAB_MAX": "16"}),
+                                        (8, {"DSL_SLAB_MAX": "40"})])
+def test_sharded_completion_phase(shards, env, monkeypatch):
+    """Slabs too small for the level (DSL_SLAB_MAX) or none at all (DSL_SLAB=0): the records past
+    each slab, the route-spilled successors (k_respill) and the spills past their room go through
+    the completion phase; C5 d12 per-depth counts and a terminal trace stay exact."""
+    import argmap
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    case = MPX["mp_c5_d12"]
+    proto = argmap.protocol(case["args"])
+    eng = Engine(proto, virtual_shards=shards, replicate_below=0)
+    try:
+        r = eng.bfs(proto.initial_state(), argmap.settings(case["args"], proto, table_log2=23))
+        st = eng.kernel_stats()
+    finally:
+        eng.close()
+    assert r.per_depth == case["per_depth"]
+    assert st["completions"] > 0, st
+    e2 = Engine(PingPong(1, 10, check_value=False), virtual_shards=shards, replicate_below=0)
+    try:
+        s = SearchSettings().addInvariant(RESULTS_OK).addGoal(CLIENTS_DONE)
+        s.table_log2_slots = 20
+        r2 = e2.bfs(e2.protocol.initial_state(), s)
+    finally:
+        e2.close()
+    assert r2.endCondition() == EndCondition.INVARIANT_VIOLATED
+    assert r2.invariantViolatingState().trace() == LAB0["lab0_mutant_nocheck"]["pinned"]["trace"]

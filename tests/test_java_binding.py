@@ -34,7 +34,8 @@ FIELDS = {
                      "N_INVARIANTS": "n_invariants", "N_GOALS": "n_goals", "N_PRUNES": "n_prunes",
                      "INVARIANTS": "invariants", "GOALS": "goals", "PRUNES": "prunes",
                      "TABLE_LOG2": "table_log2_slots", "N_POOL": "n_pool", "MAX_FRONTIER": "max_frontier_states",
-                     "MEMORY_BUDGET": "memory_budget_bytes", "POOL": "pool"},
+                     "MEMORY_BUDGET": "memory_budget_bytes", "POOL": "pool", "DO_CHECKS": "do_checks",
+                     "CHECK_SAMPLE": "check_sample"},
     "dsl_engine_config": {"ENGINE_CONFIG": None, "CFG_DEVICE": "device", "CFG_RANK": "rank",
                           "CFG_WORLD": "world_size", "CFG_VSHARDS": "virtual_shards", "CFG_COMM_ID": "comm_id",
                           "CFG_REPLICATE_BELOW": "replicate_below", "CFG_FLAGS": "flags"},
@@ -45,7 +46,10 @@ FIELDS = {
                    "RES_PRED_INDEX": "predicate_index", "RES_MAX_DEPTH": "max_depth", "RES_STATES": "states",
                    "RES_N_LEVELS": "n_levels", "RES_TRACE_LEN": "trace_len", "RES_PER_DEPTH": "per_depth",
                    "RES_TRACE": "trace", "RES_TERMINAL_STATE": "terminal_state", "RES_STATE_BYTES": "state_bytes",
-                   "RES_INITIAL_DEPTH": "initial_depth", "RES_ELAPSED": "elapsed_s"},
+                   "RES_INITIAL_DEPTH": "initial_depth", "RES_ELAPSED": "elapsed_s", "RES_CHECKS_RUN": "checks_run",
+                   "RES_NOT_DETERMINISTIC": "not_deterministic", "RES_NOT_IDEMPOTENT": "not_idempotent",
+                   "RES_FIRST_NOT_DETERMINISTIC": "first_not_deterministic",
+                   "RES_FIRST_NOT_IDEMPOTENT": "first_not_idempotent"},
 }
 
 
@@ -60,7 +64,7 @@ def test_java_struct_offsets_match_the_c_abi():
             else:
                 assert c["OFF_" + jname] == getattr(S, field).offset, (struct, jname)
             checked += 1
-    assert checked == 60
+    assert checked == 67
 
 
 def test_java_end_conditions_and_predicate_ids_match_the_header():
