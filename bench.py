@@ -24,7 +24,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355X"
+METRIC = "unique states explored/sec (whole node) for Paxos BFS at 1/2/4/8 MI355X"  # BASELINE.json (C5)
+
+
+def metric_name(workload: str) -> str:
+    """BASELINE.json's metric names Paxos (C5, the default workload); another workload's line says
+    which search it measured instead of passing for a Paxos number."""
+    if workload in ("multipaxos", "multipaxos_ir"):
+        return METRIC
+    return f"unique states explored/sec (whole node) for {workload} BFS at 1/2/4/8 MI355X"
 CPU_SAMPLE_S = 10.0  # seconds of timed CPU-baseline searches (a bounded sample)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 LLC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
@@ -316,7 +324,8 @@ def main():
     stats = eng.kernel_stats()
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": metric_name(args.workload),
+            "workload": args.workload,
             "value": round(total_states / elapsed, 1),
             "unit": "states/s",
             "n_gpus": world,

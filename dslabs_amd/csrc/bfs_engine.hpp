@@ -1,17 +1,17 @@
 // bfs_engine.hpp -- host side of the level-synchronous BFS (Search.run + BFS, Search.java:233-505).
 //
 // W hash shards (owner = owner_of(fingerprint, W)); each holds its visited-table partition and
-// the frontier of the states it owns. Deployments:
-//   * W = 1: one GPU, one k_level launch per BFS level, 1 host sync per level;
+// a frontier. Deployments:
+//   * W = 1: one GPU, one k_level launch per BFS level (or a device-side queue of them);
 //   * one process (or thread) per GPU, W = world size, one local shard, exchanges through a Comm
-//     (RCCL: grouped ncclSend/ncclRecv = all-to-all over the xGMI links, allreduce, broadcast);
+//     (RCCL: grouped ncclSend/ncclRecv = all-to-all over the xGMI links, allgather, broadcast);
 //   * virtual shards: W shards on ONE device, exchanges are device-to-device copies (tests).
-// Multi-shard level: k_level<ROUTE> (local successors inserted in-kernel, remote ones as 24-byte
-// FpRecs) -> round A: FpRecs to their owners -> k_probe_remote (one answer byte per record) ->
-// round B: the answers back, in the order received -> k_materialize at the source (judge, append
-// to the source's own next frontier). Only the visited set is partitioned: a new state stays
-// where it was generated, so no state crosses the links, and one count exchange serves both
-// rounds (round B's counts are round A's, reversed).
+// A sharded level (sharded_fast): k_level<ROUTE> routes every successor's 16-byte fingerprint to
+// its owner's region -> round A: fixed-size slabs to the owners -> k_probe_slab (all sources
+// interleaved, one answer byte per record) -> round B: the answers back -> k_materialize at the
+// source (judge, append to the source's own next frontier) -> the level records gathered: ONE
+// host round trip. Only the visited set is partitioned: a new state stays where it was generated
+// (no state row crosses the links); the fair race for "new" keeps the frontiers balanced.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -112,13 +112,15 @@ struct BfsEngine : EngineBase {
     TerminalRec* terms = nullptr;
     unsigned char* find_ctr = nullptr;  // scratch counter sets of a find-mode k_level
     RouteCounters* rc = nullptr;
-    FpRec* out_fp = nullptr;
+    Fp* out_key = nullptr;       // routed successors: W regions of cap_fp fingerprints (header first)
     uint64_t out_fp_cap = 0;
-    FpRec* in_fp = nullptr;
+    uint64_t* out_item = nullptr;  // ... and their (parent << 20 | event) items (stay at the source)
+    uint64_t out_item_cap = 0;
+    Fp* in_fp = nullptr;
     uint64_t in_fp_cap = 0;
-    uint8_t* rep_out = nullptr;  // answers to the received FpRecs (owner side)
+    uint8_t* rep_out = nullptr;  // answers to the received fingerprints (owner side)
     uint64_t rep_out_cap = 0;
-    uint8_t* rep_in = nullptr;   // answers to this shard's FpRecs, W regions of cap_fp (source side)
+    uint8_t* rep_in = nullptr;   // answers to this shard's fingerprints, W regions of cap_fp (source side)
     uint64_t rep_in_cap = 0;
     uint64_t* spill = nullptr;
     uint64_t spill_cap = 0;
@@ -138,11 +140,17 @@ struct BfsEngine : EngineBase {
     uint64_t cap_fp = 0;
     uint64_t* rspill = nullptr;  // route-spilled successors (k_level ROUTE past a region)
     uint64_t rspill_cap = 0;
-    FpRec* out2 = nullptr;       // completion phase: re-routed route spills, W regions
+    Fp* out2 = nullptr;          // completion phase: re-routed route spills, W regions
     uint64_t out2_cap = 0;
+    uint64_t* out2_item = nullptr;
+    uint64_t out2_item_cap = 0;
     uint8_t* rep2 = nullptr;     // ... and the owners' answers to them
     uint64_t rep2_cap = 0;
     uint64_t rs_cap = 0;         // records per out2 / rep2 region
+    uint64_t route_cs = 0;       // records per sub-slab of this level's regions
+    uint64_t* newl = nullptr;    // slots of the routed records found new (k_new_list)
+    uint64_t newl_cap = 0;
+    void* nl_ctr = nullptr;      // [0]: newl's count, [2, 2 + kMaxShards): k_respill's counts
     // a sharded level's next-frontier layout (rows): [0, seg_span) the segments, [seg_span,
     // + uns_room) rows k_unspill appends (fast path), [seg_span + uns_room, + mat_room) rows
     // k_materialize appends, [ovf_base, + ovf_cnt) spills past uns_room (completion phase)
@@ -174,11 +182,11 @@ struct BfsEngine : EngineBase {
   uint64_t* xdev = nullptr;
   // the device-side deadline of a time-limited search (LevelArgs::budget_rt): the device clock at
   // the search's start (k_clock) and the budget in its ticks; not used in a replicated level of a
-  // multi-rank search (every rank runs the level on its own clock: the host check, agreed by a
-  // collective, ends those)
+  // multi-shard search (every shard must finish it, so the replicas stay identical: the host check,
+  // agreed by a collective, ends those)
   uint64_t* t0_rt = nullptr;
   uint64_t budget_rt = 0;
-  uint64_t level_budget(bool rep) const { return comm && rep ? 0 : budget_rt; }
+  uint64_t level_budget(bool rep) const { return W > 1 && rep ? 0 : budget_rt; }
   uint64_t* xhost = nullptr;
   uint64_t* segs_dev = nullptr;   // virtual shards: the segment tables of the two exchange rounds
   uint64_t* segs_host = nullptr;
@@ -300,8 +308,8 @@ struct BfsEngine : EngineBase {
   ~BfsEngine() override {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,
-                      s.out_fp,    s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
-                      s.find_ctr,  s.rspill,   s.out2,    s.rep2};
+                      s.out_key,   s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
+                      s.find_ctr,  s.rspill,   s.out2,    s.rep2,   s.out_item, s.out2_item, s.newl, s.nl_ctr};
       for (void* q : ptrs) (void)hipFree(q);
       for (auto* q : s.hpar) (void)hipFree(q);
       for (auto* q : s.hev) (void)hipFree(q);
@@ -715,10 +723,10 @@ struct BfsEngine : EngineBase {
       stats.host_syncs++;
       DSL_TRY(comm->allreduce_u64(&fail, 1, false, stream));
     }
-    if (fail) {
+    if (fail) {  // out of device memory: not "the estimate was far off", so run() does not restart
       for (auto* q : fresh) (void)hipFree(q);
       set_error("visited table growth: device allocation of " + std::to_string(nb * 64) + " bytes failed");
-      return DSL_ERR_TABLE_FULL;
+      return DSL_ERR_HIP;
     }
     std::vector<unsigned long long*> old(sh.size());
     for (size_t l = 0; l < sh.size(); l++) {
@@ -825,41 +833,59 @@ struct BfsEngine : EngineBase {
   }
 
   // ---- sharded levels: the fast path ----------------------------------------------
-  // A sharded level moves its routed fingerprints in fixed-size SLABS: source -> owner, `slab`
-  // records (plus a header record holding the count) per pair, sized before the level from the
-  // global work and the last measured routed fraction (route_frac, x1.3). No count crosses to the
-  // host before the exchange, so the level is ONE host round trip: k_level<ROUTE> ->
-  // k_route_headers -> round A (slabs) -> k_probe_slab (owners) -> round B (one answer byte per
-  // record) -> k_materialize (sources) -> k_unspill -> k_level_record -> gather of the records ->
-  // the one synchronization. The maxDepth level has no round B and no k_materialize (its routed
-  // successors were judged at the source: LevelArgs::judge_routed). Whatever did not fit (a
-  // region past its slab, records past a region, spills past their room) is flagged in the
-  // records, and every rank then runs the completion phase (complete_sharded) with host-known
-  // counts. DSL_SLAB=0 sends everything through the completion phase (the two-round-trip
-  // exchange of round 4).
+  // A sharded level moves its routed fingerprints in fixed-size SLABS: per (source, owner) pair
+  // one region of kRouteSegs sub-slabs of `cs` records plus a header with their counts
+  // (RouteCounters), sized before the level from the busiest rank's work and the last measured
+  // routed fraction (route_frac, x1.3). No count crosses to the host before the exchange, so the
+  // level is ONE host round trip: k_level<ROUTE> -> k_route_headers -> round A (the regions) ->
+  // k_probe_slab (owners: every source interleaved, its own shard's included) -> round B (one
+  // answer byte per record) -> k_new_list + k_materialize (sources) -> k_level_record -> the
+  // records gathered -> the one synchronization. The maxDepth level has no round B and no
+  // materialization (its routed successors were judged at the source: LevelArgs::judge_routed).
+  // A record past its sub-slab is route-spilled (k_level keeps its parent and event); every rank
+  // then runs the completion phase (complete_sharded: k_respill re-fingerprints them, host-sized
+  // rounds). DSL_SLAB=0 routes everything that way (cs = 0: every record spills).
   const bool slab_mode = !(getenv("DSL_SLAB") && atoi(getenv("DSL_SLAB")) == 0);
   double route_frac = 0;  // routed records / work items of the last sharded level (0: none yet)
   uint64_t max_rank_work = 0;  // the next level's work of the busiest rank (0: no sharded level yet)
 
-  int sharded_capacity(Shard& S, uint64_t slab, bool last) {
-    // out_fp: W regions of cap_fp records, record 0 the header; the same cap on every rank
-    // (DSL_SLAB=0: the shard's work, the exact bound)
-    S.cap_fp = slab ? 2 * slab + 2 : std::max<uint64_t>(S.work, 1) + 1;
-    DSL_TRY(grow(&S.out_fp, &S.out_fp_cap, S.cap_fp * W, false, 0));
-    DSL_TRY(grow(&S.rspill, &S.rspill_cap, std::max<uint64_t>(S.work, 1), false, 0));
-    DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>((slab + 1) * W, 1), false, 0));
-    DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(slab * W, 1), false, 0));
-    DSL_TRY(grow(&S.rep_in, &S.rep_in_cap, std::max<uint64_t>(S.cap_fp * W, 1), false, 0));
-    // rows: the segments, room for spills (a quarter of the segments), room for the successors
-    // the owners find new (every record of this shard's slabs, W - 1 of them)
+  // The exchange buffers grow with 1/8 headroom and no further factor: they are the largest
+  // buffers of a sharded search (GBs at C3's deep levels), and the next search's slabs differ by a
+  // few percent.
+  template <class T>
+  int grow_x(T** ptr, uint64_t* cap, uint64_t need) {
+    if (need <= *cap && *ptr) return DSL_OK;
+    const uint64_t want = need + need / 8 + 1024;
+    if (*ptr) {
+      DSL_TRY(hsync());
+      (void)hipFree(*ptr);
+      *ptr = nullptr;
+      *cap = 0;
+    }
+    uint64_t c = 0;
+    return grow(ptr, &c, want, false, 0) == DSL_OK ? (*cap = c, DSL_OK) : DSL_ERR_HIP;
+  }
+  int sharded_capacity(Shard& S, uint64_t cs, bool last) {
+    S.route_cs = cs;
+    S.cap_fp = kRouteHdr + (uint64_t)kRouteSegs * cs;  // the same on every rank
+    DSL_TRY(grow_x(&S.out_key, &S.out_fp_cap, S.cap_fp * W));
+    DSL_TRY(grow_x(&S.out_item, &S.out_item_cap, S.cap_fp * W));
+    DSL_TRY(grow_x(&S.rspill, &S.rspill_cap, std::max<uint64_t>(S.work, 1)));
+    DSL_TRY(grow_x(&S.in_fp, &S.in_fp_cap, S.cap_fp * W));
+    DSL_TRY(grow_x(&S.rep_out, &S.rep_out_cap, S.cap_fp * W));
+    DSL_TRY(grow_x(&S.rep_in, &S.rep_in_cap, S.cap_fp * W));
+    // rows: every routed record of this shard may come back new (its own shard's included)
     S.seg_span = S.segcap * S.nseg;
-    S.uns_room = last || !slab ? 0 : S.seg_span / 4;
-    S.mat_room = last ? 0 : slab * (W - 1);
+    S.uns_room = 0;
+    S.mat_room = last ? 0 : (uint64_t)kRouteSegs * cs * W;
     S.ovf_base = S.ovf_cnt = 0;
+    DSL_TRY(grow(&S.spill, &S.spill_cap, 1, false, 0));
+    DSL_TRY(grow_x(&S.newl, &S.newl_cap, std::max<uint64_t>(S.mat_room, 1)));
     const uint64_t rows = S.seg_span + S.uns_room + S.mat_room;
     DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
     DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
     DSL_TRY(hist_grow(S, S.level_size.size(), rows, 0));
+    if (!S.nl_ctr) DSL_HIP(hipMalloc(&S.nl_ctr, (2 + kMaxShards) * 8));
     return DSL_OK;
   }
 
@@ -868,13 +894,20 @@ struct BfsEngine : EngineBase {
   int xround(const std::vector<const uint8_t*>& snd, const Mat& so, const Mat& sb, const std::vector<uint8_t*>& rcv,
              const Mat& ro, const Mat& rb) {
     stats.exchange_rounds++;
+    if (comm) {  // the transport moves the other ranks' parts; this rank's own is a device copy
+      const int me = sh[0].gid;
+      if (sb[0][me])
+        DSL_HIP(hipMemcpyAsync(rcv[0] + ro[0][me], snd[0] + so[0][me], sb[0][me], hipMemcpyDeviceToDevice, stream));
+      Mat sb2 = sb, rb2 = rb;
+      sb2[0][me] = rb2[0][me] = 0;
+      return xfer(snd, so, sb2, rcv, ro, rb2);
+    }
     return xfer(snd, so, sb, rcv, ro, rb);
   }
 
   // Every local shard's level record (k_level_record) computed on the device, gathered by every
   // rank, read with the shards' counters in ONE host round trip; recs = W records.
-  int gather_records(const std::vector<uint64_t>& extra_rows, uint64_t slab, uint64_t time_up,
-                     std::vector<uint64_t>& recs) {
+  int gather_records(const std::vector<uint64_t>& extra_rows, uint64_t time_up, std::vector<uint64_t>& recs) {
     const int L = (int)sh.size();
     const bool dev_gather = comm && comm->device_collectives();
     for (int l = 0; l < L; l++) {
@@ -892,7 +925,6 @@ struct BfsEngine : EngineBase {
       ra.gid = S.gid;
       ra.W = W;
       ra.rc = S.rc;
-      ra.slab = slab;
       ra.cap_fp = S.cap_fp;
       ra.out = xdev + (size_t)l * kRecWords;
       hipLaunchKernelGGL(k_level_record, dim3(1), dim3(64), 0, stream, ra);
@@ -922,55 +954,58 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
-  int sharded_fast(int depth, bool last, uint64_t slab, uint64_t time_up, std::vector<uint64_t>& recs,
+  int sharded_fast(int depth, bool last, uint64_t cs, uint64_t time_up, std::vector<uint64_t>& recs,
                    std::vector<std::vector<uint64_t>>& nbase, std::vector<std::vector<uint64_t>>& ncnt,
                    std::vector<uint64_t>& span) {
     const int L = (int)sh.size();
     Mat so(L, std::vector<uint64_t>(W, 0)), sb = so, ro = so, rb = so;
     std::vector<const uint8_t*> snd(L);
     std::vector<uint8_t*> rcv(L);
-    const size_t R = sizeof(FpRec);
-    if (slab) {
+    const size_t R = sizeof(Fp);
+    if (cs) {
       for (auto& S : sh) {
-        hipLaunchKernelGGL(k_route_headers, dim3(1), dim3(64), 0, stream, (const RouteCounters*)S.rc, S.out_fp,
-                           S.cap_fp, W);
+        hipLaunchKernelGGL(k_route_headers, dim3(1), dim3(kMaxShards * kRouteSegs), 0, stream,
+                           (const RouteCounters*)S.rc, S.out_key, S.cap_fp, cs, W);
         DSL_HIP(hipGetLastError());
       }
-      // round A: the slabs (header + slab records) of every (source, owner) pair
+      // round A: the regions of every (source, owner) pair
       for (int l = 0; l < L; l++) {
         Shard& S = sh[l];
         for (int d = 0; d < W; d++) {
-          const uint64_t n = d == S.gid ? 0 : (slab + 1) * R;
+          const uint64_t n = d == S.gid ? 0 : S.cap_fp * R;
           so[l][d] = (uint64_t)d * S.cap_fp * R;
           sb[l][d] = n;
-          ro[l][d] = (uint64_t)d * (slab + 1) * R;
+          ro[l][d] = (uint64_t)d * S.cap_fp * R;
           rb[l][d] = n;
         }
-        snd[l] = reinterpret_cast<const uint8_t*>(S.out_fp);
+        snd[l] = reinterpret_cast<const uint8_t*>(S.out_key);
         rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
       }
       DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
       for (auto& S : sh) {
         ProbeSlabArgs pa{};
         pa.in = S.in_fp;
-        pa.slab = slab;
+        pa.self = S.out_key + (size_t)S.gid * S.cap_fp;
+        pa.cap_fp = S.cap_fp;
+        pa.cs = cs;
         pa.W = W;
         pa.me = S.gid;
         pa.table = tbl;
         pa.table.slots = S.table;
         pa.reply = last ? nullptr : S.rep_out;
+        pa.self_reply = S.rep_in + (size_t)S.gid * S.cap_fp;
         pa.ctr = S.ctr;
-        const int blocks = (int)std::min<uint64_t>((slab * W + kBlock - 1) / kBlock, 8192);
-        hipLaunchKernelGGL(k_probe_slab, dim3(std::max(1, blocks)), dim3(kBlock), 0, stream, pa);
+        const int gy = (int)std::max<uint64_t>(1, std::min<uint64_t>((cs + kBlock - 1) / kBlock, 64));
+        hipLaunchKernelGGL(k_probe_slab, dim3(W * kRouteSegs, gy), dim3(kBlock), 0, stream, pa);
         DSL_HIP(hipGetLastError());
       }
       if (!last) {
-        // round B: one answer byte per record, back to its source (the slab's layout, reversed)
+        // round B: one answer byte per record, back to its source (the regions' layout)
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
           for (int d = 0; d < W; d++) {
-            const uint64_t n = d == S.gid ? 0 : slab;
-            so[l][d] = (uint64_t)d * slab;
+            const uint64_t n = d == S.gid ? 0 : S.cap_fp;
+            so[l][d] = (uint64_t)d * S.cap_fp;
             sb[l][d] = n;
             ro[l][d] = (uint64_t)d * S.cap_fp;
             rb[l][d] = n;
@@ -979,20 +1014,11 @@ struct BfsEngine : EngineBase {
           rcv[l] = S.rep_in;
         }
         DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
-        for (auto& S : sh) DSL_TRY(launch_materialize(S, depth, slab, 0, nullptr));
+        for (auto& S : sh) DSL_TRY(launch_materialize(S, depth, true, nullptr, S.out_key, S.out_item, S.rep_in, S.cap_fp));
       }
     }
-    for (auto& S : sh) {
-      if (!S.uns_room) continue;
-      const size_t lv = S.level_size.size();
-      const int blocks = (int)std::min<uint64_t>((S.uns_room + kBlock - 1) / kBlock, 8192);
-      hipLaunchKernelGGL(k_unspill<P>, dim3(blocks), dim3(kBlock), 0, stream, S.spill, S.uns_room, S.cur, S.cur_fp,
-                         S.next, S.next_fp, S.hpar[lv], S.hev[lv], S.seg_span, S.gid, S.ctr, prm, dset,
-                         (const unsigned long long*)&S.ctr->spilled);
-      DSL_HIP(hipGetLastError());
-    }
     std::vector<uint64_t> extra(L, 0);
-    DSL_TRY(gather_records(extra, slab, time_up, recs));
+    DSL_TRY(gather_records(extra, time_up, recs));
     bool incomplete = false, errors = false;
     for (int x = 0; x < W; x++) {
       const uint64_t* r = recs.data() + (size_t)x * kRecWords;
@@ -1000,12 +1026,11 @@ struct BfsEngine : EngineBase {
       errors |= (r[kRecErrOverflow] | r[kRecErrTable] | r[kRecErrFrontier]) != 0;
     }
     if (getenv("DSL_LEVEL_TRACE")) {
-      fprintf(stderr, "[shard] depth %d slab %llu last %d:", depth + 1, (unsigned long long)slab, last ? 1 : 0);
+      fprintf(stderr, "[shard] depth %d cs %llu last %d:", depth + 1, (unsigned long long)cs, last ? 1 : 0);
       for (int x = 0; x < W; x++) {
         const uint64_t* r = recs.data() + (size_t)x * kRecWords;
         uint64_t mx = 0;
-        for (int d = 0; d < W; d++)
-          if (d != x) mx = std::max<uint64_t>(mx, r[kRecRoute + d]);
+        for (int d = 0; d < W; d++) mx = std::max<uint64_t>(mx, r[kRecRoute + d]);
         fprintf(stderr, " [%d: work %llu max_route %llu inc %llu]", x, (unsigned long long)r[kRecWork],
                 (unsigned long long)mx, (unsigned long long)r[kRecIncomplete]);
       }
@@ -1013,29 +1038,15 @@ struct BfsEngine : EngineBase {
     }
     if (incomplete && !errors) {
       stats.completions++;
-      DSL_TRY(complete_sharded(depth, last, slab, time_up, recs));
+      DSL_TRY(complete_sharded(depth, last, time_up, recs));
     } else {
       stats.fast_levels++;
     }
     for (auto& S : sh) DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
-    // the next frontier of every local shard: segments, unspilled rows, materialized rows, and
-    // the completion phase's spills
+    // the next frontier of every local shard: the materialized rows (and the completion phase's
+    // row spills; k_level appends none on a sharded level)
     for (int l = 0; l < L; l++) {
       Shard& S = sh[l];
-      std::vector<unsigned long long> seg(kSegs * kSegStride);
-      std::memcpy(seg.data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
-      for (int q = 0; q < S.nseg; q++) {
-        const uint64_t c = std::min<uint64_t>(seg[(size_t)q * kSegStride], S.segcap);
-        if (c) {
-          nbase[l].push_back((uint64_t)q * S.segcap);
-          ncnt[l].push_back(c);
-        }
-      }
-      const uint64_t un = std::min<uint64_t>(S.lc.spilled, S.uns_room);
-      if (un) {
-        nbase[l].push_back(S.seg_span);
-        ncnt[l].push_back(un);
-      }
       const uint64_t mat = std::min<uint64_t>(S.lc.next_size, S.mat_room);
       if (mat) {
         nbase[l].push_back(S.seg_span + S.uns_room);
@@ -1050,28 +1061,33 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
-  // k_materialize of shard S: the fast path's slabs (dev counts, off == null) or host-known
-  // counts off[] of region `skip` onwards (the completion phase), appended at seg_span + uns_room.
-  int launch_materialize(Shard& S, int depth, uint64_t slab, uint64_t skip, const uint64_t* off,
-                         const FpRec* sent = nullptr, const uint8_t* reply = nullptr, uint64_t cap = 0, int hdr = 1) {
+  // k_new_list + k_materialize of shard S: the new ones among its routed records (the fast path's
+  // sub-slabs with device counts, or host counts cnt[d] of regions of `cap` records), appended at
+  // seg_span + uns_room (next_size counts them across calls).
+  int launch_materialize(Shard& S, int depth, bool dev, const uint64_t* cnt, const Fp* sent_key,
+                         const uint64_t* sent_item, const uint8_t* reply, uint64_t cap) {
     const size_t lv = S.level_size.size();
+    NewListArgs na{};
+    na.reply = reply;
+    na.cap = cap;
+    na.W = W;
+    na.dev_cnt = dev ? S.rc : nullptr;
+    na.cs = S.route_cs;
+    if (cnt)
+      for (int d = 0; d < W; d++) na.cnt[d] = cnt[d];
+    na.list = S.newl;
+    na.n_list = reinterpret_cast<unsigned long long*>(S.nl_ctr);
+    const uint64_t per = dev ? S.route_cs : cap, items = per * (uint64_t)W * (dev ? kRouteSegs : 1);
+    if (!items || !S.mat_room) return DSL_OK;
+    DSL_HIP(hipMemsetAsync(S.nl_ctr, 0, 8, stream));
+    const int gy = (int)std::max<uint64_t>(1, std::min<uint64_t>((per + kBlock - 1) / kBlock, 64));
+    hipLaunchKernelGGL(k_new_list, dim3(dev ? W * kRouteSegs : W, gy), dim3(kBlock), 0, stream, na);
+    DSL_HIP(hipGetLastError());
     MaterializeArgs<P> ma{};
-    ma.sent = sent ? sent : S.out_fp;
-    ma.reply = reply ? reply : S.rep_in;
-    ma.cap = cap ? cap : S.cap_fp;
-    ma.hdr = hdr;
-    ma.skip = skip;
-    ma.W = W;
-    uint64_t total = 0;
-    if (off) {
-      for (int d = 0; d <= kMaxShards; d++) ma.off[d] = off[d];
-      total = off[kMaxShards];
-    } else {
-      ma.dev_cnt = S.rc;
-      ma.slab = slab;
-      total = slab * (W - 1);
-    }
-    if (!total) return DSL_OK;
+    ma.sent_key = sent_key;
+    ma.sent_item = sent_item;
+    ma.list = S.newl;
+    ma.n_list = reinterpret_cast<const unsigned long long*>(S.nl_ctr);
     ma.cur = S.cur;
     ma.cur_fp = S.cur_fp;
     ma.me = S.gid;
@@ -1086,25 +1102,21 @@ struct BfsEngine : EngineBase {
     ma.ctr = S.ctr;
     ma.terms = S.terms;
     ma.term_cap = term_cap;
-    const int blocks = (int)std::min<uint64_t>((total + kBlock - 1) / kBlock, 8192);
-    hipLaunchKernelGGL(k_materialize<P>, dim3(blocks), dim3(kBlock), 0, stream, ma, prm, dset);
+    const int blocks = (int)std::min<uint64_t>((std::min(items, S.mat_room) + kBlock - 1) / kBlock, 8192);
+    hipLaunchKernelGGL(k_materialize<P>, dim3(std::max(1, blocks)), dim3(kBlock), 0, stream, ma, prm, dset);
     DSL_HIP(hipGetLastError());
     return DSL_OK;
   }
 
-  // The completion phase of a sharded level (every rank, when any record is incomplete): with the
-  // gathered route counts, (1) the route-spilled successors are re-fingerprinted per owner
-  // (k_respill; their counts gathered: a host round trip), (2) the records past each slab and (3)
-  // the re-routed ones go through a host-sized exchange round each (probe, answers,
-  // materialization), (4) spills past their room are materialized, then the records are gathered
-  // again. Rare: the slab is 1.3x the expected records per pair.
-  int complete_sharded(int depth, bool last, uint64_t slab, uint64_t time_up, std::vector<uint64_t>& recs) {
+  // The completion phase of a sharded level (every rank, when any record is incomplete): the
+  // route-spilled successors are re-fingerprinted per owner (k_respill; their counts gathered: a
+  // host round trip), go through one host-sized exchange round (probe, answers,
+  // materialization), the row spills are materialized, then the records are gathered again.
+  // Rare: a sub-slab is 1.3x the records expected in it.
+  int complete_sharded(int depth, bool last, uint64_t time_up, std::vector<uint64_t>& recs) {
     const int L = (int)sh.size();
-    const size_t R = sizeof(FpRec);
+    const size_t R = sizeof(Fp);
     const size_t lv = sh[0].level_size.size();
-    auto route = [&](int s, int d) { return recs[(size_t)s * kRecWords + kRecRoute + d]; };
-    auto cap_of = [&](int s) { return recs[(size_t)s * kRecWords + kRecCap]; };
-    // (1) route spills -> out2, per owner; the count matrix gathered
     Mat rs(W, std::vector<uint64_t>(W, 0));
     {
       std::vector<uint64_t> nrs(L);
@@ -1112,17 +1124,21 @@ struct BfsEngine : EngineBase {
         Shard& S = sh[l];
         nrs[l] = std::min<uint64_t>(S.lc.route_spilled, S.rspill_cap);
         S.rs_cap = std::max<uint64_t>(nrs[l], 1);
-        DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
+        unsigned long long* cnt = reinterpret_cast<unsigned long long*>(S.nl_ctr) + 2;
+        DSL_HIP(hipMemsetAsync(cnt, 0, kMaxShards * 8, stream));
         if (!nrs[l]) continue;
         DSL_TRY(grow(&S.out2, &S.out2_cap, nrs[l] * W, false, 0));
+        DSL_TRY(grow(&S.out2_item, &S.out2_item_cap, nrs[l] * W, false, 0));
         const int blocks = (int)std::min<uint64_t>((nrs[l] + kBlock - 1) / kBlock, 8192);
         hipLaunchKernelGGL(k_respill<P>, dim3(blocks), dim3(kBlock), 0, stream, (const uint64_t*)S.rspill, nrs[l],
-                           (const uint32_t*)S.cur, (const Fp*)S.cur_fp, W, S.out2, S.rs_cap, S.rc, S.ctr, prm, dset);
+                           (const uint32_t*)S.cur, (const Fp*)S.cur_fp, W, S.out2, S.out2_item, S.rs_cap, cnt, S.ctr,
+                           prm, dset);
         DSL_HIP(hipGetLastError());
       }
       uint64_t* h = xhost + 2 * (size_t)kMaxShards * kRecWords;
       for (int l = 0; l < L; l++)
-        DSL_HIP(hipMemcpyAsync(h + (size_t)l * kMaxShards, sh[l].rc, kMaxShards * 8, hipMemcpyDeviceToHost, stream));
+        DSL_HIP(hipMemcpyAsync(h + (size_t)l * kMaxShards, reinterpret_cast<unsigned long long*>(sh[l].nl_ctr) + 2,
+                               kMaxShards * 8, hipMemcpyDeviceToHost, stream));
       DSL_TRY(hsync());
       std::vector<uint64_t> mine((size_t)L * W), all((size_t)W * W);
       for (int l = 0; l < L; l++)
@@ -1136,18 +1152,12 @@ struct BfsEngine : EngineBase {
       }
       for (int x = 0; x < W; x++)
         for (int d = 0; d < W; d++) rs[x][d] = all[(size_t)x * W + d];
-      for (int l = 0; l < L; l++) DSL_HIP(hipMemsetAsync(sh[l].rc, 0, sizeof(RouteCounters), stream));
     }
     // rows: the materialized room grows by everything this shard may still get back
     for (int l = 0; l < L; l++) {
       Shard& S = sh[l];
-      const int g = S.gid;
       uint64_t more = 0;
-      for (int d = 0; d < W; d++) {
-        if (d == g) continue;
-        const uint64_t in_region = std::min<uint64_t>(route(g, d), cap_of(g) - 1);
-        more += (in_region > slab ? in_region - slab : 0) + rs[g][d];
-      }
+      for (int d = 0; d < W; d++) more += rs[S.gid][d];
       const uint64_t used = S.seg_span + S.uns_room + S.mat_room;
       const uint64_t ovf = S.lc.spilled > S.uns_room ? std::min<uint64_t>(S.lc.spilled, S.spill_cap) - S.uns_room : 0;
       const uint64_t need = used + more + ovf;
@@ -1156,27 +1166,15 @@ struct BfsEngine : EngineBase {
         DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, need, true, used));
         DSL_TRY(hist_grow(S, lv, need, used));
       }
-      S.mat_room += more;
+      if (!last) S.mat_room += more;
+      DSL_TRY(grow(&S.newl, &S.newl_cap, std::max<uint64_t>(more, 1), false, 0));
       S.ovf_base = S.seg_span + S.uns_room + S.mat_room;
       S.ovf_cnt = ovf;
     }
-    // (2) the records past each slab, (3) the re-routed ones: two host-sized rounds
-    for (int pass = 0; pass < 2; pass++) {
-      Mat cnt(W, std::vector<uint64_t>(W, 0));
-      for (int x = 0; x < W; x++)
-        for (int d = 0; d < W; d++) {
-          if (d == x) continue;
-          if (pass == 0) {
-            const uint64_t in_region = std::min<uint64_t>(route(x, d), cap_of(x) - 1);
-            cnt[x][d] = in_region > slab ? in_region - slab : 0;
-          } else {
-            cnt[x][d] = rs[x][d];
-          }
-        }
-      bool any = false;
-      for (int x = 0; x < W; x++)
-        for (int d = 0; d < W; d++) any |= cnt[x][d] != 0;
-      if (!any) continue;
+    bool any = false;
+    for (int x = 0; x < W; x++)
+      for (int d = 0; d < W; d++) any |= rs[x][d] != 0;
+    if (any) {
       Mat so(L, std::vector<uint64_t>(W, 0)), sb = so, ro = so, rb = so;
       std::vector<const uint8_t*> snd(L);
       std::vector<uint8_t*> rcv(L);
@@ -1186,17 +1184,16 @@ struct BfsEngine : EngineBase {
         const int g = S.gid;
         uint64_t roff = 0;
         for (int d = 0; d < W; d++) {
-          const uint64_t rcap = pass == 0 ? S.cap_fp : S.rs_cap;
-          so[l][d] = pass == 0 ? ((uint64_t)d * S.cap_fp + 1 + slab) * R : (uint64_t)d * rcap * R;
-          sb[l][d] = cnt[g][d] * R;
+          so[l][d] = (uint64_t)d * S.rs_cap * R;
+          sb[l][d] = rs[g][d] * R;
           ro[l][d] = roff * R;
-          rb[l][d] = cnt[d][g] * R;
-          roff += cnt[d][g];
+          rb[l][d] = rs[d][g] * R;
+          roff += rs[d][g];
         }
         nin[l] = roff;
         DSL_TRY(grow(&S.in_fp, &S.in_fp_cap, std::max<uint64_t>(roff, 1), false, 0));
         DSL_TRY(grow(&S.rep_out, &S.rep_out_cap, std::max<uint64_t>(roff, 1), false, 0));
-        snd[l] = reinterpret_cast<const uint8_t*>(pass == 0 ? S.out_fp : S.out2);
+        snd[l] = reinterpret_cast<const uint8_t*>(S.out2);
         rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
       }
       DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
@@ -1214,36 +1211,32 @@ struct BfsEngine : EngineBase {
         hipLaunchKernelGGL(k_probe_remote, dim3(blocks), dim3(kBlock), 0, stream, pa);
         DSL_HIP(hipGetLastError());
       }
-      if (last) continue;  // the maxDepth level: judged at the source, nothing comes back
-      for (int l = 0; l < L; l++) {
-        Shard& S = sh[l];
-        const int g = S.gid;
-        if (pass == 1) DSL_TRY(grow(&S.rep2, &S.rep2_cap, S.rs_cap * W, false, 0));
-        const uint64_t rcap = pass == 0 ? S.cap_fp : S.rs_cap;
-        uint64_t soff = 0;
-        for (int d = 0; d < W; d++) {
-          so[l][d] = soff;
-          sb[l][d] = cnt[d][g];
-          soff += cnt[d][g];
-          ro[l][d] = (uint64_t)d * rcap + (pass == 0 ? slab : 0);
-          rb[l][d] = cnt[g][d];
+      if (!last) {  // the maxDepth level: judged at the source, nothing comes back
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          const int g = S.gid;
+          DSL_TRY(grow(&S.rep2, &S.rep2_cap, S.rs_cap * W, false, 0));
+          uint64_t soff = 0;
+          for (int d = 0; d < W; d++) {
+            so[l][d] = soff;
+            sb[l][d] = rs[d][g];
+            soff += rs[d][g];
+            ro[l][d] = (uint64_t)d * S.rs_cap;
+            rb[l][d] = rs[g][d];
+          }
+          snd[l] = S.rep_out;
+          rcv[l] = S.rep2;
         }
-        snd[l] = S.rep_out;
-        rcv[l] = pass == 0 ? S.rep_in : S.rep2;
-      }
-      DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
-      for (int l = 0; l < L; l++) {
-        Shard& S = sh[l];
-        const int g = S.gid;
-        uint64_t off[kMaxShards + 1] = {0};
-        for (int d = 0; d < kMaxShards; d++) off[d + 1] = off[d] + (d < W ? cnt[g][d] : 0);
-        if (pass == 0)
-          DSL_TRY(launch_materialize(S, depth, slab, slab, off));
-        else
-          DSL_TRY(launch_materialize(S, depth, slab, 0, off, S.out2, S.rep2, S.rs_cap, 0));
+        DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
+        for (int l = 0; l < L; l++) {
+          Shard& S = sh[l];
+          uint64_t cnt[kMaxShards] = {0};
+          for (int d = 0; d < W; d++) cnt[d] = rs[S.gid][d];
+          DSL_TRY(launch_materialize(S, depth, false, cnt, S.out2, S.out2_item, S.rep2, S.rs_cap));
+        }
       }
     }
-    // (4) spills past their room
+    // spills past their room
     std::vector<uint64_t> extra(L, 0);
     for (int l = 0; l < L; l++) {
       Shard& S = sh[l];
@@ -1255,11 +1248,75 @@ struct BfsEngine : EngineBase {
       DSL_HIP(hipGetLastError());
       extra[l] = S.ovf_cnt;
     }
-    // the route counts of the records stay the level's (rc was reused by k_respill)
-    std::vector<uint64_t> keep(recs);
-    DSL_TRY(gather_records(extra, ~0ull, time_up, recs));
-    for (int x = 0; x < W; x++)
-      for (int d = 0; d < kMaxShards; d++) recs[(size_t)x * kRecWords + kRecRoute + d] = keep[(size_t)x * kRecWords + kRecRoute + d];
+    DSL_TRY(gather_records(extra, time_up, recs));
+    return DSL_OK;
+  }
+
+  // ---- GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220) ------------------------
+  // After a level, up to check_sample (0: 256) of its new states, evenly spaced over the shard's
+  // next frontier, are re-derived on the host from their parent row and event (full_step, the
+  // same transition functions compiled for the host) and compared with the device's row:
+  // CheckLogger.notDeterministic (T/utils/CheckLogger.java:104-112). With DSL_CHECKS_ALL a
+  // delivered message is also delivered again to the successor (it stays in the network, a set),
+  // which must give the successor back: CheckLogger.notIdempotent (:114-121, "not necessarily an
+  // error"). The first offending event of each kind is kept (decoded at its parent).
+  uint64_t chk_run = 0, chk_nd = 0, chk_ni = 0;
+  dsl_event chk_first_nd{}, chk_first_ni{};
+  // equal packed states: the header words and the records below the count (a device row's slots
+  // past its count keep whatever the buffer held, kernels.hpp wave_emit)
+  static bool same_state(const uint32_t* a, const uint32_t* b) {
+    using L = Layout<P>;
+    if (Net<P>::size(a) != Net<P>::size(b)) return false;
+    return std::memcmp(a, b, (size_t)(L::kRecBase + Net<P>::size(a) * L::kRecWords) * 4) == 0;
+  }
+  int run_checks(Shard& S, const std::vector<uint64_t>& nbase, const std::vector<uint64_t>& ncnt) {
+    uint64_t total = 0;
+    for (uint64_t c : ncnt) total += c;
+    if (!total) return DSL_OK;
+    const size_t lv = S.level_size.size() - 1;  // this level's history (pushed above)
+    const uint64_t want = hset.check_sample > 0 ? (uint64_t)hset.check_sample : 256;
+    const uint64_t step = std::max<uint64_t>(1, total / want);
+    const bool flip = getenv("DSL_CHECK_FLIP") != nullptr;  // tests: corrupt the first sampled row
+    typename P::State child, parent, again, twice;
+    for (uint64_t i = 0; i < total; i += step) {
+      uint64_t idx = 0, pre = 0;
+      for (size_t r = 0; r < ncnt.size(); r++) {
+        if (i < pre + ncnt[r]) {
+          idx = nbase[r] + (i - pre);
+          break;
+        }
+        pre += ncnt[r];
+      }
+      uint64_t hp = 0;
+      uint32_t k = 0;
+      DSL_HIP(hipMemcpy(child.w, S.next + idx * NW, NW * 4, hipMemcpyDeviceToHost));
+      DSL_HIP(hipMemcpy(&hp, S.hpar[lv] + idx, 8, hipMemcpyDeviceToHost));
+      DSL_HIP(hipMemcpy(&k, S.hev[lv] + idx, 4, hipMemcpyDeviceToHost));
+      const uint64_t pidx = hp & ((1ull << 48) - 1);
+      DSL_HIP(hipMemcpy(parent.w, S.cur + pidx * NW, NW * 4, hipMemcpyDeviceToHost));
+      if (flip && chk_run == 0) child.w[0] ^= 1u;
+      chk_run++;
+      const int rc = full_step<P>(parent.w, (int)k, again.w, prm, dset);
+      if (rc != STEP_OK || !same_state(again.w, child.w)) {
+        if (!chk_nd) describe_event<P>(parent.w, (int)k, prm, dset, &chk_first_nd);
+        chk_nd++;
+        continue;
+      }
+      if (hset.do_checks != DSL_CHECKS_ALL) continue;
+      const int e = locate_event<P>(parent.w, prm, dset, (int)k);
+      if (e < 0) continue;  // timers: not checked (SearchState.stepEvent's e.isMessage())
+      const auto rec = Net<P>::at(parent.w, e);
+      int e2 = -1;
+      for (int j = 0; j < Net<P>::size(child.w); j++)
+        if (Net<P>::at(child.w, j) == rec) e2 = j;
+      Delta<P> d;
+      const int rc2 = e2 < 0 ? STEP_NULL : delta_step_located<P>(child.w, e2, d, prm, dset);
+      const bool same = rc2 == STEP_OK && materialize<P>(child.w, d, twice.w) && same_state(twice.w, child.w);
+      if (!same) {
+        if (!chk_ni) describe_event<P>(parent.w, (int)k, prm, dset, &chk_first_ni);
+        chk_ni++;
+      }
+    }
     return DSL_OK;
   }
 
@@ -1374,7 +1431,10 @@ struct BfsEngine : EngineBase {
     stats.table_slots = buckets * 8 * (uint64_t)W;
     q_left = 0;
     q_pos = 0;
-    const bool use_queue = !getenv("DSL_NO_QUEUE");
+    // do_checks reads every level's rows right after the level: no device-side queue of levels
+    const bool use_queue = !getenv("DSL_NO_QUEUE") && hset.do_checks == DSL_CHECKS_NONE;
+    chk_run = chk_nd = chk_ni = 0;
+    chk_first_nd = chk_first_ni = dsl_event{};
     if (const char* qr = getenv("DSL_QUEUE_ROWS")) q_rows_forced = std::max<uint64_t>(kSegs, strtoull(qr, nullptr, 10) / kSegs * kSegs);
     const bool trace_levels = getenv("DSL_LEVEL_TRACE") != nullptr;
     tbl = Table{nullptr, buckets - 1, 0, 0};
@@ -1488,7 +1548,7 @@ struct BfsEngine : EngineBase {
     } else {
       while (true) {
         const auto lt0 = std::chrono::steady_clock::now();
-        const uint64_t reallocs0 = n_reallocs + stats.table_rehashes;
+        const uint64_t reallocs0 = n_reallocs + stats.table_rehashes, exchanged0 = exchanged;
         // every shard holds the same frontier in a replicated level: the decision is identical
         const bool rep = rep_active && level_replicated(sh[0].F, sh[0].work);
         if (rep_active && !rep) {
@@ -1558,7 +1618,7 @@ struct BfsEngine : EngineBase {
         // the host reading any count), from the global work and the last measured routed fraction;
         // identical on every rank (its inputs are). The maxDepth level expands nothing further.
         const bool last_level = hset.max_depth >= 0 && depth + 1 >= hset.max_depth;
-        uint64_t slab = 0;
+        uint64_t slab = 0;  // records per sub-slab (LevelArgs::route_cs)
         if (route && slab_mode) {
           // the most work one rank has: from the last sharded level's records; after replicated
           // levels every rank expands the parents it owns (hash-balanced, g/W); a search sharded
@@ -1566,7 +1626,7 @@ struct BfsEngine : EngineBase {
           const double per_rank = max_rank_work ? (double)max_rank_work
                                   : rep_threshold() > 0 ? (double)g[2] / W : (double)g[2];
           const double frac = route_frac > 0 ? route_frac : 1.0;
-          slab = (uint64_t)(1.3 * frac * per_rank / (W - 1)) + 64;
+          slab = (uint64_t)(1.3 * frac * per_rank / ((double)W * kRouteSegs)) + 64;
           if (const char* m = getenv("DSL_SLAB_MAX")) slab = std::min<uint64_t>(slab, std::max(1, atoi(m)));  // tests
         }
         const int lslots = level_slots((size_t)pb_max() * kRowLds + 16, route);
@@ -1575,6 +1635,16 @@ struct BfsEngine : EngineBase {
           sh[0].segcap = q_segcap;
         } else {
         for (auto& S : sh) {
+          S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf + S.cset * kCtrSet);
+          S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + S.cset * kCtrSet + kCtrSegOff);
+          // a shard that launches no k_level this level zeroes its next set here
+          if (S.F == 0) DSL_HIP(hipMemsetAsync(S.ctrbuf + (S.cset ^ 1) * kCtrSet, 0, kCtrSet, stream));
+          if (route) {  // every successor is routed: the rows come from k_materialize only
+            S.nseg = 1;
+            S.segcap = 0;
+            DSL_TRY(sharded_capacity(S, slab, last_level));
+            continue;
+          }
           uint64_t nchunks = 0;
           for (size_t q = 0; q < S.seg_cnt.size(); q++) nchunks += (S.seg_cnt[q] + PB - 1) / PB;
           const uint64_t blocks = std::max<uint64_t>(1, std::min<uint64_t>(nchunks, (uint64_t)lslots));
@@ -1587,11 +1657,6 @@ struct BfsEngine : EngineBase {
           DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
           DSL_TRY(hist_grow(S, S.level_size.size(), rows, 0));
           DSL_TRY(grow(&S.spill, &S.spill_cap, std::max<uint64_t>(S.work, 1), false, 0));
-          S.ctr = reinterpret_cast<LevelCounters*>(S.ctrbuf + S.cset * kCtrSet);
-          S.seg_ctr = reinterpret_cast<unsigned long long*>(S.ctrbuf + S.cset * kCtrSet + kCtrSegOff);
-          // a shard that launches no k_level this level zeroes its next set here
-          if (S.F == 0) DSL_HIP(hipMemsetAsync(S.ctrbuf + (S.cset ^ 1) * kCtrSet, 0, kCtrSet, stream));
-          if (route) DSL_TRY(sharded_capacity(S, slab, last_level));
         }
         }  // !queued (capacity)
         const size_t lds = (size_t)PB * kRowLds + 16;
@@ -1630,8 +1695,10 @@ struct BfsEngine : EngineBase {
           a.W = W;
           a.me = S.gid;
           a.owner_filter = route && first_sharded ? 1 : 0;
-          a.out_fp = S.out_fp;
+          a.out_key = S.out_key;
+          a.out_item = S.out_item;
           a.cap_fp = S.cap_fp;
+          a.route_cs = S.route_cs;
           a.rc = S.rc;
           a.rspill = S.rspill;
           a.rspill_cap = S.rspill_cap;
@@ -1673,8 +1740,7 @@ struct BfsEngine : EngineBase {
           for (int x = 0; x < W; x++) {
             const uint64_t* r = recs.data() + (size_t)x * kRecWords;
             lw += r[kRecWork];
-            for (int d = 0; d < W; d++)
-              if (d != x) routed += r[kRecRoute + d];
+            for (int d = 0; d < W; d++) routed += r[kRecRoute + d];  // its own shard's included
           }
           if (lw) route_frac = std::max(0.05, (double)routed / (double)lw);
           max_rank_work = 0;
@@ -1900,8 +1966,9 @@ struct BfsEngine : EngineBase {
           }
         }
         if (trace_levels)
-          fprintf(stderr, "[level] depth %d F=%llu new=%llu queued=%d wall_ms=%.4f reallocs=%llu\n", depth,
-                  (unsigned long long)gsum[7], (unsigned long long)gsum[0], queued ? 1 : 0, lms,
+          fprintf(stderr, "[level] depth %d F=%llu new=%llu queued=%d wall_ms=%.4f kernel_ms=%.4f sharded=%d "
+                  "routed=%llu reallocs=%llu\n", depth, (unsigned long long)gsum[7], (unsigned long long)gsum[0],
+                  queued ? 1 : 0, lms, (double)kms, route ? 1 : 0, (unsigned long long)(exchanged - exchanged0),
                   (unsigned long long)n_reallocs);
         if (enc != ~0ull) {
           const int wrank = (int)(enc & 0xff);
@@ -1946,6 +2013,8 @@ struct BfsEngine : EngineBase {
           trace_events = evs;
           break;
         }
+        if (hset.do_checks != DSL_CHECKS_NONE)
+          for (int l = 0; l < L; l++) DSL_TRY(run_checks(sh[l], nbase[l], ncnt[l]));
         if (gsum[1] == 0) break;
         for (int l = 0; l < L; l++) {
           Shard& S = sh[l];
@@ -2003,6 +2072,11 @@ struct BfsEngine : EngineBase {
     r->new_states_inserted = total_states;
     r->exchanged_states = exchanged;
     r->level_ms_max = level_ms_max;
+    r->checks_run = chk_run;
+    r->not_deterministic = chk_nd;
+    r->not_idempotent = chk_ni;
+    r->first_not_deterministic = chk_first_nd;
+    r->first_not_idempotent = chk_first_ni;
     r->state_bytes = sizeof(init);
     if (term_depth >= 0) {
       // events replayed on the host from the initial state with the same transition code

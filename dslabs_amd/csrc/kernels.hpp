@@ -17,8 +17,8 @@
 //      is a set, every message stays deliverable) leads back to the parent: no fingerprint, no
 //      probe. A VALID successor reserves a row (one returning atomic per wavefront) and the
 //      wavefront writes its rows cooperatively (row + fingerprint + parent pointer + event).
-//   ROUTE (multi-shard): a successor owned by another shard is not probed here; a 24-byte
-//      FpRec goes to its owner's outgoing region instead (bfs_engine.hpp runs the other phases).
+//   ROUTE (multi-shard): a successor is not probed here; its 16-byte fingerprint goes to its owner's
+//      outgoing region instead (bfs_engine.hpp runs the other phases).
 #pragma once
 #include "nodestate.hpp"
 
@@ -163,14 +163,21 @@ struct TerminalRec {
   uint64_t key;     // term_key: priority rank << 62 | fingerprint bits (deterministic tie-break)
 };
 
+// Route counters of a sharded level: per destination shard d, kRouteSegs counters (a workgroup
+// reserves in counter blockIdx % kRouteSegs), each on its own 128-byte line -- one counter per
+// destination was a single hot word that every workgroup's returning atomic hit once per pass.
+// Region d of a shard's routed records: a header of kRouteHdr 16-byte records (the kRouteSegs
+// counts, one u64 each), then kRouteSegs sub-slabs of `cs` records (sub-slab q holds the records
+// of counter q); the whole region is one slab of the exchange.
+constexpr int kRouteSegs = 32;
+constexpr int kRouteStride = 16;
+constexpr int kRouteHdr = kRouteSegs / 2;
 struct RouteCounters {
-  unsigned long long out[kMaxShards];  // records written per destination
+  unsigned long long out[kMaxShards * kRouteSegs * kRouteStride];
 };
+__host__ __device__ inline int rc_idx(int d, int q) { return (d * kRouteSegs + q) * kRouteStride; }
 
-struct FpRec {
-  uint64_t hi, lo;
-  uint64_t item;  // (parent index << 20) | event index, at the source shard
-};
+
 
 __device__ __forceinline__ uint32_t rl32(uint32_t v, int src) { return (uint32_t)__builtin_amdgcn_readlane((int)v, src); }
 __device__ __forceinline__ uint64_t rl64(uint64_t v, int src) {
@@ -225,7 +232,7 @@ struct BlockResv {
 
 template <int BS = kBlock>
 __device__ __forceinline__ unsigned long long block_reserve(BlockResv<BS>& s, unsigned long long* ctrs, bool pred,
-                                                            int dest, int W) {
+                                                            int dest, int W, int stride = 1) {
   const int wid = threadIdx.x >> 6, lane = __lane_id();
   const unsigned long long lt = (1ull << lane) - 1ull;
   unsigned long long mine = 0;
@@ -240,7 +247,7 @@ __device__ __forceinline__ unsigned long long block_reserve(BlockResv<BS>& s, un
     const int d = threadIdx.x;
     unsigned long long tot = 0;
     for (int w = 0; w < BS / 64; w++) tot += (unsigned long long)s.cnt[w][d];
-    unsigned long long base = tot ? atomicAdd(&ctrs[d], tot) : 0ull;
+    unsigned long long base = tot ? atomicAdd(&ctrs[(size_t)d * stride], tot) : 0ull;
     for (int w = 0; w < BS / 64; w++) {
       s.off[w][d] = base;
       base += (unsigned long long)s.cnt[w][d];
@@ -427,8 +434,13 @@ struct LevelArgs {
   uint64_t spill_cap;
   int32_t W, me;             // shards (ROUTE only)
   int32_t owner_filter;      // expand only parents this shard owns (first hash-sharded level)
-  FpRec* out_fp;             // W regions of cap_fp records, record 0 of each the header (ROUTE only)
-  uint64_t cap_fp;
+  // W regions of cap_fp routed successors (ROUTE only): the fingerprints, which go to the owner (16 B
+  // each; record 0 of a region its header), and beside them the (parent << 20 | event) items,
+  // which stay at the source for the materialization
+  Fp* out_key;
+  uint64_t* out_item;
+  uint64_t cap_fp;           // records per region (kRouteHdr + kRouteSegs * route_cs)
+  uint64_t route_cs;         // records per sub-slab
   RouteCounters* rc;
   uint64_t* rspill;          // routed successors past their region: (parent << 20 | event)
   uint64_t rspill_cap;
@@ -484,13 +496,16 @@ __host__ __device__ inline uint64_t est_new_states(uint64_t work, uint64_t prev_
 
 // The queue's stop rule: after a level with any of these, the host must act before the next one.
 // `room`: the visited table's headroom (states) when the queue started; the next level runs only
-// if the queue's inserted states so far plus its estimate fit (the host grows the table first).
+// if the queue's inserted states so far plus TWICE its estimate fit (the host grows the table
+// first): the estimate assumes the new / work ratio does not rise, and a level that rises past the
+// table's room restarts the whole search with a larger table, so the queue, which
+// runs up to twelve levels without the host, keeps a wider margin than the host's own growth rule.
 __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
                                                 uint64_t wlimit, uint64_t room) {
   return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier | c.time_up) && F > 0 &&
          F <= flimit &&
          c.next_work <= wlimit &&
-         c.cum_before + c.new_states + est_new_states(c.next_work, c.new_states, c.work_items) <= room;
+         c.cum_before + c.new_states + 2 * est_new_states(c.next_work, c.new_states, c.work_items) <= room;
 }
 
 // Copies n16 16-byte units from global memory to LDS with LDS-DMA: wave w issues units
@@ -697,6 +712,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   const bool spread = nchunks <= (uint64_t)a.qspread;  // at most one round of resident workgroups
   const int seg = (int)(blockIdx.x % (unsigned)a.nseg);
   int g = 0;
+  int npass = 0;  // this workgroup's passes so far (ROUTE: its sub-slab rotates with them)
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
     if (a.budget_rt) {  // the deadline, before every chunk (one workgroup-uniform decision)
       if (tid == 0) s_tup = __builtin_amdgcn_s_memrealtime() - s_t0 > a.budget_rt ? 1 : 0;
@@ -936,7 +952,11 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             PH_MARK(2);  // fingerprint
             if (ROUTE) dest = owner_of(f, a.W);
             bool judge = false;
-            if (ROUTE && dest != a.me) {
+            if (ROUTE) {
+              // a sharded level routes EVERY successor, its own shard's too: the owner probes them
+              // all in one interleaved pass (k_probe_slab), so which source wins a state generated
+              // by several is a fair race, and the shards' frontiers stay balanced (a local insert
+              // first would let every shard win all of its own, and the busiest shard grow busier)
               route = true;
               // the maxDepth level (no successor is expanded): judged here, at the source, so the
               // owner only answers nothing -- no round B, no k_materialize (a routed successor that
@@ -1031,17 +1051,23 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           }
         }
         if (ROUTE) {
-          // region `dest` of out_fp: record 0 is the header (k_route_headers), then the records; a
-          // record past the region's capacity goes to the route-spill list (parent, event), which
-          // the host re-routes after the level (BfsEngine::complete_sharded; rare)
-          const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out, route, dest, a.W);
+          // region `dest`, sub-slab `sub` (see RouteCounters); a record past its sub-slab goes to
+          // the route-spill list (parent, event), which the host re-routes after the level
+          // (BfsEngine::complete_sharded; rare)
+          // the workgroup's sub-slab rotates with its passes, so one workgroup's records (a small
+          // level has few workgroups) spread over every sub-slab
+          const int sub = (int)((blockIdx.x + (unsigned)npass++) % kRouteSegs);
+          const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out + rc_idx(0, sub), route, dest,
+                                                                     a.W, kRouteSegs * kRouteStride);
           if (route) {
-            const FpRec rec{f.hi, f.lo, ((p0 + j) << 20) | (uint64_t)k};
-            if (ridx + 1 < a.cap_fp) {
-              a.out_fp[(uint64_t)dest * a.cap_fp + 1 + ridx] = rec;
+            const uint64_t item = ((p0 + j) << 20) | (uint64_t)k;
+            if (ridx < a.route_cs) {
+              const uint64_t o = (uint64_t)dest * a.cap_fp + kRouteHdr + (uint64_t)sub * a.route_cs + ridx;
+              a.out_key[o] = f;
+              a.out_item[o] = item;
             } else {
               const unsigned long long x = atomicAdd(&a.ctr->route_spilled, 1ull);
-              if (x < a.rspill_cap) a.rspill[x] = rec.item;
+              if (x < a.rspill_cap) a.rspill[x] = item;
               else atomicAdd(&a.ctr->err_frontier, 1ull);
             }
           }
@@ -1222,7 +1248,7 @@ __global__ void __launch_bounds__(kBlock) k_copy_segments(const uint64_t* seg, i
 enum : int {
   kRecNew = 0, kRecRows, kRecSucc, kRecErrOverflow, kRecErrTable, kRecErrFrontier, kRecWork, kRecParents,
   kRecNextWork, kRecTerm, kRecTimeUp, kRecProbes, kRecLevelTimeUp,
-  kRecIncomplete,   // the fast path left work for the host (a region past its slab, spills past their room)
+  kRecIncomplete,   // the fast path left work for the host (route spills, row spills past their room)
   kRecCap,          // the records one out_fp region of the shard holds (+1: its header)
   kRecRoute,        // kMaxShards words: records routed to each shard this level
   kRecWords = kRecRoute + kMaxShards
@@ -1238,7 +1264,6 @@ struct RecordArgs {
   uint64_t parents, time_up;
   int32_t gid, W;
   const RouteCounters* rc;  // null: no routing this level
-  uint64_t slab;            // data records per slab (fast path), 0 = none
   uint64_t cap_fp;
   uint64_t* out;
 };
@@ -1262,49 +1287,57 @@ __global__ void k_level_record(RecordArgs a) {
   out[kRecTimeUp] = a.time_up;
   out[kRecProbes] = c->probes;
   out[kRecLevelTimeUp] = c->time_up;  // the level itself stopped at the deadline (partial)
-  uint64_t inc = (c->spilled > a.uns_cap ? 1 : 0) | (c->route_spilled ? 2 : 0);
+  const uint64_t inc = (c->spilled > a.uns_cap ? 1 : 0) | (c->route_spilled ? 2 : 0);
   for (int d = 0; d < kMaxShards; d++) {
-    const uint64_t r = a.rc && d < a.W ? a.rc->out[d] : 0;
+    uint64_t r = 0;
+    if (a.rc && d < a.W)
+      for (int q = 0; q < kRouteSegs; q++) r += a.rc->out[rc_idx(d, q)];
     out[kRecRoute + d] = r;
-    if (d != a.gid && r > a.slab) inc |= 4;
   }
   out[kRecIncomplete] = inc;
   out[kRecCap] = a.cap_fp;
 }
 
-// The header of every destination region of a shard's out_fp (record 0): the records routed there
-// (at most the region's capacity); the owner reads it from the slab it receives (k_probe_slab).
-__global__ void k_route_headers(const RouteCounters* rc, FpRec* out_fp, uint64_t cap_fp, int W) {
-  const int d = threadIdx.x;
-  if (d < W) out_fp[(uint64_t)d * cap_fp] = FpRec{min<uint64_t>(rc->out[d], cap_fp - 1), 0ull, 0ull};
+// The header of every destination region (the kRouteSegs counts of its sub-slabs, clipped to the
+// sub-slab capacity); the owner reads it from the region it receives (k_probe_slab).
+__global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t cap_fp, uint64_t cs, int W) {
+  const int t = threadIdx.x, d = t / kRouteSegs, q = t - d * kRouteSegs;
+  if (d < W)
+    reinterpret_cast<uint64_t*>(out_key + (uint64_t)d * cap_fp)[q] = min<uint64_t>(rc->out[rc_idx(d, q)], cs);
 }
 
-// Owner side of the fast path: W received slabs of `slab` + 1 records (header first) at
-// in[s * (slab + 1)]; record j of source s is probed and answered at reply[s * slab + j].
+// Owner side of the fast path: W regions of cap_fp records (layout: RouteCounters), the received
+// ones at in[s * cap_fp], this shard's own in its out_key (`self`). The sources are interleaved
+// (consecutive items take consecutive sources), so duplicates of one state from several sources
+// race fairly for "new". A record is answered at the same index of reply[s * cap_fp + ...], this
+// shard's own at self_reply[...] (its source-side answer array).
 struct ProbeSlabArgs {
-  const FpRec* in;
-  uint64_t slab;
+  const Fp* in;
+  const Fp* self;
+  uint64_t cap_fp, cs;
   int32_t W, me;
   Table table;
-  uint8_t* reply;  // null: no answers (the maxDepth level)
+  uint8_t* reply;       // null: no answers (the maxDepth level)
+  uint8_t* self_reply;
   LevelCounters* ctr;
 };
+// Grid: x = the W * kRouteSegs (source, sub-slab) groups, y = 256-record blocks of a sub-slab
+// (grid-stride). x varies fastest in the dispatch order, so the sources' records are probed
+// interleaved in time; no 64-bit division per record.
 __global__ void __launch_bounds__(kBlock) k_probe_slab(ProbeSlabArgs a) {
   __shared__ unsigned long long s_red[kBlock / 64];
-  __shared__ uint64_t s_n[kMaxShards];
-  if ((int)threadIdx.x < a.W)
-    s_n[threadIdx.x] = (int)threadIdx.x == a.me ? 0ull : min<uint64_t>(a.in[threadIdx.x * (a.slab + 1)].hi, a.slab);
-  __syncthreads();
+  const int g = blockIdx.x, src = g / kRouteSegs, q = g - src * kRouteSegs;
+  const bool self = src == a.me;
+  const Fp* region = self ? a.self : a.in + (uint64_t)src * a.cap_fp;
+  const uint64_t n = min<uint64_t>(reinterpret_cast<const uint64_t*>(region)[q], a.cs);
+  uint8_t* rep = a.reply ? (self ? a.self_reply : a.reply + (uint64_t)src * a.cap_fp) : nullptr;
+  const uint64_t base = kRouteHdr + (uint64_t)q * a.cs;
   unsigned long long c_new = 0;
-  const uint64_t n = (uint64_t)a.W * a.slab, stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint64_t src = i / a.slab, j = i - src * a.slab;
-    if (j >= s_n[src]) continue;
-    const FpRec r = a.in[src * (a.slab + 1) + 1 + j];
-    const int ins = table_insert(a.table, Fp{r.hi, r.lo});
+  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.y * blockDim.x) {
+    const int ins = table_insert(a.table, region[base + j]);
     if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
     c_new += ins == INS_NEW;
-    if (a.reply) a.reply[i] = ins == INS_NEW ? 1 : 0;
+    if (rep) rep[base + j] = ins == INS_NEW ? 1 : 0;
   }
   block_flush(s_red, &a.ctr->new_states, c_new);
 }
@@ -1313,8 +1346,8 @@ __global__ void __launch_bounds__(kBlock) k_probe_slab(ProbeSlabArgs a) {
 // (completion phase): region d of `out` (cap records, no header) gets those owned by d.
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_respill(const uint64_t* items, uint64_t n, const uint32_t* cur,
-                                                    const Fp* cur_fp, int32_t W, FpRec* out, uint64_t cap,
-                                                    RouteCounters* rc, LevelCounters* ctr, typename P::Params prm,
+                                                    const Fp* cur_fp, int32_t W, Fp* out_key, uint64_t* out_item, uint64_t cap,
+                                                    unsigned long long* cnt, LevelCounters* ctr, typename P::Params prm,
                                                     DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1326,19 +1359,22 @@ __global__ void __launch_bounds__(kBlock) k_respill(const uint64_t* items, uint6
     delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
     const Fp f = delta_fingerprint<P>(w, cur_fp[parent], d);
     const int dest = owner_of(f, W);
-    const unsigned long long x = atomicAdd(&rc->out[dest], 1ull);
-    if (x < cap) out[(uint64_t)dest * cap + x] = FpRec{f.hi, f.lo, items[i]};
+    const unsigned long long x = atomicAdd(&cnt[dest], 1ull);
+    if (x < cap) {
+      out_key[(uint64_t)dest * cap + x] = f;
+      out_item[(uint64_t)dest * cap + x] = items[i];
+    }
     else atomicAdd(&ctr->err_frontier, 1ull);
   }
 }
 
 // A sharded level keeps every new state at the shard that generated it; only the visited set is
-// partitioned. Remote successors go to their owner as 24-byte FpRecs (round A), the owner probes
+// partitioned. Routed successors go to their owner as 16-byte fingerprints (round A), the owner probes
 // and answers one byte per record, in the order received (round B: its counts are round A's,
 // reversed, so no second count exchange), and the source materializes, judges and appends the
 // successors its owners found new.
 struct ProbeArgs {
-  const FpRec* in;
+  const Fp* in;
   uint64_t n;
   Table table;
   uint8_t* reply;  // 1 = inserted (new), per received record
@@ -1350,8 +1386,7 @@ __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
   unsigned long long c_new = 0;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const FpRec r = a.in[i];
-    const int ins = table_insert(a.table, Fp{r.hi, r.lo});
+    const int ins = table_insert(a.table, a.in[i]);
     if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
     c_new += ins == INS_NEW;
     a.reply[i] = ins == INS_NEW ? 1 : 0;
@@ -1359,20 +1394,42 @@ __global__ void __launch_bounds__(kBlock) k_probe_remote(ProbeArgs a) {
   block_flush(s_red, &a.ctr->new_states, c_new);
 }
 
+// The routed records the owners found new, as a compact list of their slots (k_new_list), so
+// k_materialize runs one lane per new successor (a lane per routed record left ~4 of 5 lanes
+// idle on C3). Fast path: groups (d, q) = sub-slab q of region d, the first min(rc[d][q], cs)
+// records at d * cap + kRouteHdr + q * cs; completion phase: groups d, cnt[d] records at d * cap.
+struct NewListArgs {
+  const uint8_t* reply;
+  uint64_t cap;
+  int32_t W;
+  const RouteCounters* dev_cnt;  // null: the host's cnt[]
+  uint64_t cs;
+  uint64_t cnt[kMaxShards];
+  uint64_t* list;
+  unsigned long long* n_list;
+};
+// Grid: x = the groups, y = 256-record blocks of a group (grid-stride).
+__global__ void __launch_bounds__(kBlock) k_new_list(NewListArgs a) {
+  const int g = blockIdx.x;
+  const bool dev = a.dev_cnt != nullptr;
+  if (g >= (dev ? a.W * kRouteSegs : a.W)) return;
+  const int d = dev ? g / kRouteSegs : g, q = dev ? g - d * kRouteSegs : 0;
+  const uint64_t n = dev ? min<uint64_t>(a.dev_cnt->out[rc_idx(d, q)], a.cs) : a.cnt[g];
+  const uint64_t base = dev ? (uint64_t)d * a.cap + kRouteHdr + (uint64_t)q * a.cs : (uint64_t)g * a.cap;
+  for (uint64_t j0 = (uint64_t)blockIdx.y * blockDim.x; j0 < n; j0 += (uint64_t)gridDim.y * blockDim.x) {
+    const uint64_t j = j0 + threadIdx.x;
+    const bool take = j < n && a.reply[base + j] != 0;
+    const unsigned long long x = wave_reserve(a.n_list, take);
+    if (take) a.list[x] = base + j;
+  }
+}
+
 template <class P>
 struct MaterializeArgs {
-  const FpRec* sent;                 // W regions of cap records (this shard's round-A send buffer)
-  const uint8_t* reply;              // W regions of cap bytes (the owners' answers)
-  uint64_t cap;
-  uint64_t off[kMaxShards + 1];      // flattened index: records to shard d are [off[d], off[d+1])
-  // the fast path (the host has not read the route counts): the records to shard d are the first
-  // min(rc->out[d], slab) of region d (off[] is then derived on the device); otherwise `off` is
-  // the host's. Record i of region d is sent[d * cap + hdr + skip + i], its answer
-  // reply[d * cap + skip + i] (hdr = 1: the region starts with its header record)
-  const RouteCounters* dev_cnt;
-  uint64_t slab;
-  int32_t W, hdr;
-  uint64_t skip;
+  const Fp* sent_key;                // this shard's routed fingerprints (regions of k_new_list's slots)
+  const uint64_t* sent_item;         // ... and their (parent << 20 | event) items
+  const uint64_t* list;              // the slots of the new ones (k_new_list)
+  const unsigned long long* n_list;
   const uint32_t* cur;
   const Fp* cur_fp;
   int32_t me, depth, incremental;
@@ -1392,19 +1449,8 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[kBlock / 64];
-  __shared__ uint64_t s_off[kMaxShards + 1];
-  if (threadIdx.x == 0) {
-    if (a.dev_cnt) {
-      s_off[0] = 0;
-      for (int d = 0; d < kMaxShards; d++)
-        s_off[d + 1] = s_off[d] + (d < a.W && d != a.me ? min<uint64_t>(a.dev_cnt->out[d], a.slab) : 0ull);
-    } else {
-      for (int d = 0; d <= kMaxShards; d++) s_off[d] = a.off[d];
-    }
-  }
-  __syncthreads();
   unsigned long long c_next_work = 0;
-  const uint64_t n = s_off[kMaxShards];
+  const uint64_t n = *a.n_list;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
@@ -1417,16 +1463,14 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
     d.keep = 0;
     Fp f{0, 0};
     if (i < n) {
-      int dst = 0;
-      while (dst + 1 < kMaxShards && s_off[dst + 1] <= i) dst++;
-      const uint64_t slot = (uint64_t)dst * a.cap + a.skip + (i - s_off[dst]);
-      if (a.reply[slot]) {
-        const FpRec r = a.sent[slot + a.hdr];
-        parent = r.item >> 20;
-        k = (int)(r.item & 0xfffff);
+      const uint64_t slot = a.list[i];
+      {
+        const uint64_t item = a.sent_item[slot];
+        parent = item >> 20;
+        k = (int)(item & 0xfffff);
         const uint32_t* w = a.cur + parent * NW;
         delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
-        f = Fp{r.hi, r.lo};
+        f = a.sent_key[slot];
         int pi = -1;
         uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
 #pragma unroll

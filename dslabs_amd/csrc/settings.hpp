@@ -15,6 +15,8 @@ inline int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)
                             std::string* why_out) {
   DevSettings d{};
   if (num_nodes > DSL_MAX_NODES) return *why_out = "too many nodes", DSL_ERR_ARG;
+  if (in.do_checks < DSL_CHECKS_NONE || in.do_checks > DSL_CHECKS_ALL || in.check_sample < 0)
+    return *why_out = "do_checks must be DSL_CHECKS_NONE / _ERRORS / _ALL and check_sample >= 0", DSL_ERR_ARG;
   for (int f = 0; f < num_nodes; f++) {
     uint32_t row = 0;
     for (int t = 0; t < num_nodes; t++) {

@@ -145,6 +145,19 @@ class SearchSettings:
         self.table_log2_slots = 0
         self.max_frontier_states = 0
         self.memory_budget_bytes = 0
+        # GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220): a sample of every level's
+        # new states re-derived on the host (determinism) and, for doAllChecks, message deliveries
+        # stepped twice (idempotence); counts in SearchResults.checks
+        self.do_checks = _lib.DSL_CHECKS_NONE
+        self.check_sample = 0
+
+    def doErrorChecks(self, on: bool = True) -> "SearchSettings":
+        self.do_checks = _lib.DSL_CHECKS_ERRORS if on else _lib.DSL_CHECKS_NONE
+        return self
+
+    def doAllChecks(self, on: bool = True) -> "SearchSettings":
+        self.do_checks = _lib.DSL_CHECKS_ALL if on else _lib.DSL_CHECKS_NONE
+        return self
 
     # TestSettings -------------------------------------------------------------------------
     def addInvariant(self, p: StatePredicate) -> "SearchSettings":
@@ -259,7 +272,8 @@ class SearchSettings:
         return (state.protocol, self._max_depth, self._max_time_secs, self._network_active, self._deliver_timers,
                 tuple(self._link.items()), tuple(self._sender.items()), tuple(self._receiver.items()),
                 tuple(self._timers_active.items()), tuple(self._invariants), tuple(self._goals), tuple(self._prunes),
-                self.table_log2_slots, self.max_frontier_states, self.memory_budget_bytes)
+                self.table_log2_slots, self.max_frontier_states, self.memory_budget_bytes, self.do_checks,
+                self.check_sample)
 
     def _encode(self, state: "SearchState") -> _lib.dsl_settings:
         """The C ABI form (dsl_settings); the same object again while nothing it reads changed,
@@ -307,6 +321,8 @@ class SearchSettings:
         s.table_log2_slots = self.table_log2_slots
         s.max_frontier_states = self.max_frontier_states
         s.memory_budget_bytes = self.memory_budget_bytes
+        s.do_checks = self.do_checks
+        s.check_sample = self.check_sample
         return s
 
 
@@ -409,6 +425,8 @@ class SearchResults:
         self._predicate = predicate
         self.elapsed_s = elapsed_s
         self.successors = successors
+        self.checks = {"run": 0, "not_deterministic": 0, "not_idempotent": 0, "first_not_deterministic": None,
+                       "first_not_idempotent": None}
 
     def endCondition(self) -> EndCondition:
         return self._end
@@ -603,6 +621,13 @@ class Engine:
             res = SearchResults(end, r.states, per_depth, r.initial_depth, r.max_depth, terminal, pred,
                                 r.elapsed_s, r.successors)
             res._last = last
+            # CheckLogger.notDeterministic / notIdempotent (T/utils/CheckLogger.java:104-121)
+            res.checks = {"run": r.checks_run, "not_deterministic": r.not_deterministic,
+                          "not_idempotent": r.not_idempotent,
+                          "first_not_deterministic": self.protocol.render_event(r.first_not_deterministic)
+                          if r.not_deterministic else None,
+                          "first_not_idempotent": self.protocol.render_event(r.first_not_idempotent)
+                          if r.not_idempotent else None}
             return res
         finally:
             lib.dsl_result_free(res_p)

@@ -162,7 +162,7 @@ final class PBCodec {
       int c = addrs.indexOf(((Address) e.getKey()).rootAddress()) - 1 - servers;
       long seq = ((Number) field(e.getValue(), "sequenceNum")).longValue();
       long r = resultCode((Result) field(e.getValue(), "result"));
-      if (c < 0 || c >= MAX_CLIENTS || r < 0) return -1;
+      if (c < 0 || c >= MAX_CLIENTS || r < 0 || seq < 0 || seq > 3) return -1;
       bits |= (seq | r << 2) << (16 + 12 * c);
     }
     return bits;
@@ -171,9 +171,15 @@ final class PBCodec {
   private long forwardCode(Object m) throws ReflectiveOperationException {
     Object amo = field(m, "command");
     int ca = addrs.indexOf(((Address) field(amo, "clientAddress")).rootAddress());
-    if (ca <= servers) return -1;
-    return ((Number) field(m, "viewNum")).longValue() | (long) ca << 4
-        | ((Number) field(amo, "sequenceNum")).longValue() << 7;
+    long v = ((Number) field(m, "viewNum")).longValue(), seq = ((Number) field(amo, "sequenceNum")).longValue();
+    // the device fields are 4 (view) and 2 (seq) bits (pb.hpp: m & 15, (m >> 7) & 3)
+    if (ca <= servers || v < 0 || v > 15 || seq < 0 || seq > 3) return -1;
+    return v | (long) ca << 4 | seq << 7;
+  }
+
+  /** v when it fits the device field (0..max), else -1: the event then has no encoding (JVM fallback). */
+  private static long bounded(long v, long max) {
+    return v < 0 || v > max ? -1 : v;
   }
 
   /** The dsl_event of a Java event; null when it has none. */
@@ -197,7 +203,7 @@ final class PBCodec {
       switch (simpleName(m)) {
         case "Ping" -> {
           type = M_PING;
-          payload = ((Number) field(m, "viewNum")).longValue();
+          payload = bounded(((Number) field(m, "viewNum")).longValue(), 15);
         }
         case "GetView" -> {
           type = M_GETVIEW;
@@ -209,13 +215,14 @@ final class PBCodec {
         }
         case "Request" -> {
           type = M_REQUEST;
-          payload = ((Number) field(field(m, "command"), "sequenceNum")).longValue();
+          payload = bounded(((Number) field(field(m, "command"), "sequenceNum")).longValue(), 3);
         }
         case "Reply" -> {
           type = M_REPLY;
           Object amo = field(m, "result");
           long r = resultCode((Result) field(amo, "result"));
-          payload = r < 0 ? -1 : ((Number) field(amo, "sequenceNum")).longValue() | r << 2;
+          long seq = bounded(((Number) field(amo, "sequenceNum")).longValue(), 3);
+          payload = r < 0 || seq < 0 ? -1 : seq | r << 2;
         }
         case "StateTransfer" -> {
           type = M_ST;
@@ -224,7 +231,7 @@ final class PBCodec {
         }
         case "StateTransferAck" -> {
           type = M_STACK;
-          payload = ((Number) field(m, "viewNum")).longValue();
+          payload = bounded(((Number) field(m, "viewNum")).longValue(), 15);
         }
         case "Forward", "ForwardAck" -> {
           type = simpleName(m).equals("Forward") ? M_FORWARD : M_FORWARDACK;

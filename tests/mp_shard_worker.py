@@ -55,7 +55,11 @@ def main():
     else:
         from dslabs_amd import CLIENTS_DONE, RESULTS_OK, Engine, SearchSettings
         from dslabs_amd.protocols import MultiPaxos, PingPong, SIPaxos
-        if mode == "mp_c5":  # BASELINE C5 at maxDepth 12 (levels above replicate_below are sharded)
+        if mode.startswith("synth_c3_d"):  # BASELINE C3 (bench.py's workload) to a smaller maxDepth
+            sys.path.insert(0, ROOT)
+            import bench
+            proto, s, _ = bench.build_search("synthetic", int(mode[len("synth_c3_d"):]))
+        elif mode == "mp_c5":  # BASELINE C5 at maxDepth 12 (levels above replicate_below are sharded)
             proto = MultiPaxos(3, 2, "append-xy")
             s = SearchSettings().addInvariant(RESULTS_OK).addInvariant(proto.predicate("LOGS_CONSISTENT_ALL_SLOTS"))
             s.addInvariant(proto.predicate("APPENDS_LINEARIZABLE")).maxDepth(12)
@@ -69,11 +73,11 @@ def main():
             proto = SIPaxos(2, 3, ("a", "b"))
             s = SearchSettings().addInvariant(proto.predicate("Integrity")).addInvariant(proto.predicate("Agreement"))
             s.maxDepth(9)
-        s.table_log2_slots = 23 if mode == "mp_c5" else 22
+        s.table_log2_slots = 23 if mode in ("mp_c5",) or mode.startswith("synth") else 22
         rb = int(os.environ.get("DSL_TEST_REPLICATE_BELOW", "0"))
         eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=rb)
         first = None
-        if mode == "mp_c5":  # warm-up: buffers grow in the first search (each growth is a host sync)
+        if mode == "mp_c5" or mode.startswith("synth"):  # warm-up: buffers grow in the first search
             r0 = eng.bfs(proto.initial_state(), s)
             st0 = eng.kernel_stats()
             first = dict(per_depth=r0.per_depth, exchanged=st0["exchanged"], sharded_levels=st0["sharded_levels"],

@@ -80,3 +80,47 @@ def test_time_limit_ends_queued_search(secs):
                 assert n >= 6, r.per_depth
     finally:
         e.close()
+
+
+def test_do_checks_determinism_and_idempotence():
+    """GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220, CheckLogger.java:104-121):
+    every level's sampled new states re-derived on the host equal the device's rows (C5 d8, no
+    non-determinism); the synthetic protocol's Poke handler (pokes + 1 mod 4) is not idempotent and
+    is reported, Multi-Paxos's handlers are; a corrupted row (DSL_CHECK_FLIP) is reported as not
+    deterministic. Per-depth counts are unchanged by the checks."""
+    import json
+    import os
+    import sys
+    import argmap
+    from dslabs_amd import Engine
+    HERE = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(HERE))
+    import bench
+    case = json.load(open(os.path.join(HERE, "golden", "multipaxos.json")))["mp_c5_d12"]
+    proto = argmap.protocol(case["args"])
+    s = argmap.settings(case["args"], proto, table_log2=22).doAllChecks()
+    s.maxDepth(8)
+    e = Engine(proto)
+    try:
+        r = e.bfs(proto.initial_state(), s)
+    finally:
+        e.close()
+    assert r.per_depth == case["per_depth"][:9]
+    assert r.checks["run"] > 500 and r.checks["not_deterministic"] == 0 and r.checks["not_idempotent"] == 0, r.checks
+    sp, ss, _ = bench.build_search("synthetic", 5)
+    ss.table_log2_slots = 22
+    ss.doAllChecks()
+    e = Engine(sp)
+    try:
+        r = e.bfs(sp.initial_state(), ss)
+        assert r.checks["not_deterministic"] == 0 and r.checks["not_idempotent"] > 0, r.checks
+        assert "Poke" in r.checks["first_not_idempotent"], r.checks
+        ss.doErrorChecks()
+        os.environ["DSL_CHECK_FLIP"] = "1"
+        try:
+            r = e.bfs(sp.initial_state(), ss)
+        finally:
+            del os.environ["DSL_CHECK_FLIP"]
+        assert r.checks["not_deterministic"] >= 1 and r.checks["not_idempotent"] == 0, r.checks
+    finally:
+        e.close()

@@ -211,3 +211,15 @@ def test_sharded_completion_phase(shards, env, monkeypatch):
         e2.close()
     assert r2.endCondition() == EndCondition.INVARIANT_VIOLATED
     assert r2.invariantViolatingState().trace() == LAB0["lab0_mutant_nocheck"]["pinned"]["trace"]
+
+
+def test_multiprocess_c3_gloo_device_collectives():
+    """BASELINE C3 to maxDepth 7 (5.47 M states) over two processes (gloo, device-collective
+    branches), the default cost rule: per-depth counts equal the oracle's synth_c3_d7 on both
+    ranks, both ranks took identical sharding decisions."""
+    deep = json.load(open(os.path.join(GOLD, "deep.json")))
+    res = run_workers("synth_c3_d7", 2, replicate_below=-1, device_collectives=True)
+    for r in res:
+        assert r["errors"] == []
+        assert r["per_depth"] == r["first"]["per_depth"] == deep["synth_c3_d7"]["per_depth"]
+    assert len({(r["sharded_levels"], r["shard_work_min"], r["fast_levels"]) for r in res}) == 1

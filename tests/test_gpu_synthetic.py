@@ -71,3 +71,27 @@ def test_synthetic_c3_bench_config_depth10(monkeypatch):
     assert cpu["per_depth"][:9] == deep["synth_c3_d8"]["per_depth"]
     assert r.per_depth == r0.per_depth == cpu["per_depth"]
     assert r.states == cpu["states"] == 780909037
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_synthetic_c3_sharded_at_scale(shards):
+    """BASELINE C3 (the dedup / all-to-all stress configuration) hash-sharded at 3e7 states:
+    maxDepth 8 on virtual shards, levels past 100,000 frontier states sharded (slab exchange,
+    owner probes, materialization; tools/shard_scale.py runs maxDepth 9). Per-depth counts equal
+    the oracle's synth_c3_d8; the second search completes every sharded level on the fast path."""
+    import sys
+    deep = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "deep.json")))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    proto, s, _ = bench.build_search("synthetic", 8)
+    s.table_log2_slots = 24
+    e = Engine(proto, virtual_shards=shards, replicate_below=100000)
+    try:
+        r0 = e.bfs(proto.initial_state(), s)
+        r = e.bfs(proto.initial_state(), s)
+        st = e.kernel_stats()
+    finally:
+        e.close()
+    assert r0.per_depth == r.per_depth == deep["synth_c3_d8"]["per_depth"]
+    assert st["sharded_levels"] >= 2 and st["exchanged"] > 10 ** 6, st
+    assert st["fast_levels"] == st["sharded_levels"] and st["completions"] == 0, st

@@ -337,3 +337,14 @@ def test_java_dropped_network_uses_the_engine():
     assert "hasDroppedNetwork" not in bfs
     assert "eng.setDropped(eng.dropPending(packed, undrop.from(), undrop.to()))" in bfs
     assert 'getDeclaredField("droppedNetwork")' in bfs and 'getDeclaredField("network")' in bfs
+
+
+def test_java_pb_codec_bounds_every_packed_field():
+    """every PB message encoder refuses (null: JVM fallback) a value wider than its device
+    field -- viewNum 4 bits, sequenceNum 2 bits (pb.hpp: m & 15, (m >> 7) & 3) -- instead of
+    spilling into the client-address bits."""
+    src = open(os.path.join(JAVA, "gpu", "PBCodec.java")).read()
+    assert src.count("bounded(") >= 5  # the helper + Ping, Request, Reply, StateTransferAck
+    assert "v < 0 || v > 15 || seq < 0 || seq > 3" in src  # Forward / ForwardAck
+    assert "n > 15" in src  # ViewReply / StateTransfer views
+    assert "r < 0 || seq < 0 || seq > 3) return -1;" in src  # the lastResults of a StateTransfer's app
