@@ -560,7 +560,7 @@ struct BfsEngine : EngineBase {
     if (hset.max_time_ms > 0 && q_ms_per_level > 0)
       nq = std::max(1, std::min(nq, (int)((hset.max_time_ms - elapsed_ms) / q_ms_per_level)));
     const uint64_t flimit = queue_flimit(span), wlimit = queue_wlimit(span);
-    const uint64_t room = table_room();
+    const uint64_t room = table_room_queue();
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
     DSL_TRY(grow_rows(&S.cur, &S.cur_cap, std::max(span, used), true, used));
@@ -672,6 +672,13 @@ struct BfsEngine : EngineBase {
   // probes still ran out of room (an estimate far off) makes the search restart with a larger
   // first table (run). The table never shrinks: a repeated search starts at the size reached.
   uint64_t table_room() const { return tbl.bucket_mask * 4 + 4 > inserted ? tbl.bucket_mask * 4 + 4 - inserted : 0; }
+  // The queue's room (queue_continues checks twice the estimate against it): up to 3/4 of the
+  // slots, so a level whose new / work ratio doubles against the estimate still probes a table at
+  // most 3/4 full, while a level that keeps to the estimate stays under the half-full rule.
+  uint64_t table_room_queue() const {
+    const uint64_t cap = (tbl.bucket_mask + 1) * 6;
+    return cap > inserted ? cap - inserted : 0;
+  }
   uint64_t table_limit_buckets() const {
     uint64_t lim = 1ull << kKeyBits;  // 2^35 slots, 256 GiB per shard
     if (hset.memory_budget_bytes) lim = std::min<uint64_t>(lim, std::max<uint64_t>(16, hset.memory_budget_bytes / 64));
@@ -874,13 +881,17 @@ struct BfsEngine : EngineBase {
     DSL_TRY(grow_x(&S.in_fp, &S.in_fp_cap, S.cap_fp * W));
     DSL_TRY(grow_x(&S.rep_out, &S.rep_out_cap, S.cap_fp * W));
     DSL_TRY(grow_x(&S.rep_in, &S.rep_in_cap, S.cap_fp * W));
-    // rows: every routed record of this shard may come back new (its own shard's included)
+    // rows: every routed record of this shard may come back new (its own shard's included);
+    // k_materialize appends them to the level's kSegs segments (k_level<ROUTE> appends none)
+    const uint64_t mat_rows = last ? 0 : (uint64_t)kRouteSegs * cs * W;
+    S.nseg = kSegs;
+    S.segcap = mat_rows ? (mat_rows + kSegs - 1) / kSegs + 64 : 0;  // + a wave's share of imbalance
     S.seg_span = S.segcap * S.nseg;
     S.uns_room = 0;
-    S.mat_room = last ? 0 : (uint64_t)kRouteSegs * cs * W;
+    S.mat_room = 0;  // the completion phase's materialized rows, after the segments
     S.ovf_base = S.ovf_cnt = 0;
     DSL_TRY(grow(&S.spill, &S.spill_cap, 1, false, 0));
-    DSL_TRY(grow_x(&S.newl, &S.newl_cap, std::max<uint64_t>(S.mat_room, 1)));
+    DSL_TRY(grow_x(&S.newl, &S.newl_cap, std::max<uint64_t>(mat_rows, 1)));
     const uint64_t rows = S.seg_span + S.uns_room + S.mat_room;
     DSL_TRY(grow_rows(&S.next, &S.next_cap, rows, false, 0));
     DSL_TRY(grow(&S.next_fp, &S.nextfp_cap, rows, false, 0));
@@ -1043,10 +1054,19 @@ struct BfsEngine : EngineBase {
       stats.fast_levels++;
     }
     for (auto& S : sh) DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
-    // the next frontier of every local shard: the materialized rows (and the completion phase's
-    // row spills; k_level appends none on a sharded level)
+    // the next frontier of every local shard: the segments k_materialize filled, the completion
+    // phase's materialized rows and its row spills (k_level appends none on a sharded level)
     for (int l = 0; l < L; l++) {
       Shard& S = sh[l];
+      std::vector<unsigned long long> seg(kSegs * kSegStride);
+      std::memcpy(seg.data(), S.hctr + kCtrSegOff, 8 * S.nseg * kSegStride);
+      for (int q = 0; q < S.nseg; q++) {
+        const uint64_t c = std::min<uint64_t>(seg[(size_t)q * kSegStride], S.segcap);
+        if (c) {
+          nbase[l].push_back((uint64_t)q * S.segcap);
+          ncnt[l].push_back(c);
+        }
+      }
       const uint64_t mat = std::min<uint64_t>(S.lc.next_size, S.mat_room);
       if (mat) {
         nbase[l].push_back(S.seg_span + S.uns_room);
@@ -1078,7 +1098,8 @@ struct BfsEngine : EngineBase {
     na.list = S.newl;
     na.n_list = reinterpret_cast<unsigned long long*>(S.nl_ctr);
     const uint64_t per = dev ? S.route_cs : cap, items = per * (uint64_t)W * (dev ? kRouteSegs : 1);
-    if (!items || !S.mat_room) return DSL_OK;
+    const uint64_t room = dev ? S.seg_span : S.mat_room;
+    if (!items || !room) return DSL_OK;
     DSL_HIP(hipMemsetAsync(S.nl_ctr, 0, 8, stream));
     const int gy = (int)std::max<uint64_t>(1, std::min<uint64_t>((per + kBlock - 1) / kBlock, 64));
     hipLaunchKernelGGL(k_new_list, dim3(dev ? W * kRouteSegs : W, gy), dim3(kBlock), 0, stream, na);
@@ -1099,11 +1120,15 @@ struct BfsEngine : EngineBase {
     ma.next_event = S.hev[lv];
     ma.next_base = S.seg_span + S.uns_room;
     ma.next_cap = S.mat_room;
+    ma.seg_ctr = dev ? S.seg_ctr : nullptr;
+    ma.nseg = S.nseg;
+    ma.segcap = S.segcap;
     ma.ctr = S.ctr;
     ma.terms = S.terms;
     ma.term_cap = term_cap;
-    const int blocks = (int)std::min<uint64_t>((std::min(items, S.mat_room) + kBlock - 1) / kBlock, 8192);
-    hipLaunchKernelGGL(k_materialize<P>, dim3(std::max(1, blocks)), dim3(kBlock), 0, stream, ma, prm, dset);
+    const int blocks = (int)std::min<uint64_t>((std::min(items, room) + kBlock - 1) / kBlock, 8192);
+    const size_t lds = (size_t)(kBlock / 64) * mat_per_max<P>() * NW * 4;
+    hipLaunchKernelGGL(k_materialize<P>, dim3(std::max(1, blocks)), dim3(kBlock), lds, stream, ma, prm, dset);
     DSL_HIP(hipGetLastError());
     return DSL_OK;
   }
@@ -1617,7 +1642,9 @@ struct BfsEngine : EngineBase {
         // a sharded level: the slab (records per source -> owner pair the fast path moves without
         // the host reading any count), from the global work and the last measured routed fraction;
         // identical on every rank (its inputs are). The maxDepth level expands nothing further.
-        const bool last_level = hset.max_depth >= 0 && depth + 1 >= hset.max_depth;
+        // (DSL_LAST_ROUND_B=1, measurement: the maxDepth level like any other, answers back and the
+        // new ones judged at the source by k_materialize, which appends none of them: all PRUNED)
+        const bool last_level = hset.max_depth >= 0 && depth + 1 >= hset.max_depth && !getenv("DSL_LAST_ROUND_B");
         uint64_t slab = 0;  // records per sub-slab (LevelArgs::route_cs)
         if (route && slab_mode) {
           // the most work one rank has: from the last sharded level's records; after replicated
@@ -1640,8 +1667,6 @@ struct BfsEngine : EngineBase {
           // a shard that launches no k_level this level zeroes its next set here
           if (S.F == 0) DSL_HIP(hipMemsetAsync(S.ctrbuf + (S.cset ^ 1) * kCtrSet, 0, kCtrSet, stream));
           if (route) {  // every successor is routed: the rows come from k_materialize only
-            S.nseg = 1;
-            S.segcap = 0;
             DSL_TRY(sharded_capacity(S, slab, last_level));
             continue;
           }

@@ -495,11 +495,12 @@ __host__ __device__ inline uint64_t est_new_states(uint64_t work, uint64_t prev_
 }
 
 // The queue's stop rule: after a level with any of these, the host must act before the next one.
-// `room`: the visited table's headroom (states) when the queue started; the next level runs only
-// if the queue's inserted states so far plus TWICE its estimate fit (the host grows the table
-// first): the estimate assumes the new / work ratio does not rise, and a level that rises past the
-// table's room restarts the whole search with a larger table, so the queue, which
-// runs up to twelve levels without the host, keeps a wider margin than the host's own growth rule.
+// `room`: the visited table's headroom (states, up to 3/4 of its slots: BfsEngine::table_room_queue)
+// when the queue started; the next level runs only if the queue's inserted states so far plus
+// TWICE its estimate fit (the host grows the table first): the estimate assumes the new / work
+// ratio does not rise, and a level that overfills the table restarts the whole search with a
+// larger one, so the queue, which runs up to twelve levels without the host, keeps
+// a doubled level within 3/4 of the slots.
 __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
                                                 uint64_t wlimit, uint64_t room) {
   return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier | c.time_up) && F > 0 &&
@@ -1267,11 +1268,24 @@ struct RecordArgs {
   uint64_t cap_fp;
   uint64_t* out;
 };
-__global__ void k_level_record(RecordArgs a) {
-  if (threadIdx.x) return;
+__global__ void __launch_bounds__(64) k_level_record(RecordArgs a) {
+  // one wave: the segment counters and the route counters summed lane-parallel (a single thread
+  // walking them took ~13 us of dependent loads per launch)
+  const int lane = threadIdx.x;
   const LevelCounters* c = a.c;
-  uint64_t rows = a.extra_rows;
-  for (int q = 0; q < a.nseg; q++) rows += min<uint64_t>(a.seg_ctr[q * kSegStride], a.segcap);
+  uint32_t seg = 0;
+  for (int q = lane; q < a.nseg; q += 64) seg += (uint32_t)min<uint64_t>(a.seg_ctr[q * kSegStride], a.segcap);
+  uint64_t route[kMaxShards];
+#pragma unroll
+  for (int d = 0; d < kMaxShards; d++) {
+    uint64_t r = 0;
+    if (a.rc && d < a.W && lane < kRouteSegs) r = a.rc->out[rc_idx(d, lane)];
+    for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
+    route[d] = r;
+  }
+  for (int o = 32; o > 0; o >>= 1) seg += __shfl_xor(seg, o);
+  if (lane) return;
+  uint64_t rows = a.extra_rows + seg;
   rows += min<uint64_t>(c->spilled, a.uns_cap) + min<uint64_t>(c->next_size, a.mat_cap);
   uint64_t* out = a.out;
   out[kRecNew] = c->new_states;
@@ -1287,15 +1301,10 @@ __global__ void k_level_record(RecordArgs a) {
   out[kRecTimeUp] = a.time_up;
   out[kRecProbes] = c->probes;
   out[kRecLevelTimeUp] = c->time_up;  // the level itself stopped at the deadline (partial)
-  const uint64_t inc = (c->spilled > a.uns_cap ? 1 : 0) | (c->route_spilled ? 2 : 0);
-  for (int d = 0; d < kMaxShards; d++) {
-    uint64_t r = 0;
-    if (a.rc && d < a.W)
-      for (int q = 0; q < kRouteSegs; q++) r += a.rc->out[rc_idx(d, q)];
-    out[kRecRoute + d] = r;
-  }
-  out[kRecIncomplete] = inc;
+  out[kRecIncomplete] = (c->spilled > a.uns_cap ? 1 : 0) | (c->route_spilled ? 2 : 0);
   out[kRecCap] = a.cap_fp;
+#pragma unroll
+  for (int d = 0; d < kMaxShards; d++) out[kRecRoute + d] = route[d];
 }
 
 // The header of every destination region (the kRouteSegs counts of its sub-slabs, clipped to the
@@ -1408,19 +1417,37 @@ struct NewListArgs {
   uint64_t* list;
   unsigned long long* n_list;
 };
-// Grid: x = the groups, y = 256-record blocks of a group (grid-stride).
+// Grid: x = the groups, y = blocks of a group (grid-stride). A workgroup counts the new records of
+// all its items first and reserves their list slots with ONE atomic (a reservation per wave hit
+// the list's counter ~200 K times per shard on C3's level 8), then writes them.
 __global__ void __launch_bounds__(kBlock) k_new_list(NewListArgs a) {
-  const int g = blockIdx.x;
+  __shared__ uint32_t s_cnt[kBlock / 64];
+  __shared__ unsigned long long s_base;
+  const int g = blockIdx.x, lane = __lane_id(), wid = threadIdx.x >> 6;
   const bool dev = a.dev_cnt != nullptr;
   if (g >= (dev ? a.W * kRouteSegs : a.W)) return;
   const int d = dev ? g / kRouteSegs : g, q = dev ? g - d * kRouteSegs : 0;
   const uint64_t n = dev ? min<uint64_t>(a.dev_cnt->out[rc_idx(d, q)], a.cs) : a.cnt[g];
   const uint64_t base = dev ? (uint64_t)d * a.cap + kRouteHdr + (uint64_t)q * a.cs : (uint64_t)g * a.cap;
-  for (uint64_t j0 = (uint64_t)blockIdx.y * blockDim.x; j0 < n; j0 += (uint64_t)gridDim.y * blockDim.x) {
-    const uint64_t j = j0 + threadIdx.x;
+  const uint64_t stride = (uint64_t)gridDim.y * blockDim.x;
+  uint32_t mine = 0;  // this wave's new records (wave-uniform)
+  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j - threadIdx.x < n; j += stride)
+    mine += (uint32_t)__popcll(__ballot(j < n && a.reply[base + j] != 0));
+  if (lane == 0) s_cnt[wid] = mine;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kBlock / 64; w++) t += s_cnt[w];
+    s_base = t ? atomicAdd(a.n_list, (unsigned long long)t) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long x = s_base;
+  for (int w = 0; w < wid; w++) x += s_cnt[w];
+  for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j - threadIdx.x < n; j += stride) {
     const bool take = j < n && a.reply[base + j] != 0;
-    const unsigned long long x = wave_reserve(a.n_list, take);
-    if (take) a.list[x] = base + j;
+    const unsigned long long m = __ballot(take);
+    if (take) a.list[x + __popcll(m & ((1ull << lane) - 1ull))] = base + j;
+    x += __popcll(m);
   }
 }
 
@@ -1433,6 +1460,12 @@ struct MaterializeArgs {
   const uint32_t* cur;
   const Fp* cur_fp;
   int32_t me, depth, incremental;
+  // the rows' reservation: segmented (seg_ctr non-null: workgroup b appends to segment b % nseg,
+  // rows [q * segcap, (q + 1) * segcap), as k_level does -- one counter word took every wave's
+  // returning atomic, ~40 us per launch on C5's sharded levels), else next_size from next_base
+  unsigned long long* seg_ctr;
+  int32_t nseg;
+  uint64_t segcap;
   uint32_t* next;                    // rows [next_base, next_base + next_cap) of the next frontier
   Fp* next_fp;
   uint64_t* next_parent;
@@ -1443,73 +1476,102 @@ struct MaterializeArgs {
   uint32_t term_cap;
 };
 
+// States per wave at most in k_materialize: a wave stages its states' parent rows in LDS (8 KiB
+// per wave), so the handler, the judge and the emitter read LDS, not global memory.
+template <class P>
+constexpr int mat_per_max() {
+  constexpr int r = 8192 / (Layout<P>::kWords * 4);
+  return r < 8 ? 8 : r > 64 ? 64 : r;
+}
+
 template <class P>
 __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, typename P::Params prm, DevSettings set) {
   constexpr int NW = Layout<P>::kWords;
+  constexpr int PMAX = mat_per_max<P>();
   __shared__ uint32_t s_nodew[kBlock * P::kNodeWords];
   __shared__ typename P::Rec s_sends[NetPreds<P>::value ? kBlock * P::kMaxSends : 1];
   __shared__ unsigned long long s_red[kBlock / 64];
+  extern __shared__ __align__(16) uint32_t s_mrows[];  // (kBlock / 64) x PMAX parent rows
   unsigned long long c_next_work = 0;
   const uint64_t n = *a.n_list;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
-    const uint64_t i = base + threadIdx.x;
+  // states per wave: a wave writes its rows one after another (wave_emit), so a short list is
+  // spread over about as many waves as the chip holds at once (at least 8 states each) instead of
+  // 64 per wave on a few workgroups (C5's sharded levels: ~85 us per launch whatever the size); a
+  // long list keeps up to PMAX per wave (C3: the handler's lanes full)
+  const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+  const int per = (int)max<uint64_t>(8, min<uint64_t>(PMAX, (n + 4095) / 4096));
+  const int lane = __lane_id(), wid = threadIdx.x >> 6;
+  uint32_t* wrows = s_mrows + wid * PMAX * NW;
+  for (uint64_t base = ((uint64_t)blockIdx.x * (kBlock / 64) + wid) * per; base < n; base += waves * per) {
+    const uint64_t i = base + lane;
+    const bool act = lane < per && i < n;
     bool ship = false;
     int tv = 0, tpi = -1, k = 0;
-    uint64_t parent = 0, tkey = ~0ull;
+    uint64_t parent = 0, tkey = ~0ull, slot = 0;
+    if (act) {
+      slot = a.list[i];
+      const uint64_t item = a.sent_item[slot];
+      parent = item >> 20;
+      k = (int)(item & 0xfffff);
+    }
+    // the wave's parent rows into LDS, 16 bytes per lane per instruction
+    const int nr = (int)min<uint64_t>((uint64_t)per, n - base);
+    for (int r = 0; r < nr; r++) {
+      const uint4* src = reinterpret_cast<const uint4*>(a.cur + rl64(parent, r) * NW);
+      for (int c = lane; c < NW / 4; c += 64) reinterpret_cast<uint4*>(wrows + r * NW)[c] = src[c];
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t* w = wrows + (act ? lane : 0) * NW;
     Delta<P> d;
     d.node = 0;
     d.out.n = 0;
     d.keep = 0;
     Fp f{0, 0};
-    if (i < n) {
-      const uint64_t slot = a.list[i];
-      {
-        const uint64_t item = a.sent_item[slot];
-        parent = item >> 20;
-        k = (int)(item & 0xfffff);
-        const uint32_t* w = a.cur + parent * NW;
-        delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
-        f = a.sent_key[slot];
-        int pi = -1;
-        uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
+    if (act) {
+      delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
+      f = a.sent_key[slot];
+      int pi = -1;
+      uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
 #pragma unroll
-        for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
-        NodeView view{w, P::kNodeWords, d.node, my_nw};
-        if constexpr (NetPreds<P>::value) {
-          typename P::Rec* ms = s_sends + threadIdx.x * P::kMaxSends;
-          int c = 0;
+      for (int q = 0; q < P::kNodeWords; q++) my_nw[q] = d.nw[q];
+      NodeView view{w, P::kNodeWords, d.node, my_nw};
+      if constexpr (NetPreds<P>::value) {
+        typename P::Rec* ms = s_sends + threadIdx.x * P::kMaxSends;
+        int c = 0;
 #pragma unroll
-          for (int q = 0; q < P::kMaxSends; q++)
-            if ((d.keep >> q) & 1u) ms[c++] = d.out.r[q];
-          view.sends = ms;
-          view.nsends = c;
-        }
-        const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
-        if (v == V_VALID) {
-          if (Net<P>::size(w) + delta_new_count<P>(d) <= P::kNetCap) ship = true;
-          else atomicAdd(&a.ctr->err_overflow, 1ull);
-        } else if (v >= V_TERM_EXCEPTION) {
-          tv = v;
-          tpi = pi;
-          tkey = term_key(v, f.hi);
-        }
+        for (int q = 0; q < P::kMaxSends; q++)
+          if ((d.keep >> q) & 1u) ms[c++] = d.out.r[q];
+        view.sends = ms;
+        view.nsends = c;
+      }
+      const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
+      if (v == V_VALID) {
+        if (Net<P>::size(w) + delta_new_count<P>(d) <= P::kNetCap) ship = true;
+        else atomicAdd(&a.ctr->err_overflow, 1ull);
+      } else if (v >= V_TERM_EXCEPTION) {
+        tv = v;
+        tpi = pi;
+        tkey = term_key(v, f.hi);
       }
     }
     fold_terminals(tkey != ~0ull, tkey, tv, tpi, (uint32_t)k, parent, a.ctr, a.terms, a.term_cap);
-    const unsigned long long li = wave_reserve(&a.ctr->next_size, ship);
-    const bool fits = ship && li < a.next_cap;
+    // the wave's segment: waves take the list in order, so a short list only reaches the first
+    // waves -- by wave, not by workgroup, its rows spread over every segment
+    const int seg = a.seg_ctr ? (int)((blockIdx.x * (kBlock / 64) + wid) % (unsigned)a.nseg) : 0;
+    const unsigned long long li = wave_reserve(a.seg_ctr ? &a.seg_ctr[seg * kSegStride] : &a.ctr->next_size, ship);
+    const bool fits = ship && li < (a.seg_ctr ? a.segcap : a.next_cap);
     if (ship && !fits) atomicAdd(&a.ctr->err_frontier, 1ull);
-    const uint64_t idx = a.next_base + li;
+    const uint64_t idx = a.seg_ctr ? (uint64_t)seg * a.segcap + li : a.next_base + li;
     if (fits) {
-      const uint32_t* w = a.cur + parent * NW;
       a.next_fp[idx] = f;
       a.next_parent[idx] = ((uint64_t)a.me << 48) | parent;
       a.next_event[idx] = (uint32_t)k;
       c_next_work += (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
-    if (wave_emit<P>(fits, a.cur, parent, d, a.next + idx * NW) && __lane_id() == 0)
+    if (wave_emit<P>(fits, wrows, (uint64_t)lane, d, a.next + idx * NW) && __lane_id() == 0)
       atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
+    __builtin_amdgcn_wave_barrier();  // the rows are overwritten by the next iteration's staging
   }
   block_flush(s_red, &a.ctr->next_work, c_next_work);
 }
