@@ -5,17 +5,20 @@ import dslabs.framework.Command;
 import dslabs.framework.Result;
 import java.util.HashMap;
 import java.util.Map;
-import java.util.Objects;
+import lombok.Data;
 import lombok.EqualsAndHashCode;
+import lombok.NonNull;
 import lombok.ToString;
 
 /**
  * The lab1 key-value store (DESIGN.md §11): Get -> GetResult(value) or KeyNotFound, Put -> PutOk,
  * Append -> AppendResult(new value), as KVStoreWorkload expects (KVStoreWorkload.java:40-66). The
- * commands and results are the reference's (labs/lab1-clientserver/src/dslabs/kvstore/KVStore.java),
- * written as records with the same accessors, equality and (Lombok-format) toString -- PaxosTest's
- * hasCommand predicate names carry it. On the device a key is a key id (<= 3
- * keys) and a value a sequence of <= 9 equal-length workload tokens (amokv.hpp).
+ * command and result types are the reference stub's own declarations
+ * (labs/lab1-clientserver/src/dslabs/kvstore/KVStore.java:15-58: Lombok @Data, fluent accessors
+ * from the repository's lombok.config), so their equality and toString -- which PaxosTest's
+ * hasCommand predicate names carry, "KVStore.Append(key=foo, value=X)" -- are Lombok's; only
+ * execute() is written here. On the device a key is a key id (<= 3 keys) and a value a sequence of
+ * <= 9 equal-length workload tokens (amokv.hpp).
  */
 @ToString
 @EqualsAndHashCode
@@ -27,15 +30,9 @@ public class KVStore implements Application {
     String key();
   }
 
-  public record Get(String key) implements SingleKeyCommand {
-    public Get {
-      Objects.requireNonNull(key);
-    }
-
-    @Override
-    public String toString() {
-      return "KVStore.Get(key=" + key + ")";
-    }
+  @Data
+  public static final class Get implements SingleKeyCommand {
+    @NonNull private final String key;
 
     @Override
     public boolean readOnly() {
@@ -43,66 +40,32 @@ public class KVStore implements Application {
     }
   }
 
-  public record Put(String key, String value) implements SingleKeyCommand {
-    public Put {
-      Objects.requireNonNull(key);
-      Objects.requireNonNull(value);
-    }
-
-    @Override
-    public String toString() {
-      return "KVStore.Put(key=" + key + ", value=" + value + ")";
-    }
+  @Data
+  public static final class Put implements SingleKeyCommand {
+    @NonNull private final String key, value;
   }
 
-  public record Append(String key, String value) implements SingleKeyCommand {
-    public Append {
-      Objects.requireNonNull(key);
-      Objects.requireNonNull(value);
-    }
-
-    @Override
-    public String toString() {
-      return "KVStore.Append(key=" + key + ", value=" + value + ")";
-    }
+  @Data
+  public static final class Append implements SingleKeyCommand {
+    @NonNull private final String key, value;
   }
 
   public interface KVStoreResult extends Result {}
 
-  public record GetResult(String value) implements KVStoreResult {
-    public GetResult {
-      Objects.requireNonNull(value);
-    }
-
-    @Override
-    public String toString() {
-      return "KVStore.GetResult(value=" + value + ")";
-    }
+  @Data
+  public static final class GetResult implements KVStoreResult {
+    @NonNull private final String value;
   }
 
-  public record KeyNotFound() implements KVStoreResult {
-    @Override
-    public String toString() {
-      return "KVStore.KeyNotFound()";
-    }
-  }
+  @Data
+  public static final class KeyNotFound implements KVStoreResult {}
 
-  public record PutOk() implements KVStoreResult {
-    @Override
-    public String toString() {
-      return "KVStore.PutOk()";
-    }
-  }
+  @Data
+  public static final class PutOk implements KVStoreResult {}
 
-  public record AppendResult(String value) implements KVStoreResult {
-    public AppendResult {
-      Objects.requireNonNull(value);
-    }
-
-    @Override
-    public String toString() {
-      return "KVStore.AppendResult(value=" + value + ")";
-    }
+  @Data
+  public static final class AppendResult implements KVStoreResult {
+    @NonNull private final String value;
   }
 
   private final Map<String, String> data = new HashMap<>();

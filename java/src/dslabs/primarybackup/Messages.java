@@ -5,37 +5,66 @@ import dslabs.atmostonce.AMOCommand;
 import dslabs.atmostonce.AMOResult;
 import dslabs.framework.Application;
 import dslabs.framework.Message;
+import lombok.Data;
 
 /*
- * lab2 messages (DESIGN.md §12) as records: the same names, components and equality as the
- * reference's (labs/lab2-primarybackup/src/dslabs/primarybackup/Messages.java) plus this solution's
- * primary-backup messages. Device records (dslabs_amd/csrc/protocols/pb.hpp): type:4 | from | to |
- * payload, types 0 Ping .. 8 ForwardAck.
+ * lab2 messages (DESIGN.md §12): the reference stub's ViewServer messages as it declares them
+ * (labs/lab2-primarybackup/src/dslabs/primarybackup/Messages.java: Lombok @Data, fluent accessors)
+ * plus this solution's primary-backup messages in the same form. Device records
+ * (dslabs_amd/csrc/protocols/pb.hpp): type:4 | from | to | payload, types 0 Ping .. 8 ForwardAck.
  */
 
 /* ViewServer messages */
-record Ping(int viewNum) implements Message {}
+@Data
+class Ping implements Message {
+  private final int viewNum;
+}
 
-record GetView() implements Message {}
+@Data
+class GetView implements Message {}
 
-record ViewReply(View view) implements Message {}
+@Data
+class ViewReply implements Message {
+  private final View view;
+}
 
 /* Primary-backup messages */
 
 /** A client's command to the primary it knows (device: type 3, the command's sequence number). */
-record Request(AMOCommand command) implements Message {}
+@Data
+class Request implements Message {
+  private final AMOCommand command;
+}
 
 /** The primary's answer (device: type 4, seq | result:10 @2). */
-record Reply(AMOResult result) implements Message {}
+@Data
+class Reply implements Message {
+  private final AMOResult result;
+}
 
 /** The primary's application, sent to the backup of a new view (device: type 5, view | app:40 @8). */
-record StateTransfer(View view, AMOApplication<Application> app) implements Message {}
+@Data
+class StateTransfer implements Message {
+  private final View view;
+  private final AMOApplication<Application> app;
+}
 
 /** The backup installed the view's state (device: type 6, viewNum). */
-record StateTransferAck(int viewNum) implements Message {}
+@Data
+class StateTransferAck implements Message {
+  private final int viewNum;
+}
 
 /** A client command the primary forwards to its backup (device: type 7, viewNum | client @4 | seq @7). */
-record Forward(int viewNum, AMOCommand command) implements Message {}
+@Data
+class Forward implements Message {
+  private final int viewNum;
+  private final AMOCommand command;
+}
 
 /** The backup executed the forwarded command (device: type 8, as Forward). */
-record ForwardAck(int viewNum, AMOCommand command) implements Message {}
+@Data
+class ForwardAck implements Message {
+  private final int viewNum;
+  private final AMOCommand command;
+}

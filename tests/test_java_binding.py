@@ -348,3 +348,38 @@ def test_java_pb_codec_bounds_every_packed_field():
     assert "v < 0 || v > 15 || seq < 0 || seq > 3" in src  # Forward / ForwardAck
     assert "n > 15" in src  # ViewReply / StateTransfer views
     assert "r < 0 || seq < 0 || seq > 3) return -1;" in src  # the lastResults of a StateTransfer's app
+
+
+def test_java_kvstore_types_are_the_reference_lombok_declarations():
+    """the KV command and result types are the reference stub's own Lombok @Data
+    classes (labs/lab1-clientserver/src/dslabs/kvstore/KVStore.java:15-58, fluent accessors from
+    the repository's lombok.config), not records with hand-written strings, so their toString is
+    Lombok's "KVStore.Append(key=foo, value=X)" -- the form PaxosTest's hasCommand names carry
+    (PaxosTest.java:119-121) and MultiPaxosCodec parses."""
+    src = open(os.path.join(ROOT, "java", "src", "dslabs", "kvstore", "KVStore.java")).read()
+    want = {"Get": ["key"], "Put": ["key, value"], "Append": ["key, value"], "GetResult": ["value"],
+            "KeyNotFound": [], "PutOk": [], "AppendResult": ["value"]}
+    for cls, fields in want.items():
+        m = re.search(r"@Data\s+public static final class %s implements (\w+) \{(.*?)\n  \}" % cls, src, re.S)
+        assert m, cls
+        body = m.group(2)
+        for f in fields:
+            assert "@NonNull private final String %s;" % f in body, (cls, f)
+        assert "toString" not in body
+    assert "record " not in src and "toString()" not in src.split("public class KVStore")[1]
+    codec = open(os.path.join(JAVA, "gpu", "MultiPaxosCodec.java")).read()
+    pat = re.search(r'Pattern KV = Pattern\.compile\("(.*)"\);', codec).group(1).replace("\\\\", "\\")
+    for s, g in (("KVStore.Append(key=foo, value=X)", ("Append", "foo", "X")), ("KVStore.Get(key=foo)", ("Get", "foo", None)),
+                 ("KVStore.Put(key=foo, value=XY)", ("Put", "foo", "XY"))):
+        assert re.fullmatch(pat, s).groups() == g, s
+    # the Paxos / PB message and timer classes are Lombok @Data too (no hand-written strings)
+    seen = 0
+    for d in ("paxos", "primarybackup", "clientserver"):
+        for f in os.listdir(os.path.join(ROOT, "java", "src", "dslabs", d)):
+            text = open(os.path.join(ROOT, "java", "src", "dslabs", d, f)).read()
+            assert not re.search(r"\nrecord \w+\(.*\) implements (?:Message|Timer)", text), f
+            for m in re.finditer(r"\n((?:public )?(?:final )?class (\w+) implements (?:Message|Timer)\b)", text):
+                assert "@Data\n" + m.group(1) in text, (f, m.group(2))
+                seen += 1
+            assert "String toString()" not in text, f
+    assert seen >= 12, seen

@@ -1,5 +1,5 @@
 # Per-level k_level durations of the C5 d12 search for each library variant in $DSL_VARIANTS
-# ("default" = the product library). usage: DSL_VARIANTS="a b" bash tools/gpu_r02_vlevels.sh TAG [bench args]
+# ("default" = the product library). usage: DSL_VARIANTS="a b" bash tools/gpu_level_times.sh TAG [bench args]
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

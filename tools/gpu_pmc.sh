@@ -1,6 +1,6 @@
 # Round-2 profile of bench.py's workload: kernel trace + stats, then one rocprofv3 --pmc pass per
 # counter group (HBM bytes, atomics at L2 / memory, L2 hit rate, DRAM vs Infinity-Cache reads, SQ).
-# usage: bash tools/gpu_r02_prof.sh TAG [bench args...]
+# usage: bash tools/gpu_pmc.sh TAG [bench args...]
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

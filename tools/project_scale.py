@@ -53,6 +53,7 @@ def main():
     slabs = shard_lines(ew)
     t_single = sum(sum(l.values()) for l in single)
     t_multi = 0.0
+    rep_t, sh_t = [], []
     print(f"# W={W}: per level, one GPU's time (us): kernels (sum over shards / W), exchange at {bw} GB/s per link "
           f"+ {round_us} us per round, {sync_us} us host round trip; replicated levels as on one GPU")
     for i, lv in enumerate(multi):
@@ -65,12 +66,26 @@ def main():
             t = k / W + comm + sync_us
             print(f"level {depth}: sharded, kernels {k / W:.1f} + exchange {comm:.1f} + sync {sync_us} = {t:.1f} "
                   f"(one GPU: {sum(single[i].values()):.1f})")
+            sh_t.append(t)
         else:
             t = sum(single[i].values())
             print(f"level {depth}: replicated {t:.1f}")
+            sh_t.append(None)
+        rep_t.append(sum(single[i].values()))
         t_multi += t
     print(f"kernels of one search on one GPU {t_single:.1f} us; projected at W={W}: {t_multi:.1f} us "
           f"-> {t_single / t_multi:.2f}x (per-search host time excluded from both)")
+    # the cost rule's plan: replicated up to some level, sharded from there on (a sharded level's
+    # tables no longer hold every state), the switch where it pays most
+    best, best_s = sum(rep_t), len(rep_t)
+    for sw in range(len(rep_t)):
+        if any(x is None for x in sh_t[sw:]):
+            continue
+        t = sum(rep_t[:sw]) + sum(sh_t[sw:])
+        if t < best:
+            best, best_s = t, sw
+    plan = "replicated throughout" if best_s == len(rep_t) else f"sharded from level {best_s + 1}"
+    print(f"best plan ({plan}): {best:.1f} us -> {t_single / best:.2f}x")
 
 
 if __name__ == "__main__":
