@@ -178,7 +178,8 @@ struct BfsEngine : EngineBase {
   // k_level_record), on the device and pinned on the host
   // [0, kMaxShards * kRecWords): the local shards' records; then the gathered records (RCCL);
   // then the completion phase's route-spill counts (kMaxShards x kMaxShards)
-  static constexpr int kXWords = 2 * kMaxShards * kRecWords + kMaxShards * kMaxShards;
+  static constexpr int kXRecEnd = 2 * kMaxShards * kRecWords + kMaxShards * kMaxShards;
+  static constexpr int kXWords = kXRecEnd + kMaxShards * kCtrMirrorWords;  // + the counters' mirrors
   uint64_t* xdev = nullptr;
   // the device-side deadline of a time-limited search (LevelArgs::budget_rt): the device clock at
   // the search's start (k_clock) and the budget in its ticks; not used in a replicated level of a
@@ -918,7 +919,9 @@ struct BfsEngine : EngineBase {
 
   // Every local shard's level record (k_level_record) computed on the device, gathered by every
   // rank, read with the shards' counters in ONE host round trip; recs = W records.
-  int gather_records(const std::vector<uint64_t>& extra_rows, uint64_t time_up, std::vector<uint64_t>& recs) {
+  // zero_rc: the fast path's gather is the route counters' last reader (no fill launch per level).
+  int gather_records(const std::vector<uint64_t>& extra_rows, uint64_t time_up, std::vector<uint64_t>& recs,
+                     bool zero_rc = false) {
     const int L = (int)sh.size();
     const bool dev_gather = comm && comm->device_collectives();
     for (int l = 0; l < L; l++) {
@@ -936,21 +939,26 @@ struct BfsEngine : EngineBase {
       ra.gid = S.gid;
       ra.W = W;
       ra.rc = S.rc;
+      ra.zero_rc = zero_rc ? 1 : 0;
       ra.cap_fp = S.cap_fp;
       ra.out = xdev + (size_t)l * kRecWords;
+      ra.ctr_out = xdev + kXRecEnd + (size_t)l * kCtrMirrorWords;
       hipLaunchKernelGGL(k_level_record, dim3(1), dim3(64), 0, stream, ra);
       DSL_HIP(hipGetLastError());
     }
     uint64_t* gdev = xdev + (size_t)kMaxShards * kRecWords;
-    if (dev_gather) {
-      DSL_TRY(comm->allgather_dev(xdev, kRecWords, gdev, stream));
-      DSL_HIP(hipMemcpyAsync(xhost, gdev, (size_t)W * kRecWords * 8, hipMemcpyDeviceToHost, stream));
-    } else {
-      DSL_HIP(hipMemcpyAsync(xhost, xdev, (size_t)L * kRecWords * 8, hipMemcpyDeviceToHost, stream));
-    }
-    for (auto& S : sh)
-      DSL_HIP(hipMemcpyAsync(S.hctr, S.ctr, kCtrSegOff + 8 * S.nseg * kSegStride, hipMemcpyDeviceToHost, stream));
+    if (dev_gather) DSL_TRY(comm->allgather_dev(xdev, kRecWords, gdev, stream));
+    // ONE copy: the (gathered) records through the local shards' counter mirrors
+    const size_t from = dev_gather ? (size_t)kMaxShards * kRecWords : 0;
+    DSL_HIP(hipMemcpyAsync(xhost, xdev + from, (kXRecEnd + (size_t)L * kCtrMirrorWords - from) * 8,
+                           hipMemcpyDeviceToHost, stream));
     DSL_TRY(hsync());
+    for (int l = 0; l < L; l++) {  // the counters as the strided counter set (S.hctr's layout)
+      Shard& S = sh[l];
+      const uint64_t* m = xhost + (kXRecEnd - from) + (size_t)l * kCtrMirrorWords;
+      std::memcpy(S.hctr, m, sizeof(LevelCounters));
+      for (int q = 0; q < S.nseg; q++) std::memcpy(S.hctr + kCtrSegOff + (size_t)q * kSegStride * 8, m + kLcWords + q, 8);
+    }
     recs.assign((size_t)W * kRecWords, 0);
     if (comm && !dev_gather) {
       stats.host_syncs++;
@@ -976,7 +984,8 @@ struct BfsEngine : EngineBase {
     if (cs) {
       for (auto& S : sh) {
         hipLaunchKernelGGL(k_route_headers, dim3(1), dim3(kMaxShards * kRouteSegs), 0, stream,
-                           (const RouteCounters*)S.rc, S.out_key, S.cap_fp, cs, W);
+                           (const RouteCounters*)S.rc, S.out_key, S.cap_fp, cs, W,
+                           (unsigned long long*)(last ? nullptr : S.nl_ctr));
         DSL_HIP(hipGetLastError());
       }
       // round A: the regions of every (source, owner) pair
@@ -1006,8 +1015,7 @@ struct BfsEngine : EngineBase {
         pa.reply = last ? nullptr : S.rep_out;
         pa.self_reply = S.rep_in + (size_t)S.gid * S.cap_fp;
         pa.ctr = S.ctr;
-        const int gy = (int)std::max<uint64_t>(1, std::min<uint64_t>((cs + kBlock - 1) / kBlock, 64));
-        hipLaunchKernelGGL(k_probe_slab, dim3(W * kRouteSegs, gy), dim3(kBlock), 0, stream, pa);
+        hipLaunchKernelGGL(k_probe_slab, dim3(W * kRouteSegs, slab_gy(W * kRouteSegs, cs)), dim3(kBlock), 0, stream, pa);
         DSL_HIP(hipGetLastError());
       }
       if (!last) {
@@ -1029,7 +1037,7 @@ struct BfsEngine : EngineBase {
       }
     }
     std::vector<uint64_t> extra(L, 0);
-    DSL_TRY(gather_records(extra, time_up, recs));
+    DSL_TRY(gather_records(extra, time_up, recs, true));
     bool incomplete = false, errors = false;
     for (int x = 0; x < W; x++) {
       const uint64_t* r = recs.data() + (size_t)x * kRecWords;
@@ -1049,11 +1057,16 @@ struct BfsEngine : EngineBase {
     }
     if (incomplete && !errors) {
       stats.completions++;
+      // the level's routed counts: the first gather's (it zeroed the route counters)
+      std::vector<uint64_t> routes((size_t)W * kMaxShards);
+      for (int x = 0; x < W; x++)
+        std::memcpy(&routes[(size_t)x * kMaxShards], &recs[(size_t)x * kRecWords + kRecRoute], kMaxShards * 8);
       DSL_TRY(complete_sharded(depth, last, time_up, recs));
+      for (int x = 0; x < W; x++)
+        std::memcpy(&recs[(size_t)x * kRecWords + kRecRoute], &routes[(size_t)x * kMaxShards], kMaxShards * 8);
     } else {
       stats.fast_levels++;
     }
-    for (auto& S : sh) DSL_HIP(hipMemsetAsync(S.rc, 0, sizeof(RouteCounters), stream));
     // the next frontier of every local shard: the segments k_materialize filled, the completion
     // phase's materialized rows and its row spills (k_level appends none on a sharded level)
     for (int l = 0; l < L; l++) {
@@ -1081,6 +1094,16 @@ struct BfsEngine : EngineBase {
     return DSL_OK;
   }
 
+  // Blocks per group of the slab kernels (k_probe_slab, k_new_list: grid x = the groups, y =
+  // blocks of a group, grid-stride): about the workgroups resident at once in all. The grid used to
+  // be (W * 32, up to 64) = 16,384 workgroups at W = 8, mostly without a record: dispatching them
+  // was most of the launch (C5's level 12: 27 us of k_probe_slab per shard).
+  static int slab_gy(int groups, uint64_t per) {
+    static const int total = getenv("DSL_SLAB_BLOCKS") ? std::max(1, atoi(getenv("DSL_SLAB_BLOCKS"))) : 2048;
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>((per + kBlock - 1) / kBlock,
+                                                         (uint64_t)std::max(1, total / std::max(1, groups))));
+  }
+
   // k_new_list + k_materialize of shard S: the new ones among its routed records (the fast path's
   // sub-slabs with device counts, or host counts cnt[d] of regions of `cap` records), appended at
   // seg_span + uns_room (next_size counts them across calls).
@@ -1100,9 +1123,9 @@ struct BfsEngine : EngineBase {
     const uint64_t per = dev ? S.route_cs : cap, items = per * (uint64_t)W * (dev ? kRouteSegs : 1);
     const uint64_t room = dev ? S.seg_span : S.mat_room;
     if (!items || !room) return DSL_OK;
-    DSL_HIP(hipMemsetAsync(S.nl_ctr, 0, 8, stream));
-    const int gy = (int)std::max<uint64_t>(1, std::min<uint64_t>((per + kBlock - 1) / kBlock, 64));
-    hipLaunchKernelGGL(k_new_list, dim3(dev ? W * kRouteSegs : W, gy), dim3(kBlock), 0, stream, na);
+    if (!dev) DSL_HIP(hipMemsetAsync(S.nl_ctr, 0, 8, stream));  // dev: zeroed by k_route_headers
+    const int groups = dev ? W * kRouteSegs : W;
+    hipLaunchKernelGGL(k_new_list, dim3(groups, slab_gy(groups, per)), dim3(kBlock), 0, stream, na);
     DSL_HIP(hipGetLastError());
     MaterializeArgs<P> ma{};
     ma.sent_key = sent_key;
@@ -1126,8 +1149,13 @@ struct BfsEngine : EngineBase {
     ma.ctr = S.ctr;
     ma.terms = S.terms;
     ma.term_cap = term_cap;
-    const int blocks = (int)std::min<uint64_t>((std::min(items, room) + kBlock - 1) / kBlock, 8192);
-    const size_t lds = (size_t)(kBlock / 64) * mat_per_max<P>() * NW * 4;
+    // the grid: the workgroups resident at once (a wave takes 8..PMAX states; more workgroups only
+    // launched and left, ~7,000 of 8,192 on C5's sharded levels)
+    static const int mat_blocks = getenv("DSL_MAT_BLOCKS") ? std::max(1, atoi(getenv("DSL_MAT_BLOCKS"))) : 1024;
+    const int blocks = (int)std::min<uint64_t>((std::min(items, room) + kBlock - 1) / kBlock, (uint64_t)mat_blocks);
+    static const int mat_per = getenv("DSL_MAT_PER") ? std::max(1, std::min(mat_per_max<P>(), atoi(getenv("DSL_MAT_PER")))) : 0;
+    ma.per_fixed = mat_per;
+    const size_t lds = (size_t)(kBlock / 64) * (mat_per ? mat_per : mat_per_max<P>()) * NW * 4;
     hipLaunchKernelGGL(k_materialize<P>, dim3(std::max(1, blocks)), dim3(kBlock), lds, stream, ma, prm, dset);
     DSL_HIP(hipGetLastError());
     return DSL_OK;
@@ -1848,6 +1876,13 @@ struct BfsEngine : EngineBase {
             if (S.lc.phcls[16 + c])
               fprintf(stderr, " c%d: %.3g cyc / %llu passes (%.0f)", c, (double)S.lc.phcls[c],
                       (unsigned long long)S.lc.phcls[16 + c], (double)S.lc.phcls[c] / S.lc.phcls[16 + c]);
+          if (S.lc.phcls[31]) {  // k_materialize (sharded levels): cycles per wave pass by phase
+            fprintf(stderr, "\n[matph] depth %d passes %llu cycles/pass: items %.0f stage %.0f handler %.0f judge %.0f "
+                    "reserve+count %.0f emit %.0f", depth + 1, (unsigned long long)S.lc.phcls[31],
+                    (double)S.lc.phcls[10] / S.lc.phcls[31], (double)S.lc.phcls[11] / S.lc.phcls[31],
+                    (double)S.lc.phcls[12] / S.lc.phcls[31], (double)S.lc.phcls[13] / S.lc.phcls[31],
+                    (double)S.lc.phcls[14] / S.lc.phcls[31], (double)S.lc.phcls[15] / S.lc.phcls[31]);
+          }
           fprintf(stderr, "\n");
         }
 #elif defined(DSL_TIMELINE)

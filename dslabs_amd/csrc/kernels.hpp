@@ -257,6 +257,27 @@ __device__ __forceinline__ unsigned long long block_reserve(BlockResv<BS>& s, un
   return pred ? s.off[wid][dest] + (unsigned long long)__popcll(mine & lt) : 0ull;
 }
 
+// Wave-level slot reservation on per-destination counters (ctrs[d * stride], d < W <= kMaxShards):
+// one ballot per destination, then lane d issues destination d's returning atomic -- the W atomics
+// of a wave are in flight together, one memory round trip, and no barrier (k_level's routed passes
+// then take dynamic groups like the unrouted ones). Must be called by all lanes of the wave.
+__device__ __forceinline__ unsigned long long wave_reserve_dest(unsigned long long* ctrs, bool pred, int dest, int W,
+                                                                int stride) {
+  const int lane = __lane_id();
+  unsigned long long mine = 0;
+  uint32_t cnt = 0;
+  for (int d = 0; d < W; d++) {
+    const bool me = pred && dest == d;
+    const unsigned long long m = __ballot(me);
+    if (lane == d) cnt = (uint32_t)__popcll(m);
+    if (me) mine = m;
+  }
+  unsigned long long base = 0;
+  if (lane < W && cnt) base = atomicAdd(&ctrs[(size_t)lane * stride], (unsigned long long)cnt);
+  base = __shfl(base, pred ? dest : 0);
+  return pred ? base + (unsigned long long)__popcll(mine & ((1ull << lane) - 1ull)) : 0ull;
+}
+
 // Sums a per-thread value over the workgroup and adds it to *ctr with one atomic (kernel exit).
 template <int BS = kBlock>
 __device__ __forceinline__ void block_flush(unsigned long long* red, unsigned long long* ctr, unsigned long long v) {
@@ -886,12 +907,16 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
       // wave, so a shorter critical path. In a larger level (throughput-bound) each wave takes the
       // next group of 64 class-sorted items from an LDS counter until the window is done, so the
       // waves finish the window together whatever their handlers cost (a fixed share per wave
-      // left the others waiting at the window's barrier). ROUTE levels keep fixed shares:
-      // block_reserve is a workgroup-wide step.
+      // left the others waiting at the window's barrier). ROUTE levels too: their reservations are
+      // per wave (wave_reserve_dest).
 #ifdef DSL_NO_DYN  // measurement variant: fixed shares in every level
       const bool dyn = false;
 #else
+#ifdef DSL_ROUTE_BLOCK  // measurement variant: workgroup-wide route reservations, fixed shares
       const bool dyn = !ROUTE && !spread;
+#else
+      const bool dyn = !spread;
+#endif
 #endif
       for (int base = 0;;) {
         int t;
@@ -1057,9 +1082,16 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           // (BfsEngine::complete_sharded; rare)
           // the workgroup's sub-slab rotates with its passes, so one workgroup's records (a small
           // level has few workgroups) spread over every sub-slab
+#ifdef DSL_ROUTE_BLOCK
           const int sub = (int)((blockIdx.x + (unsigned)npass++) % kRouteSegs);
           const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out + rc_idx(0, sub), route, dest,
                                                                      a.W, kRouteSegs * kRouteStride);
+#else
+          // by wave: the wave's sub-slab rotates with its passes
+          const int sub = (int)((blockIdx.x * NWAVE + (unsigned)wid + (unsigned)npass++) % kRouteSegs);
+          const unsigned long long ridx = wave_reserve_dest(a.rc->out + rc_idx(0, sub), route, dest, a.W,
+                                                            kRouteSegs * kRouteStride);
+#endif
           if (route) {
             const uint64_t item = ((p0 + j) << 20) | (uint64_t)k;
             if (ridx < a.route_cs) {
@@ -1264,22 +1296,36 @@ struct RecordArgs {
   uint64_t mat_cap;        // materialized rows = min(next_size, mat_cap)
   uint64_t parents, time_up;
   int32_t gid, W;
-  const RouteCounters* rc;  // null: no routing this level
+  RouteCounters* rc;  // null: no routing this level
+  int32_t zero_rc;    // the record is the route counters' last reader: zero them for the next level
   uint64_t cap_fp;
   uint64_t* out;
+  uint64_t* ctr_out;  // the shard's LevelCounters and its nseg segment counts (kCtrMirrorWords), so
+                      // the host reads records and counters in ONE copy
 };
+constexpr int kLcWords = (int)(sizeof(LevelCounters) / 8);
+constexpr int kCtrMirrorWords = kLcWords + kSegs;
+static_assert(sizeof(LevelCounters) % 8 == 0, "LevelCounters mirrored in 8-byte words");
 __global__ void __launch_bounds__(64) k_level_record(RecordArgs a) {
   // one wave: the segment counters and the route counters summed lane-parallel (a single thread
   // walking them took ~13 us of dependent loads per launch)
   const int lane = threadIdx.x;
   const LevelCounters* c = a.c;
   uint32_t seg = 0;
-  for (int q = lane; q < a.nseg; q += 64) seg += (uint32_t)min<uint64_t>(a.seg_ctr[q * kSegStride], a.segcap);
+  for (int q = lane; q < a.nseg; q += 64) {
+    const uint64_t v = a.seg_ctr[q * kSegStride];
+    seg += (uint32_t)min<uint64_t>(v, a.segcap);
+    a.ctr_out[kLcWords + q] = v;
+  }
+  for (int i = lane; i < kLcWords; i += 64) a.ctr_out[i] = reinterpret_cast<const uint64_t*>(c)[i];
   uint64_t route[kMaxShards];
 #pragma unroll
   for (int d = 0; d < kMaxShards; d++) {
     uint64_t r = 0;
-    if (a.rc && d < a.W && lane < kRouteSegs) r = a.rc->out[rc_idx(d, lane)];
+    if (a.rc && d < a.W && lane < kRouteSegs) {
+      r = a.rc->out[rc_idx(d, lane)];
+      if (a.zero_rc) a.rc->out[rc_idx(d, lane)] = 0;
+    }
     for (int o = 32; o > 0; o >>= 1) r += __shfl_xor(r, o);
     route[d] = r;
   }
@@ -1308,9 +1354,12 @@ __global__ void __launch_bounds__(64) k_level_record(RecordArgs a) {
 }
 
 // The header of every destination region (the kRouteSegs counts of its sub-slabs, clipped to the
-// sub-slab capacity); the owner reads it from the region it receives (k_probe_slab).
-__global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t cap_fp, uint64_t cs, int W) {
+// sub-slab capacity); the owner reads it from the region it receives (k_probe_slab). Also zeroes
+// k_new_list's counter for this level (no separate fill launch).
+__global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t cap_fp, uint64_t cs, int W,
+                                unsigned long long* zero_ctr) {
   const int t = threadIdx.x, d = t / kRouteSegs, q = t - d * kRouteSegs;
+  if (t == 0 && zero_ctr) *zero_ctr = 0ull;
   if (d < W)
     reinterpret_cast<uint64_t*>(out_key + (uint64_t)d * cap_fp)[q] = min<uint64_t>(rc->out[rc_idx(d, q)], cs);
 }
@@ -1474,6 +1523,7 @@ struct MaterializeArgs {
   LevelCounters* ctr;                // next_size counts the appended rows
   TerminalRec* terms;
   uint32_t term_cap;
+  int32_t per_fixed;                 // states per wave (<= the LDS rows per wave), 0: from the list size
 };
 
 // States per wave at most in k_materialize: a wave stages its states' parent rows in LDS (8 KiB
@@ -1497,12 +1547,23 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
   // states per wave: a wave writes its rows one after another (wave_emit), so a short list is
   // spread over about as many waves as the chip holds at once (at least 8 states each) instead of
   // 64 per wave on a few workgroups (C5's sharded levels: ~85 us per launch whatever the size); a
-  // long list keeps up to PMAX per wave (C3: the handler's lanes full)
+  // long list keeps up to PMAX per wave (C3: the handler's lanes full). The grid is about the
+  // resident workgroups (BfsEngine::launch_materialize): every wave of it has work.
   const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
-  const int per = (int)max<uint64_t>(8, min<uint64_t>(PMAX, (n + 4095) / 4096));
+  const int per = a.per_fixed ? a.per_fixed : (int)max<uint64_t>(8, min<uint64_t>(PMAX, (n + waves - 1) / waves));
   const int lane = __lane_id(), wid = threadIdx.x >> 6;
-  uint32_t* wrows = s_mrows + wid * PMAX * NW;
+  uint32_t* wrows = s_mrows + wid * per * NW;
+#ifdef DSL_PHASES  // per-phase shader cycles of the wave passes: LevelCounters::phcls[10..15], passes in [31]
+  unsigned long long mph[6] = {0, 0, 0, 0, 0, 0}, mpass = 0, mt = clock64();
+#define MAT_PH(i) do { const unsigned long long t1 = clock64(); mph[i] += t1 - mt; mt = t1; } while (0)
+#else
+#define MAT_PH(i) do { } while (0)
+#endif
   for (uint64_t base = ((uint64_t)blockIdx.x * (kBlock / 64) + wid) * per; base < n; base += waves * per) {
+#ifdef DSL_PHASES
+    mpass++;
+    mt = clock64();
+#endif
     const uint64_t i = base + lane;
     const bool act = lane < per && i < n;
     bool ship = false;
@@ -1514,14 +1575,21 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       parent = item >> 20;
       k = (int)(item & 0xfffff);
     }
-    // the wave's parent rows into LDS, 16 bytes per lane per instruction
+    MAT_PH(0);  // (the loads' latency shows in the staging phase, their first use)
+    // the wave's parent rows into LDS with LDS-DMA (no register round trip: a load-then-store
+    // copy waited for each row's load before the next row's, ~9 us per pass on C5's level 11)
     const int nr = (int)min<uint64_t>((uint64_t)per, n - base);
     for (int r = 0; r < nr; r++) {
       const uint4* src = reinterpret_cast<const uint4*>(a.cur + rl64(parent, r) * NW);
-      for (int c = lane; c < NW / 4; c += 64) reinterpret_cast<uint4*>(wrows + r * NW)[c] = src[c];
+#pragma unroll
+      for (int b = 0; b < NW / 4; b += 64)
+        if (b + lane < NW / 4)
+          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + b + lane),
+                                           (__attribute__((address_space(3))) void*)(wrows + r * NW + 4 * b), 16, 0, 0);
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
+    MAT_PH(1);
     const uint32_t* w = wrows + (act ? lane : 0) * NW;
     Delta<P> d;
     d.node = 0;
@@ -1530,6 +1598,9 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
     Fp f{0, 0};
     if (act) {
       delta_step<P>(w, k, d, prm, set);  // deterministic: the successor k_level fingerprinted
+    }
+    MAT_PH(2);
+    if (act) {
       f = a.sent_key[slot];
       int pi = -1;
       uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
@@ -1556,6 +1627,7 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       }
     }
     fold_terminals(tkey != ~0ull, tkey, tv, tpi, (uint32_t)k, parent, a.ctr, a.terms, a.term_cap);
+    MAT_PH(3);
     // the wave's segment: waves take the list in order, so a short list only reaches the first
     // waves -- by wave, not by workgroup, its rows spread over every segment
     const int seg = a.seg_ctr ? (int)((blockIdx.x * (kBlock / 64) + wid) % (unsigned)a.nseg) : 0;
@@ -1569,10 +1641,20 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       a.next_event[idx] = (uint32_t)k;
       c_next_work += (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
-    if (wave_emit<P>(fits, wrows, (uint64_t)lane, d, a.next + idx * NW) && __lane_id() == 0)
+    MAT_PH(4);
+    if (wave_emit<P>(fits, wrows, (uint64_t)lane, d, a.next + idx * NW, s_nodew + (threadIdx.x - lane) * P::kNodeWords) &&
+        __lane_id() == 0)
       atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
     __builtin_amdgcn_wave_barrier();  // the rows are overwritten by the next iteration's staging
+    MAT_PH(5);
   }
+#ifdef DSL_PHASES
+  if (lane == 0 && mpass) {
+    for (int q = 0; q < 6; q++) atomicAdd(&a.ctr->phcls[10 + q], mph[q]);
+    atomicAdd(&a.ctr->phcls[31], mpass);
+  }
+#endif
+#undef MAT_PH
   block_flush(s_red, &a.ctr->next_work, c_next_work);
 }
 

@@ -21,6 +21,7 @@
 // prints one JSON line: end, per_depth, states (per run), elapsed_s (last run), threads,
 // states_per_s (timed runs' states / their time), runs, timed_s
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -122,6 +123,12 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
     std::atomic<int> level_best{99};
     std::atomic<int> level_err{0};
     constexpr uint64_t kChunk = 64;
+    // DSL_CPU_CENSUS: per handler class (event_class_skip), events / filtered as surely no-op /
+    // run but no-op / probed / new (a measurement of the no-op filter's reach, to stderr)
+    constexpr int NC = P::kMsgClasses + 2;
+    static const bool census = getenv("DSL_CPU_CENSUS") != nullptr;
+    std::vector<std::array<unsigned long long, 5 * NC>> cen(threads);
+    for (auto& c : cen) c.fill(0);
     auto work = [&](int t) {
       std::vector<Row>& out = (*nxt)[t];
       out.clear();
@@ -139,7 +146,22 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
           const int ne = count_events<P>(r.w, prm, set);
           for (int k = 0; k < ne; k++) {
             Delta<P> dl;
+            int cls = 0, real = 0;
+            if (census) {
+              cls = event_class_skip<P>(r.w, prm, set, k);
+              // the filtered events' real class (the handler a skipped event would have run)
+              real = cls;
+              if (cls == P::kMsgClasses + 1) {
+                const int e = locate_event<P>(r.w, prm, set, k);
+                real = e < 0 ? P::kMsgClasses : P::msg_class(Net<P>::at(r.w, e));
+              }
+              cen[t][5 * real + (cls == P::kMsgClasses + 1 ? 1 : 0)]++;
+            }
             const int rc = delta_step<P>(r.w, k, dl, prm, set);
+            if (census && cls != P::kMsgClasses + 1) {
+              const bool nop = rc == STEP_OK && dl.keep == 0 && same_words<P::kNodeWords>(dl.nw, r.w + dl.node * P::kNodeWords);
+              cen[t][5 * real + (nop ? 2 : 3)]++;
+            }
             if (rc == STEP_NULL) continue;
             if (rc == STEP_EXCEPTION) {  // never equal to another state: new and terminal
               c_new++;
@@ -159,6 +181,7 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
             }
             if (ins == 0) continue;
             c_new++;
+            if (census) cen[t][5 * (cls == P::kMsgClasses + 1 ? 0 : cls) + 4]++;
             int pidx = -1;
             NodeView view{r.w, P::kNodeWords, dl.node, dl.nw};
             typename P::Rec news[P::kMaxSends];
@@ -193,6 +216,17 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
     if (getenv("DSL_CPU_TRACE"))
       fprintf(stderr, "level %d: %llu parents, %.3f ms\n", depth + 1, (unsigned long long)F,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count());
+    if (census) {
+      fprintf(stderr, "census level %d (class: events filtered run_noop probed new):", depth + 1);
+      for (int c = 0; c < NC; c++) {
+        unsigned long long v[5] = {0, 0, 0, 0, 0};
+        for (auto& x : cen)
+          for (int i = 0; i < 5; i++) v[i] += x[5 * c + i];
+        if (v[0] || v[1] || v[2] || v[3])
+          fprintf(stderr, " | %d: %llu %llu %llu %llu %llu", c, v[0] + v[1], v[1], v[2], v[3], v[4]);
+      }
+      fprintf(stderr, "\n");
+    }
     per.push_back(level_new.load());
     if (level_err) err = level_err == 2 ? "visited table full" : "network overflow";
     best = level_best.load();
