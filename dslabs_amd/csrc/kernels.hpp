@@ -432,6 +432,84 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
   return collision;
 }
 
+// Lane-parallel row emission for small rows (LaneEmit<P>: at most 64 words and 3 sends per step,
+// e.g. the synthetic C3's 64-byte rows): every active lane writes its OWN row, 16 bytes per store,
+// instead of the wavefront writing its rows one after another (wave_emit: ~100 wave-instructions
+// per row, the same for a 64-byte row as for a 640-byte one). The row is streamed in 16-byte units
+// with compile-time word offsets: header words from the parent row `pw` (LDS) with the changed
+// node's words and the new record count patched in; the records as the merge of the parent's
+// sorted records with the kept sends, sorted first by a compare-exchange network (at most 3).
+// Returns true (wave-uniform) when two kept sends of one row were equal (see wave_emit).
+template <class P, class = void>
+struct LaneEmit : std::integral_constant<bool, (Layout<P>::kWords <= 64 && P::kMaxSends <= 3)> {};
+
+template <class P>
+__device__ __forceinline__ bool lane_emit(bool active, const uint32_t* pw, const Delta<P>& d, uint32_t* dst) {
+  using L = Layout<P>;
+  using Rec = typename P::Rec;
+  constexpr int NW = L::kWords, RW = L::kRecWords, M = P::kMaxSends, NWd = P::kNodeWords;
+  bool coll = false;
+  if (active) {
+    const int n = Net<P>::size(pw);
+    Rec sv[M];
+#pragma unroll
+    for (int i = 0; i < M; i++) sv[i] = ((d.keep >> i) & 1u) ? d.out.r[i] : ~(Rec)0;
+    const int m = __builtin_popcount(d.keep);
+    // compare-exchange network (M <= 3): ascending, the unkept sentinels last
+    auto cx = [&](int a, int b) {
+      const Rec lo = sv[a] < sv[b] ? sv[a] : sv[b], hi = sv[a] < sv[b] ? sv[b] : sv[a];
+      sv[a] = lo;
+      sv[b] = hi;
+    };
+    if constexpr (M >= 2) cx(0, 1);
+    if constexpr (M >= 3) {
+      cx(1, 2);
+      cx(0, 1);
+    }
+    if constexpr (SendsDistinct<P>::value) {  // two kept sends equal: they would share a slot
+#pragma unroll
+      for (int i = 0; i + 1 < M; i++) coll |= i + 1 < m && sv[i] == sv[i + 1];
+    }
+    const int rel0 = d.node * NWd;
+    int i = 0, j = 0;  // the merge: next send, next parent record
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    typedef __attribute__((address_space(1))) v4u g128;
+    g128* o4 = (g128*)dst;
+#pragma unroll
+    for (int u = 0; u < NW / 4; u++) {
+      uint32_t w4[4];
+      Rec cur = 0;
+#pragma unroll
+      for (int t = 0; t < 4; t++) {
+        const int o = 4 * u + t;
+        uint32_t v = 0;
+        if (o < L::kNetCount) {
+          v = pw[o];
+          const int rel = o - rel0;
+#pragma unroll
+          for (int x = 0; x < NWd; x++) v = rel == x ? d.nw[x] : v;
+        } else if (o == L::kNetCount) {
+          v = (uint32_t)(n + m);
+        } else if (o >= L::kRecBase && o < L::kRecBase + P::kNetCap * RW) {
+          if ((o - L::kRecBase) % RW == 0) {  // the next merged record
+            const Rec s = M == 1 ? sv[0] : M == 2 ? (i == 0 ? sv[0] : sv[1 < M ? 1 : 0])
+                                              : (i == 0 ? sv[0] : i == 1 ? sv[1 < M ? 1 : 0] : sv[2 < M ? 2 : 0]);
+            const Rec p = j < n ? Net<P>::at(pw, j) : ~(Rec)0;
+            const bool take_s = i < m && (j >= n || s < p);
+            cur = take_s ? s : j < n ? p : (Rec)0;
+            i += take_s ? 1 : 0;
+            j += (!take_s && j < n) ? 1 : 0;
+          }
+          v = RW == 2 && (o - L::kRecBase) % RW == 1 ? (uint32_t)((uint64_t)cur >> 32) : (uint32_t)cur;
+        }
+        w4[t] = v;
+      }
+      o4[u] = v4u{w4[0], w4[1], w4[2], w4[3]};
+    }
+  }
+  return __ballot(coll) != 0ull;
+}
+
 template <class P>
 struct LevelArgs {
   const uint32_t* cur;       // frontier rows of kWords (row ranges in `segs`)
@@ -1059,8 +1137,10 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             a.next_event[idx] = (uint32_t)k;
             c_next_work += (uint32_t)delta_event_count<P>(w, off[j + 1] - off[j], d, prm, set);
           }
-          if (wave_emit<P, SP>(fits, rows, (uint64_t)j, d, a.next + idx * NW, s_nodew + (tid - lane) * P::kNodeWords) &&
-              lane == 0)
+          bool coll;
+          if constexpr (LaneEmit<P>::value) coll = lane_emit<P>(fits, rows + j * SP, d, a.next + idx * NW);
+          else coll = wave_emit<P, SP>(fits, rows, (uint64_t)j, d, a.next + idx * NW, s_nodew + (tid - lane) * P::kNodeWords);
+          if (coll && lane == 0)
             atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
 #ifdef DSL_X2_EMIT  // cost probe (measurement builds): the same rows written twice
           wave_emit<P, SP>(fits, rows, (uint64_t)j, d, a.next + idx * NW);
@@ -1579,13 +1659,27 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
     // the wave's parent rows into LDS with LDS-DMA (no register round trip: a load-then-store
     // copy waited for each row's load before the next row's, ~9 us per pass on C5's level 11)
     const int nr = (int)min<uint64_t>((uint64_t)per, n - base);
-    for (int r = 0; r < nr; r++) {
-      const uint4* src = reinterpret_cast<const uint4*>(a.cur + rl64(parent, r) * NW);
+    constexpr int U = NW / 4;  // 16-byte units per row
+    if constexpr (U < 64 && 64 % U == 0) {
+      // small rows: 64 / U rows per wave-instruction (lane = row * U + unit; LDS row-major)
+      constexpr int RPI = 64 / U;
+      for (int r0 = 0; r0 < nr; r0 += RPI) {
+        const int r = r0 + lane / U;
+        const uint64_t pr = __shfl((unsigned long long)parent, r < 64 ? r : 63);
+        if (r < nr)
+          __builtin_amdgcn_global_load_lds(
+              (const __attribute__((address_space(1))) void*)(reinterpret_cast<const uint4*>(a.cur + pr * NW) + lane % U),
+              (__attribute__((address_space(3))) void*)(wrows + r0 * NW), 16, 0, 0);
+      }
+    } else {
+      for (int r = 0; r < nr; r++) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.cur + rl64(parent, r) * NW);
 #pragma unroll
-      for (int b = 0; b < NW / 4; b += 64)
-        if (b + lane < NW / 4)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + b + lane),
-                                           (__attribute__((address_space(3))) void*)(wrows + r * NW + 4 * b), 16, 0, 0);
+        for (int b = 0; b < U; b += 64)
+          if (b + lane < U)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + b + lane),
+                                             (__attribute__((address_space(3))) void*)(wrows + r * NW + 4 * b), 16, 0, 0);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
@@ -1642,8 +1736,10 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
       c_next_work += (unsigned long long)delta_event_count<P>(w, count_events<P>(w, prm, set), d, prm, set);
     }
     MAT_PH(4);
-    if (wave_emit<P>(fits, wrows, (uint64_t)lane, d, a.next + idx * NW, s_nodew + (threadIdx.x - lane) * P::kNodeWords) &&
-        __lane_id() == 0)
+    bool coll;
+    if constexpr (LaneEmit<P>::value) coll = lane_emit<P>(fits, w, d, a.next + idx * NW);
+    else coll = wave_emit<P>(fits, wrows, (uint64_t)lane, d, a.next + idx * NW, s_nodew + (threadIdx.x - lane) * P::kNodeWords);
+    if (coll && __lane_id() == 0)
       atomicAdd(&a.ctr->err_overflow, 1ull);  // two equal kept sends (see wave_emit)
     __builtin_amdgcn_wave_barrier();  // the rows are overwritten by the next iteration's staging
     MAT_PH(5);
