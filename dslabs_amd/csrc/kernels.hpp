@@ -378,6 +378,11 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
       e[t] = q < n ? Net<P>::at(pw, q) : ~(Rec)0;
       rk[t] = q;
     }
+    // the kept sends, one pass: send i goes to lane q (the next free one) with rank pos = the
+    // elements already placed below it (parents and earlier sends; free lanes hold ~0, never
+    // below), and every placed element above it moves up one -- a later, smaller send then raises
+    // the earlier sends' ranks the same way, so the ranks end as the merged order's slots (one
+    // readlane per kept send and one scalar test per possible send; it was two of each)
     {
       int q = n;
 #pragma unroll
@@ -386,36 +391,23 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
           Rec r;
           if constexpr (sizeof(Rec) == 8) r = (Rec)rl64((uint64_t)d.out.r[i], src);
           else r = (Rec)rl32((uint32_t)d.out.r[i], src);
-#pragma unroll
-          for (int t = 0; t < TR; t++) e[t] = lane + 64 * t == q ? r : e[t];
-          q++;
-        }
-      }
-    }
-    {
-      int j = n;
-#pragma unroll
-      for (int i = 0; i < P::kMaxSends; i++) {
-        if ((keep >> i) & 1u) {
-          Rec r;
-          if constexpr (sizeof(Rec) == 8) r = (Rec)rl64((uint64_t)d.out.r[i], src);
-          else r = (Rec)rl32((uint32_t)d.out.r[i], src);
-          int pos = 0;  // elements below r: its slot (free lanes hold ~0, never below)
+          int pos = 0;
 #pragma unroll
           for (int t = 0; t < TR; t++) pos += __popcll(__ballot(e[t] < r));
-          if constexpr (SendsDistinct<P>::value) {  // r itself is the one element equal to it
+          if constexpr (SendsDistinct<P>::value) {  // an earlier kept send equal to r
             int eq = 0;
 #pragma unroll
-            for (int t = 0; t < TR; t++) eq += __popcll(__ballot(e[t] == r));
-            collision |= eq != 1;
+            for (int t = 0; t < TR; t++) eq += __popcll(__ballot(lane + 64 * t < q && e[t] == r));
+            collision |= eq != 0;
           }
 #pragma unroll
           for (int t = 0; t < TR; t++) {
-            const int q = lane + 64 * t;
-            rk[t] += (q < n && r < e[t]) ? 1 : 0;
-            rk[t] = q == j ? pos : rk[t];
+            const int x = lane + 64 * t;
+            rk[t] += (x < q && r < e[t]) ? 1 : 0;
+            rk[t] = x == q ? pos : rk[t];
+            e[t] = x == q ? r : e[t];
           }
-          j++;
+          q++;
         }
       }
     }
