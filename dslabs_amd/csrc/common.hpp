@@ -73,6 +73,17 @@ struct DevSettings {
   }
 };
 
+// True when no active lane of the wavefront has `p` (device; one thread on the host): the exit of
+// a fixed-trip loop over a per-lane list once every lane is past its end (the unrolled iterations
+// after it would each still pay their exec-mask test and branch).
+DSL_HD bool wave_none(bool p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __ballot(p) == 0ull;
+#else
+  return !p;
+#endif
+}
+
 DSL_HD bool should_deliver(const DevSettings& s, int from, int to) {
   return (s.deliver[from] >> to) & 1u;
 }

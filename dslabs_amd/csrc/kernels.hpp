@@ -387,6 +387,7 @@ __device__ __forceinline__ bool wave_emit(bool active, const uint32_t* base, uin
       int q = n;
 #pragma unroll
       for (int i = 0; i < P::kMaxSends; i++) {  // constant indices: the send list stays in VGPRs
+        if ((keep >> i) == 0u) break;  // no kept send left (sends are kept mostly from the front)
         if ((keep >> i) & 1u) {
           Rec r;
           if constexpr (sizeof(Rec) == 8) r = (Rec)rl64((uint64_t)d.out.r[i], src);

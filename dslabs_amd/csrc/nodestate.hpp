@@ -353,8 +353,10 @@ DSL_HD void canon_sends(const uint32_t* w, Delta<P>& d) {
   uint32_t keep = 0;
   const int nr = Net<P>::size(w);
 #pragma unroll
-  for (int i = 0; i < K; i++)
+  for (int i = 0; i < K; i++) {
+    if (wave_none(i < n)) break;
     if (i < n && !net_contains_fixed<P>(w, nr, d.out.r[i])) keep |= 1u << i;
+  }
   d.keep = keep;
 }
 
@@ -408,8 +410,10 @@ DSL_HD Fp delta_fingerprint(const uint32_t* w, Fp parent, const Delta<P>& d) {
   Fp f = fp_xor(parent, node_hash<P>(d.node, w + d.node * P::kNodeWords));
   f = fp_xor(f, node_hash<P>(d.node, d.nw));
 #pragma unroll
-  for (int j = 0; j < P::kMaxSends; j++)
+  for (int j = 0; j < P::kMaxSends; j++) {
+    if (wave_none((d.keep >> j) != 0u)) break;
     if ((d.keep >> j) & 1u) f = fp_xor(f, msg_hash<P>(d.out.r[j]));  // the records new to the set
+  }
   return f;
 }
 
@@ -419,8 +423,10 @@ template <class P>
 DSL_HD Fp delta_fingerprint_cached(Fp parent_without_node, const Delta<P>& d) {
   Fp f = fp_xor(parent_without_node, node_hash<P>(d.node, d.nw));
 #pragma unroll
-  for (int j = 0; j < P::kMaxSends; j++)
+  for (int j = 0; j < P::kMaxSends; j++) {
+    if (wave_none((d.keep >> j) != 0u)) break;
     if ((d.keep >> j) & 1u) f = fp_xor(f, msg_hash<P>(d.out.r[j]));
+  }
   return f;
 }
 
@@ -434,6 +440,7 @@ DSL_HD int delta_event_count(const uint32_t* w, int parent_events, const Delta<P
     n += P::num_timer_events(d.node, d.nw, prm) - P::num_timer_events(d.node, w + d.node * P::kNodeWords, prm);
 #pragma unroll
   for (int j = 0; j < P::kMaxSends; j++) {  // the records new to the set
+    if (wave_none((d.keep >> j) != 0u)) break;
     if ((d.keep >> j) & 1u) {
       const auto r = d.out.r[j];
       if (set.all_deliver || should_deliver(set, P::rec_from(r), P::rec_to(r))) n++;
