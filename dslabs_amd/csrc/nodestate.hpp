@@ -125,7 +125,10 @@ struct Sender {
     r[0] = x;
 #else
 #pragma unroll
-    for (int i = 0; i < K; i++) r[i] = keep_value(i == n ? x : r[i]);
+    for (int i = 0; i < K; i++) {
+      if (wave_none(i <= n)) break;  // every sending lane's slot is behind
+      r[i] = keep_value(i == n ? x : r[i]);
+    }
 #endif
     n++;
   }
