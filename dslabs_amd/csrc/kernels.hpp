@@ -1084,7 +1084,12 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
                   view.sends = ms;
                   view.nsends = dn;
                 }
+#ifdef DSL_X0_JUDGE  // cost probe (measurement builds): no judge (every new state VALID below maxDepth)
+                const int v = set.max_depth >= 0 && a.depth >= set.max_depth ? V_PRUNED : V_VALID;
+                (void)view;
+#else
                 const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
+#endif
                 if (v == V_VALID) {
                   if (route) {
                   } else if (Net<P>::size(w) + dn <= P::kNetCap) {
