@@ -261,6 +261,9 @@ def main():
     ap.add_argument("--workload", default="multipaxos")
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # N > 1: the engine's replicated-or-sharded rule (Engine replicate_below): -1 = the cost model
+    # (default), 0 = every level hash-sharded (tests), n > 0 = shard frontiers of at least n states
+    ap.add_argument("--replicate-below", type=int, default=-1)
     args = ap.parse_args()
 
     import torch
@@ -270,33 +273,33 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # DSL_BENCH_SHARE_DEVICE=1 (rehearsal on a one-GPU box, never a bench line): every rank on
-    # device 0, torch's own group over gloo; the engine's RCCL communicator is the one under test
+    # device 0 over gloo. RCCL refuses two ranks on one device, so the engine's transport is the
+    # caller's (TorchHostComm) with DSL_HOST_COMM_DEVICE_COLLECTIVES: the engine takes the same
+    # device-collective branches as with its RCCL communicator (level records gathered on the
+    # device), each gather emulated by a device->host copy, the gloo allgather and a copy back
     share = os.environ.get("DSL_BENCH_SHARE_DEVICE") == "1"
     device = 0 if share else local_rank
     torch.cuda.set_device(device)
     dist = None
     comm_id = None
+    host_comm = None
     if world > 1:
         import torch.distributed as dist
         if share:
             dist.init_process_group("gloo")
+            from dslabs_amd.distributed import TorchHostComm
+            host_comm = TorchHostComm(device_collectives=True)
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        from dslabs_amd import _lib
-        lib = _lib.load()
-        import ctypes
-        buf = (ctypes.c_uint8 * 128)()
-        if rank == 0:
-            _lib.check(lib.dsl_comm_unique_id(buf), "dsl_comm_unique_id")
-        obj = [bytes(buf)]
-        dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
+            from dslabs_amd.distributed import broadcast_comm_id
+            comm_id = broadcast_comm_id(rank)
 
     from dslabs_amd import Engine
     wl = WORKLOADS[args.workload]
     depth = args.depth if args.depth is not None else wl["depth"]
     proto, settings, oracle_args = build_search(args.workload, depth)
-    eng = Engine(proto, device=device, rank=rank, world_size=world, comm_id=comm_id)
+    eng = Engine(proto, device=device, rank=rank, world_size=world, comm_id=comm_id, host_comm=host_comm,
+                 replicate_below=args.replicate_below)
     # C4 starts from PrimaryBackupTest.initView's prepared state (PrimaryBackupTest.java:124-187)
     state = proto.initView(2, "server1", "server2", "client1", device=device) if args.workload == "pb" \
         else proto.initial_state()
@@ -322,6 +325,13 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = eng.kernel_stats()
+    per_rank = None
+    if dist is not None:  # every rank's share of the last search (load balance of the shards)
+        mine = {k: stats[k] for k in ("parents", "work_items", "new_states", "exchanged", "probes")}
+        mine["expand_ms"] = round(stats["expand_ms"], 4)
+        mine["exchange_ms"] = round(stats["exchange_ms"], 4)
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
     if rank == 0:
         line = {
             "metric": metric_name(args.workload),
@@ -343,6 +353,15 @@ def main():
                        "successors_per_step": res.successors, "parallelism": f"hash-sharded x{world}"},
             "roofline": roofline(stats, args.workload, depth),
         }
+        if world > 1:  # the last search's sharding bookkeeping (dsl_stats), rank 0's view
+            line["sharding"] = {
+                "transport": "gloo host comm, device-collective branches (one-GPU rehearsal)" if share
+                else f"RCCL {stats['rccl_version']}",
+                "elapsed_s_max_over_ranks": elapsed,
+                **{k: stats[k] for k in ("sharded_levels", "fast_levels", "completions", "host_syncs",
+                                         "exchange_rounds", "exchanged", "shard_work_min")},
+                "cost_c_ns": round(stats["cost_c_ns"], 4), "cost_x_us": round(stats["cost_x_us"], 2),
+                "exchanged_all_ranks": sum(r["exchanged"] for r in per_rank), "per_rank": per_rank}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(proto, settings, min(depth, wl.get("cpu_mt_depth", depth)) if depth >= 0
                                                 else depth, res.per_depth, oracle_args, wl["cpu_depth"], state)

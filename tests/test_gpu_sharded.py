@@ -122,6 +122,43 @@ def test_multiprocess_sharded_completion_c5(world, slab_max):
         assert r["completions"] > 0, r
 
 
+@pytest.mark.parametrize("rep", [0, -1])
+def test_bench_multi_gpu_branch_share_device(rep):
+    """bench.py's N > 1 branch end to end before the driver's 8-GPU run: torch.distributed.run
+    starts 2 ranks of `bench.py --gpus 2` on the one GPU (DSL_BENCH_SHARE_DEVICE=1: gloo, the engine
+    on the caller transport with its device-collective branches -- RCCL refuses two ranks on one
+    device). Rank 0 prints the one JSON line: 2 GPUs, hash-sharded, per-depth counts equal C5 d12's
+    golden vector, value = states x steps / the max-over-ranks time. rep 0: every level sharded,
+    each on the one-round-trip fast path; rep -1: the cost model's choice (the driver's default)."""
+    import subprocess
+    import sys
+    from test_distributed import _free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DSL_BENCH_SHARE_DEVICE="1")
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", "--replicate-below", str(rep)],
+                       cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    b = json.loads(lines[0])
+    assert b["n_gpus"] == 2 and b["steps"] == 3
+    assert b["config"]["parallelism"] == "hash-sharded x2"
+    assert b["config"]["per_depth"] == MPX["mp_c5_d12"]["per_depth"]
+    assert "cpu_baseline" not in b
+    sh = b["sharding"]
+    want = b["config"]["unique_states_per_step"] * 3 / sh["elapsed_s_max_over_ranks"]
+    assert abs(b["value"] - want) <= 1e-6 * want + 0.1  # value = round(., 1)
+    assert sh["completions"] == 0
+    if rep == 0:
+        assert sh["sharded_levels"] == 12 and sh["fast_levels"] == 12, sh
+        assert sh["exchanged_all_ranks"] > 0 and len(sh["per_rank"]) == 2
+        assert sh["host_syncs"] <= sh["sharded_levels"] + 1, sh
+        assert sh["exchange_rounds"] == 2 * sh["sharded_levels"] - 1, sh
+
+
 def test_rccl_engine_at_world_1():
     """make_comm / ncclCommInitRank / ncclGetVersion and the RcclComm collectives run once on a
     one-GPU box: a world-size-1 engine with its RCCL communicator (DSL_CFG_RCCL_AT_WORLD_1) runs
