@@ -4,6 +4,7 @@ import dslabs.framework.testing.Event;
 import dslabs.framework.testing.MessageEnvelope;
 import dslabs.framework.testing.StatePredicate;
 import dslabs.framework.testing.StatePredicate.PredicateResult;
+import dslabs.framework.testing.utils.GlobalSettings;
 import dslabs.framework.testing.search.SearchResults.EndCondition;
 import dslabs.framework.testing.search.gpu.Dsl;
 import dslabs.framework.testing.search.gpu.GpuPredicates;
@@ -37,6 +38,11 @@ public final class GpuBFS {
   public static SearchResults bfs(SearchState init, SearchSettings settings) {
     if (settings == null) settings = new SearchSettings();
     if (!Dsl.deviceAvailable()) return Search.bfs(init, settings);
+    // GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220) re-step every explored state
+    // and report each offending event with its starting SearchState through CheckLogger; that
+    // state is a Java object the device never holds, so a checked run keeps the JVM search (the
+    // engine's own sampled checks, dsl_settings.do_checks, are for its tests and the C ABI)
+    if (GlobalSettings.doErrorChecks()) return Search.bfs(init, settings);
     List<SearchState> chain = new ArrayList<>();
     init.trace().forEach(chain::add);
     GpuProtocols.Desc desc = GpuProtocols.describe(chain.get(0));

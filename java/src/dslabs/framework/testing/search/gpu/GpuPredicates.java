@@ -5,7 +5,6 @@ import dslabs.framework.Message;
 import dslabs.framework.testing.MessageEnvelope;
 import dslabs.framework.testing.StatePredicate;
 import dslabs.framework.testing.search.SearchSettings;
-import dslabs.framework.testing.utils.GlobalSettings;
 import java.lang.foreign.Arena;
 import java.lang.foreign.MemorySegment;
 import java.lang.foreign.ValueLayout;
@@ -74,9 +73,9 @@ public final class GpuPredicates {
     if (pool.size() > Dsl.MAX_POOL) return null;
     m.set(ValueLayout.JAVA_INT, Dsl.OFF_N_POOL, pool.size());
     m.set(ValueLayout.JAVA_INT, Dsl.OFF_TABLE_LOG2, 0);  // automatic
-    // GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220): re-checked on a sample per level
-    m.set(ValueLayout.JAVA_INT, Dsl.OFF_DO_CHECKS, GlobalSettings.doAllChecks() ? Dsl.CHECKS_ALL
-        : GlobalSettings.doErrorChecks() ? Dsl.CHECKS_ERRORS : Dsl.CHECKS_NONE);
+    // GlobalSettings checks (Search.java:201-220) keep the JVM search (GpuBFS.bfs): the device's
+    // sampled checks could count offending events but not hand CheckLogger their Java states
+    m.set(ValueLayout.JAVA_INT, Dsl.OFF_DO_CHECKS, Dsl.CHECKS_NONE);
     m.set(ValueLayout.JAVA_INT, Dsl.OFF_CHECK_SAMPLE, 0);
     return m;
   }

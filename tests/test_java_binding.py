@@ -383,3 +383,17 @@ def test_java_kvstore_types_are_the_reference_lombok_declarations():
                 seen += 1
             assert "String toString()" not in text, f
     assert seen >= 12, seen
+
+
+def test_java_error_checks_keep_the_jvm_search():
+    """GlobalSettings.doErrorChecks / doAllChecks (Search.java:201-220) report every
+    offending event with its starting Java SearchState through CheckLogger, which the device cannot
+    supply; so a checked run keeps the JVM search (before any engine is created), and the encoder
+    never turns the device's sampled checks on (their counts would be dropped)."""
+    bfs = open(os.path.join(JAVA, "GpuBFS.java")).read()
+    i = bfs.index("public static SearchResults bfs(")
+    body = bfs[i:bfs.index("new Dsl.Engine(", i)]
+    assert "if (GlobalSettings.doErrorChecks()) return Search.bfs(init, settings);" in body
+    enc = open(os.path.join(JAVA, "gpu", "GpuPredicates.java")).read()
+    assert "m.set(ValueLayout.JAVA_INT, Dsl.OFF_DO_CHECKS, Dsl.CHECKS_NONE);" in enc
+    assert "doAllChecks()" not in enc and "doErrorChecks()" not in enc
