@@ -561,7 +561,7 @@ struct BfsEngine : EngineBase {
     if (hset.max_time_ms > 0 && q_ms_per_level > 0)
       nq = std::max(1, std::min(nq, (int)((hset.max_time_ms - elapsed_ms) / q_ms_per_level)));
     const uint64_t flimit = queue_flimit(span), wlimit = queue_wlimit(span);
-    const uint64_t room = table_room_queue();
+    const uint64_t room = table_room_queue(), room_half = table_room();
     uint64_t used = 0;  // rows of the current frontier that must be kept
     for (size_t q = 0; q < S.seg_cnt.size(); q++) used = std::max(used, S.seg_base[q] + S.seg_cnt[q]);
     DSL_TRY(grow_rows(&S.cur, &S.cur_cap, std::max(span, used), true, used));
@@ -598,6 +598,7 @@ struct BfsEngine : EngineBase {
       a.qflimit = flimit;
       a.qwlimit = wlimit;
       a.qroom = room;
+      a.qroom_half = room_half;
       a.qspread = spread;
       a.t0_rt = t0_rt;
       a.budget_rt = level_budget(W > 1);
@@ -655,7 +656,7 @@ struct BfsEngine : EngineBase {
         std::memcpy(&v, set + kCtrSegOff + (size_t)q * kSegStride * 8, 8);
         F += std::min<uint64_t>(v, q_segcap);
       }
-      if (!queue_continues(c, F, flimit, wlimit, room)) {
+      if (!queue_continues(c, F, flimit, wlimit, room, room_half)) {
         *ran = j + 1;
         break;
       }
@@ -673,9 +674,9 @@ struct BfsEngine : EngineBase {
   // probes still ran out of room (an estimate far off) makes the search restart with a larger
   // first table (run). The table never shrinks: a repeated search starts at the size reached.
   uint64_t table_room() const { return tbl.bucket_mask * 4 + 4 > inserted ? tbl.bucket_mask * 4 + 4 - inserted : 0; }
-  // The queue's room (queue_continues checks twice the estimate against it): up to 3/4 of the
-  // slots, so a level whose new / work ratio doubles against the estimate still probes a table at
-  // most 3/4 full, while a level that keeps to the estimate stays under the half-full rule.
+  // The queue's second room (queue_continues: twice the estimate, beside the estimate against
+  // table_room's half-full rule): up to 3/4 of the slots, so a level whose new / work ratio doubles
+  // against the estimate still probes a table at most 3/4 full.
   uint64_t table_room_queue() const {
     const uint64_t cap = (tbl.bucket_mask + 1) * 6;
     return cap > inserted ? cap - inserted : 0;
@@ -1313,6 +1314,11 @@ struct BfsEngine : EngineBase {
   // delivered message is also delivered again to the successor (it stays in the network, a set),
   // which must give the successor back: CheckLogger.notIdempotent (:114-121, "not necessarily an
   // error"). The first offending event of each kind is kept (decoded at its parent).
+  // Scope: the sample is drawn from the level's device ROWS, i.e. its VALID new states. Pruned and
+  // terminal successors, and every state of the maxDepth level, are never written as rows, so there
+  // is no device result to compare them with (the reference checks every non-terminal state before
+  // its prune test, Search.java:201-220); the handlers that produce them are the same code. A
+  // multi-rank search sums the counts over the ranks (allreduce at the end of run_once).
   uint64_t chk_run = 0, chk_nd = 0, chk_ni = 0;
   dsl_event chk_first_nd{}, chk_first_ni{};
   // equal packed states: the header words and the records below the count (a device row's slots
@@ -2116,6 +2122,15 @@ struct BfsEngine : EngineBase {
       q_span_want = std::max(q_span_want, want);
     }
     stats.exchanged = exchanged;
+    if (comm && hset.do_checks != DSL_CHECKS_NONE) {
+      // every rank checked a sample of its own shards' rows: the result carries the sums (the first
+      // offending event of each kind stays the one this rank found, if any)
+      uint64_t cv[3] = {chk_run, chk_nd, chk_ni};
+      DSL_TRY((stats.host_syncs++, comm->allreduce_u64(cv, 3, false, stream)));
+      chk_run = cv[0];
+      chk_nd = cv[1];
+      chk_ni = cv[2];
+    }
     const double elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count();
     dsl_result* r = (dsl_result*)calloc(1, sizeof(dsl_result));
     r->end_condition = end;

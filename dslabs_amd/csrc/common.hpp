@@ -38,6 +38,7 @@ constexpr int32_t kOpAnd = -1, kOpOr = -2, kOpNot = -3;
 constexpr uint32_t kReadsAll = 0xffffffffu;
 constexpr int kMaxProgOps = 64;   // ops of all the programs of one search
 constexpr int kMaxProgStack = 16;  // values on a program's stack (2 bits each in one word)
+constexpr int kFlatUnroll = 4;     // leaves judge_view unrolls on a flat program list
 
 // A top-level predicate (an invariant, goal or prune): ops [start, start + len) of the pool.
 struct DevProg {
@@ -53,6 +54,11 @@ struct DevSettings {
   int32_t all_deliver;  // every (from, to) pair of the protocol's nodes delivers
   int32_t max_depth;
   int32_t n_inv, n_goal, n_prune, n_ops;
+  // 1: every program is a single leaf (no combinator), so ops[t] is program t in checkState order
+  // -- invariants, goals, prunes (resolve_settings emits them in that order); judge_view then walks
+  // the leaves directly (no program descriptors, no stack)
+  int32_t flat;
+  int32_t pad_flat;
   DevProg inv[DSL_MAX_PREDICATES];
   DevProg goal[DSL_MAX_PREDICATES];
   DevProg prune[DSL_MAX_PREDICATES];

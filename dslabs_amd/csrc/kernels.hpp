@@ -542,8 +542,8 @@ struct LevelArgs {
   const LevelCounters* qprev;        // null: the table is `segs`
   const unsigned long long* qprev_seg;
   uint64_t qflimit, qwlimit;         // the queue stops above these frontier / work sizes
-  uint64_t qroom;                    // ... and before a level whose estimated new states would
-                                     // take the visited table past half full (table_room)
+  uint64_t qroom;                    // ... and before a level whose estimated new states would take
+  uint64_t qroom_half;               // the table past half full, or twice them past 3/4 of its slots
   int32_t qspread;                   // resident workgroups (BfsEngine::level_slots): a level of at most
                                      // this many chunks is one round; queued: pb = balanced_chunk(F, PB, qspread)
   uint32_t term_cap;                 // TerminalRec entries of `terms`
@@ -587,18 +587,19 @@ __host__ __device__ inline uint64_t est_new_states(uint64_t work, uint64_t prev_
 }
 
 // The queue's stop rule: after a level with any of these, the host must act before the next one.
-// `room`: the visited table's headroom (states, up to 3/4 of its slots: BfsEngine::table_room_queue)
-// when the queue started; the next level runs only if the queue's inserted states so far plus
-// TWICE its estimate fit (the host grows the table first): the estimate assumes the new / work
-// ratio does not rise, and a level that overfills the table restarts the whole search with a
-// larger one, so the queue, which runs up to twelve levels without the host, keeps
-// a doubled level within 3/4 of the slots.
+// The visited table's headroom when the queue started (BfsEngine::table_room / table_room_queue):
+// the next level runs only if the queue's inserted states so far plus its estimate keep the table
+// at most half full -- the rule ensure_table applies between unqueued levels -- AND plus TWICE the
+// estimate at most 3/4 full: the estimate assumes the new / work ratio does not rise, and a level
+// that overfills the table restarts the whole search with a larger one, so the queue,
+// which runs up to twelve levels without the host, stays within 3/4 even when a level doubles.
 __host__ __device__ inline bool queue_continues(const LevelCounters& c, uint64_t F, uint64_t flimit,
-                                                uint64_t wlimit, uint64_t room) {
+                                                uint64_t wlimit, uint64_t room34, uint64_t room_half) {
+  const uint64_t est = est_new_states(c.next_work, c.new_states, c.work_items);
   return !(c.spilled | c.n_terminals | c.err_overflow | c.err_table | c.err_frontier | c.time_up) && F > 0 &&
          F <= flimit &&
          c.next_work <= wlimit &&
-         c.cum_before + c.new_states + 2 * est_new_states(c.next_work, c.new_states, c.work_items) <= room;
+         c.cum_before + c.new_states + 2 * est <= room34 && c.cum_before + c.new_states + est <= room_half;
 }
 
 // Copies n16 16-byte units from global memory to LDS with LDS-DMA: wave w issues units
@@ -721,7 +722,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   constexpr int NWAVE = kLevelBlock / 64;
   // handler classes: messages, timers, then the events whose handler surely changes nothing
   // (NoopFilter: counted as successors and never run; they sort last and the passes stop before them)
-  constexpr int NC = P::kMsgClasses + 2;
+  constexpr int NC = Classes<P>::kCount;
   static_assert(P::kNodes * 256 < 32768 && P::kNetCap < 32768, "a located event fits s_ev's 16 bits");
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                           // a.PB (max) rows, stride SP
@@ -783,7 +784,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         s_segs.n = a.nseg;
         s_segs.pb = pb;
         s_segs.chunk0[0] = 0;
-        s_stop = queue_continues(*a.qprev, F, a.qflimit, a.qwlimit, a.qroom) ? 0 : 1;
+        s_stop = queue_continues(*a.qprev, F, a.qflimit, a.qwlimit, a.qroom, a.qroom_half) ? 0 : 1;
       }
     }
   } else {
@@ -883,7 +884,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     for (int w0 = 0; w0 < total; w0 += kWin) {
       const int wn = min(kWin, total - w0);
       // 3a. (parent, handler class) of every item of the window: a team of TPP threads per
-      //     parent writes its events' entries (no search, no atomics)
+      //     parent writes its events' entries (no search, no atomics). (Measured: one thread per
+      //     item -- a binary search for the first item's parent, then runs of ceil(wn / 256) items
+      //     -- was 3 % slower on C5 d12, profiles/r06_classify_ab.txt.)
       {
         const int tpp = pb > 128 ? 1 : pb > 64 ? 2 : pb > 32 ? 4 : pb > 16 ? 8 : pb > 8 ? 16 : 32;
         const int j = tid / tpp, sub = tid - j * tpp;

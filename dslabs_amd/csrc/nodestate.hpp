@@ -266,13 +266,26 @@ DSL_HD int locate_event(const uint32_t* w, const typename P::Params& prm, const 
   return INT32_MIN;
 }
 
-// Handler class of event k (messages: P::msg_class < P::kMsgClasses, timers: P::kMsgClasses).
+// Handler classes (k_level sorts a chunk's work items by class, so a wavefront mostly runs one
+// handler): messages [0, kMsgClasses) by P::msg_class; timers from kMsgClasses on, one class, or
+// TimerClasses<P> of them when the protocol splits its timer handlers by node kind
+// (P::kTimerClasses + P::timer_class(node): Multi-Paxos's server Tick and client ClientTimer,
+// which a wave of mixed timer items would otherwise both run); last the skip class (NoopFilter).
+template <class P, class = void>
+struct TimerClasses : std::integral_constant<int, 1> {
+  static DSL_HD int of(int, const typename P::Params&) { return 0; }
+};
 template <class P>
-DSL_HD int event_class(const uint32_t* w, const typename P::Params& prm, const DevSettings& set, int k) {
-  static_assert(P::kMsgClasses >= 1 && P::kMsgClasses < 15, "at most 14 message classes + the timer and skip classes");
-  const int e = locate_event<P>(w, prm, set, k);
-  return e >= 0 ? P::msg_class(Net<P>::at(w, e)) : P::kMsgClasses;
-}
+struct TimerClasses<P, std::void_t<decltype(P::kTimerClasses)>> : std::integral_constant<int, P::kTimerClasses> {
+  static DSL_HD int of(int node, const typename P::Params& prm) { return P::timer_class(node, prm); }
+};
+template <class P>
+struct Classes {
+  static constexpr int kTimer0 = P::kMsgClasses;
+  static constexpr int kSkip = P::kMsgClasses + TimerClasses<P>::value;
+  static constexpr int kCount = kSkip + 1;
+  static_assert(P::kMsgClasses >= 1 && kCount <= 16, "at most 16 handler classes, the skip class included");
+};
 
 // Events whose handler surely changes nothing: a protocol may provide
 //   static bool surely_noop(int node, const uint32_t* w, Rec r, const Params&)
@@ -281,7 +294,7 @@ DSL_HD int event_class(const uint32_t* w, const typename P::Params& prm, const D
 // node's words unchanged and every send already in the network (the successor is the parent;
 // `false` whenever unsure). k_level counts such an event as a successor (Search.java:481-485: it
 // is generated, then found in the visited set) without running its handler; tests/hostcheck
-// checks the implication on every explored event. event_class_skip returns kMsgClasses + 1 for them.
+// checks the implication on every explored event. event_class_skip returns Classes<P>::kSkip for them.
 template <class P, class = void>
 struct NoopFilter {
   static DSL_HD bool msg(int, const uint32_t*, typename P::Rec, const typename P::Params&) { return false; }
@@ -309,13 +322,14 @@ DSL_HD int event_class_skip(const uint32_t* w, const typename P::Params& prm, co
   const int e = locate_event<P>(w, prm, set, k);
   if (located) *located = e;  // k_level keeps it for delta_step_located (no second walk)
   if (e < 0) {
-    if (e == INT32_MIN) return P::kMsgClasses;
+    if (e == INT32_MIN) return Classes<P>::kTimer0;
     const int x = -1 - e;
-    return NoopTimerFilter<P>::timer(x >> 8, w, x & 255, prm) ? P::kMsgClasses + 1 : P::kMsgClasses;
+    return NoopTimerFilter<P>::timer(x >> 8, w, x & 255, prm) ? Classes<P>::kSkip
+                                                                : Classes<P>::kTimer0 + TimerClasses<P>::of(x >> 8, prm);
   }
   const auto r = Net<P>::at(w, e);
   const int i = P::rec_to(r);
-  if (i < P::num_nodes(prm) && NoopFilter<P>::msg(i, w, r, prm)) return P::kMsgClasses + 1;
+  if (i < P::num_nodes(prm) && NoopFilter<P>::msg(i, w, r, prm)) return Classes<P>::kSkip;
   return P::msg_class(r);
 }
 
@@ -632,6 +646,62 @@ DSL_HD Verdict judge_view(const NodeView& v0, const typename P::Params& prm, con
     v.ndropped = set.n_dropped;
   }
   const int ng = set.n_inv + set.n_goal, nt = ng + set.n_prune;
+#ifdef DSL_NO_FLAT  // measurement variant: the program interpreter for every predicate list
+  if (false) {
+#else
+  if (set.flat) {
+#endif
+    // every program is one leaf (resolve_settings): program t IS ops[t], in checkState order
+    // (invariants, goals, prunes) -- no program descriptors, no stack machine
+#ifdef DSL_FLAT_UNROLL
+#pragma unroll
+    for (int t = 0; t < kFlatUnroll; t++) {
+      if (t >= nt) break;
+#else
+    for (int t = 0; t < nt; t++) {
+#endif
+      const DevPred& op = set.ops[t];
+      if (incremental && v.changed >= 0 && leaf_unchanged<P>(op, v)) continue;
+      int x = P::eval(op, v, prm);
+      if (x != PV_THREW && op.negate) x = !x;
+      if (t < set.n_inv) {
+        if (x != PV_TRUE) {  // a false or throwing invariant is violated
+          *pred_index = t;
+          return V_TERM_INVARIANT;
+        }
+      } else if (t < ng) {
+        if (x == PV_TRUE) {  // throwing goals are ignored
+          *pred_index = t - set.n_inv;
+          return V_TERM_GOAL;
+        }
+      } else if (x != PV_FALSE) {
+        return V_PRUNED;  // true or throwing
+      }
+    }
+#ifdef DSL_FLAT_UNROLL
+    for (int t = kFlatUnroll; t < nt; t++) {
+      const DevPred& op = set.ops[t];
+      if (incremental && v.changed >= 0 && leaf_unchanged<P>(op, v)) continue;
+      int x = P::eval(op, v, prm);
+      if (x != PV_THREW && op.negate) x = !x;
+      if (t < set.n_inv) {
+        if (x != PV_TRUE) {
+          *pred_index = t;
+          return V_TERM_INVARIANT;
+        }
+      } else if (t < ng) {
+        if (x == PV_TRUE) {
+          *pred_index = t - set.n_inv;
+          return V_TERM_GOAL;
+        }
+      } else if (x != PV_FALSE) {
+        return V_PRUNED;
+      }
+    }
+#endif
+    if (set.max_depth >= 0 && depth >= set.max_depth) return V_PRUNED;
+    return V_VALID;
+  }
   for (int t = 0; t < nt; t++) {
     const int kind = t < set.n_inv ? 0 : t < ng ? 1 : 2;
     const int i = kind == 0 ? t : kind == 1 ? t - set.n_inv : t - ng;

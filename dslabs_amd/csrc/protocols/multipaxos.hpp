@@ -43,7 +43,7 @@ struct MultiPaxos {
   // other servers for each of the 4 slots, plus up to 4 replies from execute); a larger send
   // list would be a hard STEP_OVERFLOW error, never a truncation.
   static constexpr int kNodes = kMaxServers + kMaxClients, kNodeWords = 6, kNetCap = 64, kMaxSends = 12;
-  static constexpr int kMsgClasses = 8;  // handler classes of messages (message types 0..7); timers: class 8
+  static constexpr int kMsgClasses = 8;  // handler classes of messages (message types 0..7); timers: 8 (Tick), 9 (ClientTimer)
   // No handler sends one record twice in one step (broadcasts go to distinct servers, execute
   // replies once per newly executed command, become_leader proposes each slot once), so Sender
   // skips its duplicate check; tests/hostcheck checks distinctness on every explored step.
@@ -73,6 +73,9 @@ struct MultiPaxos {
   // Handler class of a message (< kMsgClasses; timers are class kMsgClasses): k_level groups a chunk's work items
   // by class so that the lanes of a wavefront run the same handler.
   static DSL_HD int msg_class(Rec r) { return m_type(r); }
+  // Timer handler classes: a server's Tick and a client's ClientTimer (nodestate.hpp TimerClasses)
+  static constexpr int kTimerClasses = 2;
+  static DSL_HD int timer_class(int node, const Params& p) { return node >= p.servers ? 1 : 0; }
   static DSL_HD int get(const uint32_t* w, int bit, int width) { return field_get<kNodeWords>(w, bit, width); }
   static DSL_HD void put(uint32_t* w, int bit, int width, int v) { field_put<kNodeWords>(w, bit, width, v); }
   // ---- server fields ------------------------------------------------------------------------------

@@ -87,6 +87,7 @@ inline int resolve_settings(const dsl_settings& in, int num_nodes, bool (*known)
     *why_out = why;
     return why.rfind("predicate not supported", 0) == 0 ? DSL_ERR_UNKNOWN_PREDICATE : DSL_ERR_ARG;
   }
+  d.flat = d.n_ops == d.n_inv + d.n_goal + d.n_prune ? 1 : 0;  // one leaf per program
   *out = d;
   return DSL_OK;
 }

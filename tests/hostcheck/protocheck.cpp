@@ -107,7 +107,7 @@ static int run(const dsl_protocol_desc& d, DevSettings set) {
     for (int k = 0; k < ne; k++) {
       Delta<P> dl;
       const int rc = delta_step<P>(n.s.w, k, dl, prm, set);
-      if (event_class_skip<P>(n.s.w, prm, set, k) == P::kMsgClasses + 1) {  // the kernels skip its handler
+      if (event_class_skip<P>(n.s.w, prm, set, k) == Classes<P>::kSkip) {  // the kernels skip its handler
         skipped++;
         if (rc != STEP_OK || dl.keep != 0 || !same_words<P::kNodeWords>(dl.nw, n.s.w + dl.node * P::kNodeWords))
           skip_mismatch++;

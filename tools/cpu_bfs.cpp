@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <unordered_set>
 #include <vector>
 
 #include "../dslabs_amd/csrc/protocols/all.hpp"
@@ -122,10 +123,16 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
     std::atomic<unsigned long long> level_new{0};
     std::atomic<int> level_best{99};
     std::atomic<int> level_err{0};
-    constexpr uint64_t kChunk = 64;
+    // DSL_CPU_CHUNK_CENSUS=PB: chunks of PB consecutive frontier rows (k_level's chunk), and per
+    // level the probed successors whose fingerprint an earlier successor of the SAME chunk already
+    // had (diamonds among sibling parents: what an in-chunk LDS dedup would take off the global
+    // probes), to stderr
+    static const uint64_t chunk_census = getenv("DSL_CPU_CHUNK_CENSUS") ? strtoull(getenv("DSL_CPU_CHUNK_CENSUS"), nullptr, 10) : 0;
+    const uint64_t kChunk = chunk_census ? chunk_census : 64;
+    std::atomic<unsigned long long> cc_probed{0}, cc_dup{0};
     // DSL_CPU_CENSUS: per handler class (event_class_skip), events / filtered as surely no-op /
     // run but no-op / probed / new (a measurement of the no-op filter's reach, to stderr)
-    constexpr int NC = P::kMsgClasses + 2;
+    constexpr int NC = Classes<P>::kCount;
     static const bool census = getenv("DSL_CPU_CENSUS") != nullptr;
     std::vector<std::array<unsigned long long, 5 * NC>> cen(threads);
     for (auto& c : cen) c.fill(0);
@@ -139,6 +146,7 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
         const uint64_t b = next_i.fetch_add(kChunk, std::memory_order_relaxed);
         if (b >= F) break;
         const uint64_t e = std::min(F, b + kChunk);
+        std::unordered_set<uint64_t> local;
         size_t part = std::upper_bound(start.begin(), start.end(), b) - start.begin() - 1;
         for (uint64_t g = b; g < e; g++) {
           while (g >= start[part + 1]) part++;
@@ -151,14 +159,14 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
               cls = event_class_skip<P>(r.w, prm, set, k);
               // the filtered events' real class (the handler a skipped event would have run)
               real = cls;
-              if (cls == P::kMsgClasses + 1) {
+              if (cls == Classes<P>::kSkip) {
                 const int e = locate_event<P>(r.w, prm, set, k);
-                real = e < 0 ? P::kMsgClasses : P::msg_class(Net<P>::at(r.w, e));
+                real = e < 0 ? Classes<P>::kTimer0 + TimerClasses<P>::of((-1 - e) >> 8, prm) : P::msg_class(Net<P>::at(r.w, e));
               }
-              cen[t][5 * real + (cls == P::kMsgClasses + 1 ? 1 : 0)]++;
+              cen[t][5 * real + (cls == Classes<P>::kSkip ? 1 : 0)]++;
             }
             const int rc = delta_step<P>(r.w, k, dl, prm, set);
-            if (census && cls != P::kMsgClasses + 1) {
+            if (census && cls != Classes<P>::kSkip) {
               const bool nop = rc == STEP_OK && dl.keep == 0 && same_words<P::kNodeWords>(dl.nw, r.w + dl.node * P::kNodeWords);
               cen[t][5 * real + (nop ? 2 : 3)]++;
             }
@@ -174,6 +182,10 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
             }
             if (dl.keep == 0 && same_words<P::kNodeWords>(dl.nw, r.w + dl.node * P::kNodeWords)) continue;
             const Fp f = delta_fingerprint<P>(r.w, r.fp, dl);
+            if (chunk_census) {
+              cc_probed++;
+              if (!local.insert(f.lo ^ (f.hi * 0x9E3779B97F4A7C15ull)).second) cc_dup++;
+            }
             const int ins = seen.insert(f);
             if (ins < 0) {
               my_err = 2;
@@ -181,7 +193,7 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
             }
             if (ins == 0) continue;
             c_new++;
-            if (census) cen[t][5 * (cls == P::kMsgClasses + 1 ? 0 : cls) + 4]++;
+            if (census) cen[t][5 * (cls == Classes<P>::kSkip ? 0 : cls) + 4]++;
             int pidx = -1;
             NodeView view{r.w, P::kNodeWords, dl.node, dl.nw};
             typename P::Rec news[P::kMaxSends];
@@ -216,6 +228,10 @@ int run(const dsl_protocol_desc& d, const dsl_settings& hs, int threads, int tab
     if (getenv("DSL_CPU_TRACE"))
       fprintf(stderr, "level %d: %llu parents, %.3f ms\n", depth + 1, (unsigned long long)F,
               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt0).count());
+    if (chunk_census)
+      fprintf(stderr, "chunk census level %d (PB %llu): probed %llu, in-chunk duplicates %llu (%.1f %%), new %llu\n", depth + 1,
+              (unsigned long long)chunk_census, cc_probed.load(), cc_dup.load(),
+              cc_probed.load() ? 100.0 * cc_dup.load() / cc_probed.load() : 0.0, level_new.load());
     if (census) {
       fprintf(stderr, "census level %d (class: events filtered run_noop probed new):", depth + 1);
       for (int c = 0; c < NC; c++) {

@@ -1,4 +1,4 @@
-# A/B of library variants (DSL_LIB_VARIANT): VARIANTS="pad0 pad1" beside the product library,
+# A/B of library variants (DSL_LIB_VARIANT): VARIANTS="pad0 pad1" beside the product library (NOPRODUCT=1: without it),
 # $VN alternating rounds of bench.py --no-cpu-baseline $BENCH_ARGS; then, with PMC=1, one
 # LDS-counter pass per variant (SQ_INSTS_LDS, SQ_LDS_BANK_CONFLICT, SQ_WAVE_CYCLES, SQ_WAIT_ANY).
 set -e
@@ -6,8 +6,9 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-var}
 mkdir -p $OUT
+LIST="product $VARIANTS"; [ -n "$NOPRODUCT" ] && LIST="$VARIANTS"
 for i in $(seq 1 ${VN:-2}); do
-  for v in product $VARIANTS; do
+  for v in $LIST; do
     vv=$v; [ "$v" = product ] && vv=""
     DSL_LIB_VARIANT=$vv timeout -k 10 200 python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/$v.$i.json 2>> $OUT/err.log
     python3 -c "import json; a=json.load(open('$OUT/$v.$i.json')); r=a['roofline']; print('%-8s %.4g states/s %.3f ms k=%.4f slots=%s' % ('$v', a['value'], a['ms_per_step'], r['avg_launch_ms'], r.get('level_slots')))"
