@@ -738,7 +738,14 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 #endif
   __shared__ unsigned long long s_red5[NWAVE * 5];
   __shared__ int s_wsum[NWAVE];
+#ifndef DSL_SORT_BALLOT
+  // the window's class counts (LDS atomics in step 3a, each item's rank within its class in s_rnk)
+  __shared__ int s_ccnt[16], s_cbase0[16];
+  __shared__ uint16_t s_rnk[kWin];
+  __shared__ int s_cbase[1][NC];
+#else
   __shared__ int s_cbase[kWin / 64][NC];
+#endif
   __shared__ uint8_t s_par[kWin], s_cls[kWin];
   __shared__ uint16_t s_perm[kWin];
   __shared__ int16_t s_ev[kWin];  // each item's located event (locate_event code; kEvNone: none)
@@ -794,6 +801,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     if (tid == 0) s_stop = 0;
   }
   if (a.budget_rt && tid == 0) s_t0 = *a.t0_rt;
+#ifndef DSL_SORT_BALLOT
+  if (tid < 16) s_ccnt[tid] = 0;
+#endif
   __syncthreads();
   if (s_stop) return;  // an earlier queued level stopped the queue
   PH_MARK(8);  // prologue: the frontier's segment table (+ the queue rule)
@@ -897,13 +907,26 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           for (int q = lo + sub; q < hi; q += tpp) {
             int ev;
             s_par[q - w0] = (uint8_t)j;
+#ifndef DSL_SORT_BALLOT
+            const int cls = event_class_skip<P>(w, prm, set, q - e0, &ev);
+            s_cls[q - w0] = (uint8_t)cls;
+            s_rnk[q - w0] = (uint16_t)atomicAdd(&s_ccnt[cls], 1);
+#else
             s_cls[q - w0] = (uint8_t)event_class_skip<P>(w, prm, set, q - e0, &ev);
+#endif
             s_ev[q - w0] = (int16_t)(ev == INT32_MIN ? kEvNone : ev);
           }
         }
       }
       __syncthreads();
-      // 3b. class counts per 64-item group (ballots), bases in class-major order
+#ifdef DSL_PH_SPLIT_CLS  // phase builds: slot 8 (the prologue's) also takes step 3a, slot 7 only the sort
+      PH_MARK(8);
+#endif
+      // 3b. the window sorted by class: one 64-item group is ranked by wave 0 alone with ballots;
+      //     a larger window by its LDS-atomic class counts (step 3a: each item's rank within its
+      //     class, s_rnk), the class bases by one wave, then one scatter pass -- two barriers and
+      //     no per-group ballots (C5 d12 1.54 -> 1.60e9 states/s, profiles/r06_sort_atomic_ab.txt;
+      //     the per-group ballot sort of rounds 2-5 stays as -DDSL_SORT_BALLOT)
       const int ng = (wn + 63) >> 6;
       if (ng == 1) {
         // one group (every small level): wave 0 sorts it alone, in registers, with one barrier
@@ -925,9 +948,33 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           }
           const int b = __shfl(run, c < 0 ? 0 : c);
           if (lane < wn) s_perm[b + rank] = (uint16_t)lane;
+#ifndef DSL_SORT_BALLOT
+          if (lane < 16) s_ccnt[lane] = 0;
+#endif
         }
         __syncthreads();
       } else {
+#ifndef DSL_SORT_BALLOT
+      // counting sort from the LDS-atomic class counts of step 3a: bases by one wave, then every
+      // item to its class base + its rank (the order within a class is the atomics' order)
+      if (tid < 64) {
+        const int cnt = lane < NC ? s_ccnt[lane] : 0;
+        const int inc = (int)row_incl_sum((uint32_t)cnt);
+        const int run = inc - cnt;
+        if (lane == NC - 1) {  // the skipped events: counted, never run
+          s_weff = run;
+          s_gnext = 0;
+          c_succ += (uint32_t)cnt;
+        }
+        if (lane < 16) {
+          s_cbase0[lane] = run;
+          s_ccnt[lane] = 0;
+        }
+      }
+      __syncthreads();
+      for (int t = tid; t < wn; t += kLevelBlock) s_perm[s_cbase0[s_cls[t]] + s_rnk[t]] = (uint16_t)t;
+      __syncthreads();
+#else
       for (int gr = wid; gr < ng; gr += NWAVE) {
         const int t = gr * 64 + lane;
         const int c = t < wn ? (int)s_cls[t] : -1;
@@ -972,6 +1019,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
         if (t < wn) s_perm[s_cbase[gr][c] + rank] = (uint16_t)t;
       }
       __syncthreads();
+#endif
       }
       PH_MARK(7);  // classify + sort
       const int wrun = s_weff;  // the window's events whose handler runs (a prefix of s_perm)
@@ -1168,8 +1216,12 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const unsigned long long ridx = block_reserve<kLevelBlock>(s_resv, a.rc->out + rc_idx(0, sub), route, dest,
                                                                      a.W, kRouteSegs * kRouteStride);
 #else
-          // by wave: the wave's sub-slab rotates with its passes
-          const int sub = (int)((blockIdx.x * NWAVE + (unsigned)wid + (unsigned)npass++) % kRouteSegs);
+          // by wave: the wave's sub-slab rotates with its passes and with the workgroup, so every
+          // sub-slab takes records of all four waves of many workgroups (blockIdx * 4 + wid gave
+          // sub-slab q only wave q % 4's records: in a one-round level each wave routes its own
+          // share of the class-sorted items, so the sub-slabs of one wave index filled 1.6x the
+          // mean and overflowed into the completion phase)
+          const int sub = (int)((blockIdx.x + (unsigned)wid * (kRouteSegs / NWAVE) + (unsigned)npass++) % kRouteSegs);
           const unsigned long long ridx = wave_reserve_dest(a.rc->out + rc_idx(0, sub), route, dest, a.W,
                                                             kRouteSegs * kRouteStride);
 #endif
