@@ -40,7 +40,7 @@ EXPORTED = [
     "dsl_kernel_stats", "dsl_result_free", "dsl_destroy", "dsl_last_error", "dsl_create_with_host_comm",
     "dsl_run_dfs", "dsl_replay", "dsl_human_readable_trace", "dsl_set_dropped",
 ]
-DSL_ABI_VERSION = 4  # include/dslabs_hip.h; load() refuses a library of another layout
+DSL_ABI_VERSION = 5  # include/dslabs_hip.h; load() refuses a library of another layout
 
 
 class dsl_protocol_desc(ctypes.Structure):
@@ -123,7 +123,8 @@ class dsl_stats(ctypes.Structure):
                 ("host_syncs", ctypes.c_uint64), ("table_rehashes", ctypes.c_uint64),
                 ("rccl_version", ctypes.c_int32), ("level_slots", ctypes.c_int32),
                 ("cost_c_ns", ctypes.c_double), ("cost_x_us", ctypes.c_double), ("shard_work_min", ctypes.c_uint64),
-                ("exchange_rounds", ctypes.c_uint64), ("fast_levels", ctypes.c_uint64), ("completions", ctypes.c_uint64)]
+                ("exchange_rounds", ctypes.c_uint64), ("fast_levels", ctypes.c_uint64), ("completions", ctypes.c_uint64),
+                ("deduped", ctypes.c_uint64)]
 
 
 _lib = None

@@ -69,6 +69,11 @@ struct Comm {
   // operation of the communicator (ncclCommAbort), so a failed rank ends the search on every rank
   // with DSL_ERR_COMM instead of leaving the others blocked in a collective.
   virtual int async_error() { return DSL_OK; }
+  // true once the stream has reached the last collective it enqueued since the last synced():
+  // a wait then waits on the collective, and only then does the deadline run (a long local kernel
+  // before it is not a stalled peer); false for a transport without stream collectives
+  virtual bool collective_reached() { return false; }
+  virtual void synced() {}
   virtual void abort() {}
 };
 
@@ -199,7 +204,8 @@ struct BfsEngine : EngineBase {
   // DSL_BLOCKING_SYNC=1 restores the blocking wait.
   bool spin_sync = !getenv("DSL_BLOCKING_SYNC");
   // With a communicator the wait also polls its asynchronous error and a deadline
-  // (DSL_COMM_TIMEOUT_MS, default 300 s): either aborts the communicator and fails the search.
+  // (DSL_COMM_TIMEOUT_MS, default 300 s, counted once the stream reached its last collective):
+  // either aborts the communicator and fails the search.
   const double comm_timeout_ms = getenv("DSL_COMM_TIMEOUT_MS") ? atof(getenv("DSL_COMM_TIMEOUT_MS")) : 300000.0;
   bool comm_failed = false;
   int comm_fail(const std::string& why) {
@@ -211,16 +217,21 @@ struct BfsEngine : EngineBase {
   }
   int hsync() {
     if (comm) {
-      const auto t0 = std::chrono::steady_clock::now();
+      // the deadline counts from the moment the stream reached its last collective (local work
+      // before it may take as long as it takes)
+      auto t0 = std::chrono::steady_clock::now();
       hipError_t e;
       for (uint64_t it = 0; (e = hipStreamQuery(stream)) == hipErrorNotReady; it++) {
         if ((it & 1023) == 1023) {
           if (comm->async_error() != DSL_OK) return comm_fail("asynchronous communicator error");
-          if (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > comm_timeout_ms)
+          const auto now = std::chrono::steady_clock::now();
+          if (!comm->collective_reached()) t0 = now;
+          else if (std::chrono::duration<double, std::milli>(now - t0).count() > comm_timeout_ms)
             return comm_fail("no progress within DSL_COMM_TIMEOUT_MS");
         }
       }
       if (e != hipSuccess) DSL_HIP(e);
+      comm->synced();
     } else if (spin_sync) {
       seg_since_sync = 0;
       hipError_t e;
@@ -1928,6 +1939,7 @@ struct BfsEngine : EngineBase {
           stats.work_items += S.lc.work_items;
           stats.new_states += S.lc.new_states;
           stats.probes += S.lc.probes;
+          stats.deduped += S.lc.deduped;
           stats.appended += fn;
           if (S.lc.term_best && recs.empty()) {  // the level's exact best terminal (fold_terminals)
             const uint64_t key = ~(uint64_t)S.lc.term_best;

@@ -24,10 +24,19 @@ struct RcclComm : Comm {
   uint64_t* dbuf = nullptr;  // 2 * (kMaxShards * 64) u64
   static constexpr int kScratch = 2 * kMaxShards * 64;
   const double timeout_ms = getenv("DSL_COMM_TIMEOUT_MS") ? atof(getenv("DSL_COMM_TIMEOUT_MS")) : 300000.0;
+  hipEvent_t ev = nullptr;  // recorded before each collective: the deadline starts when it is reached
+  bool ev_set = false;
   ~RcclComm() override {
     if (c) ncclCommDestroy(c);
     hipFree(dbuf);
+    if (ev) hipEventDestroy(ev);
   }
+  void mark(hipStream_t st) {
+    if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+    if (hipEventRecord(ev, st) == hipSuccess) ev_set = true;
+  }
+  bool collective_reached() override { return ev_set && hipEventQuery(ev) == hipSuccess; }
+  void synced() override { ev_set = false; }
   int async_error() override {
     if (!c) return DSL_ERR_COMM;
     ncclResult_t st = ncclSuccess;
@@ -43,14 +52,17 @@ struct RcclComm : Comm {
     c = nullptr;
   }
   // The small host-read collectives wait for their result polling the communicator's error and a
-  // deadline (a dead peer aborts the communicator instead of blocking this rank forever).
+  // deadline (a dead peer aborts the communicator instead of blocking this rank forever); the
+  // deadline counts from the moment the stream reached the collective (mark), not from the local
+  // kernels enqueued before it.
   int wait(hipStream_t st) {
-    const auto t0 = std::chrono::steady_clock::now();
+    auto t0 = std::chrono::steady_clock::now();
     hipError_t e;
     for (uint64_t it = 0; (e = hipStreamQuery(st)) == hipErrorNotReady; it++) {
       if ((it & 1023) == 1023) {
-        if (async_error() != DSL_OK ||
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() > timeout_ms) {
+        const auto now = std::chrono::steady_clock::now();
+        if (!collective_reached()) t0 = now;
+        if (async_error() != DSL_OK || std::chrono::duration<double, std::milli>(now - t0).count() > timeout_ms) {
           abort();
           set_error("RCCL collective failed or timed out on rank " + std::to_string(r) + " (communicator aborted)");
           return DSL_ERR_COMM;
@@ -61,6 +73,7 @@ struct RcclComm : Comm {
       set_error(std::string("HIP error ") + hipGetErrorString(e) + " in an RCCL collective");
       return DSL_ERR_HIP;
     }
+    ev_set = false;  // the stream is drained
     return DSL_OK;
   }
   int rank() const override { return r; }
@@ -75,6 +88,7 @@ struct RcclComm : Comm {
   int allgather_u64(const uint64_t* in, int k, uint64_t* out, hipStream_t st) override {
     if (!c) return DSL_ERR_COMM;
     if (k * (n + 1) > kScratch) return DSL_ERR_ARG;
+    mark(st);
     DSL_HIP(hipMemcpyAsync(dbuf, in, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclAllGather(dbuf, dbuf + k, k, ncclUint64, c, st), "allgather");
     if (rc) return rc;
@@ -84,6 +98,7 @@ struct RcclComm : Comm {
   int allreduce_u64(uint64_t* v, int k, bool min, hipStream_t st) override {
     if (!c) return DSL_ERR_COMM;
     if (k > kScratch) return DSL_ERR_ARG;
+    mark(st);
     DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclAllReduce(dbuf, dbuf, k, ncclUint64, min ? ncclMin : ncclSum, c, st), "allreduce");
     if (rc) return rc;
@@ -93,6 +108,7 @@ struct RcclComm : Comm {
   int bcast_u64(uint64_t* v, int k, int root, hipStream_t st) override {
     if (!c) return DSL_ERR_COMM;
     if (k > kScratch) return DSL_ERR_ARG;
+    mark(st);
     DSL_HIP(hipMemcpyAsync(dbuf, v, k * 8, hipMemcpyHostToDevice, st));
     int rc = ck(ncclBroadcast(dbuf, dbuf, k, ncclUint64, root, c, st), "broadcast");
     if (rc) return rc;
@@ -102,6 +118,7 @@ struct RcclComm : Comm {
   bool device_collectives() const override { return true; }
   int allgather_dev(const uint64_t* d_in, int k, uint64_t* d_out, hipStream_t st) override {
     if (!c) return DSL_ERR_COMM;
+    mark(st);
     return ck(ncclAllGather(d_in, d_out, k, ncclUint64, c, st), "allgather");
   }
   int ver = 0;
@@ -109,6 +126,7 @@ struct RcclComm : Comm {
   int alltoallv(const uint8_t* send, const uint64_t* so, const uint64_t* sb, uint8_t* recv, const uint64_t* ro,
                 const uint64_t* rb, hipStream_t st) override {
     if (!c) return DSL_ERR_COMM;
+    mark(st);
     int rc = ck(ncclGroupStart(), "group start");
     if (rc) return rc;
     for (int p = 0; p < n; p++) {
@@ -263,6 +281,8 @@ static int create_any(const dsl_protocol_desc& d, const dsl_engine_config& cfg, 
 #ifdef DSL_ONLY_MULTIPAXOS  // measurement variants (tools/build_variant.sh): C5's protocol (hand-written, IR), fast builds
     case DSL_PROTO_MULTIPAXOS: return make_engine<MultiPaxos>(d, cfg, out);
     case DSL_PROTO_MULTIPAXOS_IR: return make_engine<MultiPaxosIR>(d, cfg, out);
+#elif defined(DSL_ONLY_SYNTHETIC)  // measurement variants: C3's protocol only
+    case DSL_PROTO_SYNTHETIC: return make_engine<Synthetic>(d, cfg, out);
 #else
     case DSL_PROTO_PINGPONG: return make_engine<PingPong>(d, cfg, out);
     case DSL_PROTO_SIPAXOS: return make_engine<SIPaxos>(d, cfg, out);

@@ -102,6 +102,7 @@ struct LevelCounters {
   unsigned long long time_up;       // the search's deadline passed during this level (it is partial)
   unsigned long long route_spilled; // routed successors past their destination region (rspill list)
   unsigned long long unspilled;     // rows k_unspill appended (multi-shard fast path: device count)
+  unsigned long long deduped;       // successors found in the chunk's LDS set (ChunkDedup): not probed / routed
   unsigned long long phase[12];     // DSL_PHASES builds only: shader cycles per k_level phase
   unsigned long long phcls[32];     // DSL_PHASES: handler cycles per class [0, 16), wave-passes [16, 32)
 };
@@ -503,6 +504,38 @@ __device__ __forceinline__ bool lane_emit(bool active, const uint32_t* pw, const
   return __ballot(coll) != 0ull;
 }
 
+// In-chunk duplicate filter (P::kChunkDedup): a chunk's parents are consecutive frontier rows,
+// so siblings sit together, and two interleavings of two independent events of one grandparent
+// (a diamond) reach the same state inside one chunk -- 18 % of the C3 synthetic protocol's probes
+// (tools/cpu_bfs.cpp DSL_CPU_CHUNK_CENSUS, profiles/r06_chunk_census.txt). Every probing lane
+// first inserts its fingerprint's high word into an LDS set of the chunk (a 64-bit LDS CAS,
+// linear probing, at most 8 slots): a lane that finds it there is a successor of this chunk
+// already probed (or routed) by another lane -- the same state (63 fingerprint bits), so not new
+// (Search.java:485: discovered.add returns false) and neither probed nor routed again. A crowded
+// set only lets a duplicate through to the global probe, which answers exactly. A false merge needs
+// two distinct states of one chunk with equal high words: about (items per chunk)^2 / 2^64 per
+// chunk, 3e-8 for the whole C3 d10 search, within the visited table's own bound.
+template <class P, class = void>
+struct ChunkDedup : std::false_type {};
+template <class P>
+struct ChunkDedup<P, std::void_t<decltype(P::kChunkDedup)>> : std::integral_constant<bool, P::kChunkDedup> {};
+#ifndef DSL_DEDUP_SLOTS
+#define DSL_DEDUP_SLOTS 1024
+#endif
+constexpr int kDedupSlots = DSL_DEDUP_SLOTS;  // a power of two
+__device__ __forceinline__ bool chunk_seen(unsigned long long* set, const Fp& f) {
+  const unsigned long long key = f.hi | 1ull;  // never 0 (an empty slot)
+  uint32_t h = (uint32_t)f.lo & (uint32_t)(kDedupSlots - 1);
+#pragma unroll 1
+  for (int i = 0; i < 8; i++) {
+    const unsigned long long old = atomicCAS(set + h, 0ull, key);
+    if (old == 0ull) return false;
+    if (old == key) return true;
+    h = (h + 1u) & (uint32_t)(kDedupSlots - 1);
+  }
+  return false;
+}
+
 template <class P>
 struct LevelArgs {
   const uint32_t* cur;       // frontier rows of kWords (row ranges in `segs`)
@@ -736,7 +769,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 #ifdef DSL_PHASES
   __shared__ unsigned long long s_red[NWAVE];  // PH_FLUSH (instrumented builds)
 #endif
-  __shared__ unsigned long long s_red5[NWAVE * 5];
+  __shared__ unsigned long long s_red5[NWAVE * 6];
   __shared__ int s_wsum[NWAVE];
 #ifndef DSL_SORT_BALLOT
   // the window's class counts (LDS atomics in step 3a, each item's rank within its class in s_rnk)
@@ -751,10 +784,11 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ int16_t s_ev[kWin];  // each item's located event (locate_event code; kEvNone: none)
   __shared__ int s_stop, s_weff, s_gnext, s_tup;
   __shared__ uint64_t s_t0;
+  __shared__ unsigned long long s_dd[ChunkDedup<P>::value ? kDedupSlots : 1];
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
   const bool find = a.find != 0;
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
-  uint32_t c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0, c_probe = 0;
+  uint32_t c_succ = 0, c_new = 0, c_next_work = 0, c_work = 0, c_probe = 0, c_dup = 0;
   PH_DECL
   PH_CLS_DECL
 #ifdef DSL_KWARM
@@ -839,6 +873,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     else
       stage_rows_padded<NW, SP>(reinterpret_cast<const uint4*>(a.cur + p0 * NW), rows, pb);
     stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
+    if constexpr (ChunkDedup<P>::value)  // the chunk's duplicate filter starts empty (the staging barrier publishes it)
+      for (int i = tid; i < kDedupSlots; i += kLevelBlock) s_dd[i] = 0ull;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     PH_MARK(9);  // staging (LDS-DMA + wait + barrier)
@@ -846,6 +882,14 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     //    term of the incremental fingerprint: fp ^ H(i, old) ^ H(i, new) ^ ...), one lane per
     //    (parent, node); then the enabled events per parent (SearchState.events) and a workgroup
     //    exclusive scan (wave scans); the scan's barrier also publishes the hashes
+#ifndef DSL_CNT_SERIAL  // a chunk of <= 64 parents: waves 1-3 hash while wave 0 counts (+0.7 % on C5 d12)
+    if (pb <= 64) {
+      for (int x = tid - 64; x >= 0 && x < pb * P::kNodes; x += kLevelBlock - 64) {
+        const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
+        nh[x] = node_hash<P>(ii, rows + jj * SP + ii * P::kNodeWords);
+      }
+    } else
+#endif
     for (int x = tid; x < pb * P::kNodes; x += kLevelBlock) {
       const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
       nh[x] = node_hash<P>(ii, rows + jj * SP + ii * P::kNodeWords);
@@ -904,7 +948,26 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           const int e0 = off[j];
           const int lo = max(e0, w0), hi = min(off[j + 1], w0 + wn);
           const uint32_t* w = rows + j * SP;
-          for (int q = lo + sub; q < hi; q += tpp) {
+          int q = lo + sub;
+#ifndef DSL_CLS_ONE_LOOP  // message events first, by a branch-free body, then the timers (+1.3 % on C5 d12)
+          if (set.all_deliver) {  // event k < size is record k (SearchState.events: messages first)
+            const int mhi = min(hi, e0 + (int)Net<P>::size(w));
+            const int nn = P::num_nodes(prm);
+            for (; q < mhi; q += tpp) {
+              const auto r = Net<P>::at(w, q - e0);
+              const int i = P::rec_to(r);
+              const bool skip = i < nn && NoopFilter<P>::msg(i < nn ? i : 0, w, r, prm);
+              const int cls = skip ? Classes<P>::kSkip : P::msg_class(r);
+              s_par[q - w0] = (uint8_t)j;
+              s_cls[q - w0] = (uint8_t)cls;
+#ifndef DSL_SORT_BALLOT
+              s_rnk[q - w0] = (uint16_t)atomicAdd(&s_ccnt[cls], 1);
+#endif
+              s_ev[q - w0] = (int16_t)(q - e0);
+            }
+          }
+#endif
+          for (; q < hi; q += tpp) {
             int ev;
             s_par[q - w0] = (uint8_t)j;
 #ifndef DSL_SORT_BALLOT
@@ -1098,9 +1161,15 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
           if (rc == STEP_OK) c_succ++;
           if (rc == STEP_OK && !noop) {
             PH_MARK(2);  // fingerprint
+            // a successor of this chunk seen before (ChunkDedup): the same state, not new; it was
+            // probed or routed once already
+            bool dup = false;
+            if constexpr (ChunkDedup<P>::value) dup = !find && chunk_seen(s_dd, f);
+            c_dup += dup ? 1u : 0u;
             if (ROUTE) dest = owner_of(f, a.W);
             bool judge = false;
-            if (ROUTE) {
+            if (dup) {
+            } else if (ROUTE) {
               // a sharded level routes EVERY successor, its own shard's too: the owner probes them
               // all in one interleaved pass (k_probe_slab), so which source wins a state generated
               // by several is a fair race, and the shards' frontiers stay balanced (a local insert
@@ -1245,19 +1314,26 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     __syncthreads();  // LDS is reused by the next chunk
     PH_MARK(10);  // end-of-window / end-of-chunk barrier waits
   }
-  {  // the five statistics in one workgroup reduction (one barrier pair, five atomics)
-    const uint32_t v[5] = {wave_sum(c_succ), wave_sum(c_new), wave_sum(c_next_work), wave_sum(c_work),
-                           wave_sum(c_probe)};
+  {  // the statistics in one workgroup reduction (one barrier pair, one atomic each)
+    constexpr int NS = ChunkDedup<P>::value ? 6 : 5;
+    uint32_t v[NS];
+    v[0] = wave_sum(c_succ);
+    v[1] = wave_sum(c_new);
+    v[2] = wave_sum(c_next_work);
+    v[3] = wave_sum(c_work);
+    v[4] = wave_sum(c_probe);
+    if constexpr (NS > 5) v[5] = wave_sum(c_dup);
     __syncthreads();
     if (lane == 0)
 #pragma unroll
-      for (int i = 0; i < 5; i++) s_red5[wid * 5 + i] = v[i];
+      for (int i = 0; i < NS; i++) s_red5[wid * 6 + i] = v[i];
     __syncthreads();
-    if (tid < 5) {
+    if (tid < NS) {
       unsigned long long t = 0;
-      for (int w = 0; w < NWAVE; w++) t += s_red5[w * 5 + tid];
+      for (int w = 0; w < NWAVE; w++) t += s_red5[w * 6 + tid];
       unsigned long long* dst = tid == 0 ? &a.ctr->successors : tid == 1 ? &a.ctr->new_states
-                                : tid == 2 ? &a.ctr->next_work : tid == 3 ? &a.ctr->work_items : &a.ctr->probes;
+                                : tid == 2 ? &a.ctr->next_work : tid == 3 ? &a.ctr->work_items
+                                : tid == 4 ? &a.ctr->probes : &a.ctr->deduped;
       if (t) atomicAdd(dst, t);
     }
   }

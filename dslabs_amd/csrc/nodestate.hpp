@@ -627,6 +627,28 @@ DSL_HD int eval_prog(const DevSettings& set, DevProg g, const NodeView& v, const
   return (int)(st & 3u);
 }
 
+// A leaf known to hold on the parent (an invariant, not negated, of an expanded parent: the view is
+// incremental) may be evaluated on the successor from what the changed node's words changed: a
+// protocol may provide
+//   static int eval_held(const DevPred&, const NodeView&, const Params&, bool held)
+// (Multi-Paxos LOGS_CONSISTENT: only the slots whose entries the changed server changed, the other
+// slots are as valid as on the parent); it must equal eval whenever held is true of the parent
+// (tests/hostcheck compares the incremental verdict with the full one on every explored successor).
+template <class P, class = void>
+struct EvalHeld {
+  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const typename P::Params& prm, bool) {
+    return P::eval(pr, v, prm);
+  }
+};
+#ifndef DSL_NO_EVAL_HELD  // (measurement builds: -DDSL_NO_EVAL_HELD evaluates every leaf in full)
+template <class P>
+struct EvalHeld<P, std::void_t<decltype(&P::eval_held)>> {
+  static DSL_HD int eval(const DevPred& pr, const NodeView& v, const typename P::Params& prm, bool held) {
+    return P::eval_held(pr, v, prm, held);
+  }
+};
+#endif
+
 // checkState order over a node view (Search.java:162-231).
 // incremental: the view is a successor of an EXPANDED, non-initial parent, which therefore had
 // every invariant true, every goal false or throwing (ignored) and every prune false (a state
@@ -662,7 +684,7 @@ DSL_HD Verdict judge_view(const NodeView& v0, const typename P::Params& prm, con
 #endif
       const DevPred& op = set.ops[t];
       if (incremental && v.changed >= 0 && leaf_unchanged<P>(op, v)) continue;
-      int x = P::eval(op, v, prm);
+      int x = EvalHeld<P>::eval(op, v, prm, incremental && v.changed >= 0 && t < set.n_inv && !op.negate);
       if (x != PV_THREW && op.negate) x = !x;
       if (t < set.n_inv) {
         if (x != PV_TRUE) {  // a false or throwing invariant is violated
@@ -682,7 +704,7 @@ DSL_HD Verdict judge_view(const NodeView& v0, const typename P::Params& prm, con
     for (int t = kFlatUnroll; t < nt; t++) {
       const DevPred& op = set.ops[t];
       if (incremental && v.changed >= 0 && leaf_unchanged<P>(op, v)) continue;
-      int x = P::eval(op, v, prm);
+      int x = EvalHeld<P>::eval(op, v, prm, incremental && v.changed >= 0 && t < set.n_inv && !op.negate);
       if (x != PV_THREW && op.negate) x = !x;
       if (t < set.n_inv) {
         if (x != PV_TRUE) {

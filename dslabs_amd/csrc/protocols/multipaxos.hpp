@@ -615,6 +615,33 @@ struct MultiPaxos {
     return PV_TRUE;
   }
 
+  // LOGS_CONSISTENT on a successor whose parent held it (nodestate.hpp EvalHeld): a slot's validity
+  // reads only the servers' entries of that slot, so only the slots whose entry the changed server
+  // changed can have become invalid; each lane checks those (usually one: a uniform loop over the
+  // wave's changed slots instead of all four slots of the full check).
+  static DSL_HD int logs_consistent_held(const NodeView& v, const Params& p) {
+    if (v.changed < 0 || v.changed >= p.servers) return logs_consistent(v, p);
+    const uint32_t* o = v.base + v.changed * v.nw;
+    const uint32_t* n = v.over;
+    const uint32_t d1 = o[1] ^ n[1], d2 = o[2] ^ n[2];
+    uint32_t m = (d1 & 0xffffu ? 1u : 0u) | (d1 >> 16 ? 2u : 0u) | (d2 & 0xffffu ? 4u : 0u) | (d2 >> 16 ? 8u : 0u);
+    uint32_t lw[kMaxServers][2];
+    load_logs(v, p, lw);
+    bool ok = true;
+    while (!wave_none(m != 0u)) {
+      if (m) {
+        const int slot = __builtin_ctz(m) + 1;
+        m &= m - 1u;
+        ok &= slot_valid(lw, p, slot);
+      }
+    }
+    return ok ? PV_TRUE : PV_FALSE;
+  }
+  static DSL_HD int eval_held(const DevPred& pr, const NodeView& v, const Params& p, bool held) {
+    if (held && (pr.id == DSL_PRED_LOGS_CONSISTENT || pr.id == DSL_PRED_LOGS_CONSISTENT_ACTIVE))
+      return logs_consistent_held(v, p);
+    return eval(pr, v, p);
+  }
   static DSL_HD int eval(const DevPred& pr, const NodeView& v, const Params& p) {
     switch (pr.id) {
       case DSL_PRED_RESULTS_OK:

@@ -18,14 +18,24 @@
 
 namespace dsl {
 
+// k_level at 6 waves per SIMD (80 VGPRs): as fast as 8 (64 VGPRs) on C3 d10 with half the scratch
+// (60 vs 124 B per lane; profiles/r06_c3_dedup_waves_ab.txt)
 #ifndef DSL_SYNTH_WAVES
-#define DSL_SYNTH_WAVES 8
+#define DSL_SYNTH_WAVES 6
 #endif
 
 struct Synthetic {
   static constexpr int kMaxNodes = 5;
   static constexpr int kNodes = kMaxNodes, kNodeWords = 2, kNetCap = kMaxNodes, kMaxSends = 1;
   static constexpr int kLevelWaves = DSL_SYNTH_WAVES;  // k_level waves per SIMD (kernels.hpp LevelWaves)
+// k_level's in-chunk duplicate filter (kernels.hpp ChunkDedup): off. 18 % of C3's probes are
+// in-chunk duplicates (profiles/r06_chunk_census.txt), but the filter measured 7 % slower on C3 d10
+// (profiles/r06_c3_dedup_waves_ab.txt): every probing lane pays its LDS CAS chain, and a
+// duplicate's global probe is cheap (its line was just touched by the first occurrence).
+#ifndef DSL_SYNTH_DEDUP
+#define DSL_SYNTH_DEDUP 0
+#endif
+  static constexpr bool kChunkDedup = DSL_SYNTH_DEDUP;
   static constexpr int kMsgClasses = 1;  // handler classes of messages (Poke); timers: class 1
   static constexpr int kTimerMin = 1, kTimerMax = 100;
   using Rec = uint32_t;

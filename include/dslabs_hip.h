@@ -34,10 +34,11 @@
 extern "C" {
 #endif
 
-#define DSL_ABI_VERSION 4 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version;
+#define DSL_ABI_VERSION 5 /* 2: dsl_set_dropped; dsl_stats host_syncs / table_rehashes / rccl_version;
                             3: dsl_engine_config.flags, dsl_host_comm.flags;
                             4: dsl_settings.do_checks / check_sample, dsl_result check counts,
-                               dsl_stats exchange_rounds / fast_levels / completions */
+                               dsl_stats exchange_rounds / fast_levels / completions;
+                            5: dsl_stats deduped */
 #define DSL_MAX_NODES 32
 #define DSL_MAX_PREDICATES 16
 #define DSL_MAX_POOL 48          /* operands of combinator predicates (dsl_settings.pool) */
@@ -334,6 +335,9 @@ typedef struct {
   uint64_t exchange_rounds;
   uint64_t fast_levels;
   uint64_t completions;
+  /* successors an earlier successor of the same k_level chunk had already produced (the in-chunk
+     duplicate filter of protocols that enable it): not new, neither probed nor routed */
+  uint64_t deduped;
 } dsl_stats;
 
 int dsl_kernel_stats(dsl_engine* e, dsl_stats* out);

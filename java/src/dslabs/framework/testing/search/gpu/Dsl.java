@@ -46,7 +46,7 @@ public final class Dsl {
       OFF_RES_NOT_IDEMPOTENT = 120, OFF_RES_FIRST_NOT_DETERMINISTIC = 128, OFF_RES_FIRST_NOT_IDEMPOTENT = 224;
 
   // DSL_ABI_VERSION: the struct layout above; a library of another version is refused
-  public static final int ABI_VERSION = 4;
+  public static final int ABI_VERSION = 5;
   public static final int MAX_EVENT_FIELDS = 8;
 
   // dsl_protocol_id (include/dslabs_hip.h)
