@@ -1698,7 +1698,11 @@ struct BfsEngine : EngineBase {
           const double per_rank = max_rank_work ? (double)max_rank_work
                                   : rep_threshold() > 0 ? (double)g[2] / W : (double)g[2];
           const double frac = route_frac > 0 ? route_frac : 1.0;
-          slab = (uint64_t)(1.3 * frac * per_rank / ((double)W * kRouteSegs)) + 64;
+          // 1.15x the expected records per sub-slab + one wave's 64: every sub-slab takes records of
+          // all four wave indexes of many workgroups (k_level), so the fill is even (1.3x before
+          // round 6, when a sub-slab took one wave index's records)
+          static const double factor = getenv("DSL_SLAB_FACTOR") ? atof(getenv("DSL_SLAB_FACTOR")) : 1.15;
+          slab = (uint64_t)(factor * frac * per_rank / ((double)W * kRouteSegs)) + 64;
           if (const char* m = getenv("DSL_SLAB_MAX")) slab = std::min<uint64_t>(slab, std::max(1, atoi(m)));  // tests
         }
         const int lslots = level_slots((size_t)pb_max() * kRowLds + 16, route);

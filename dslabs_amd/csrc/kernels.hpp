@@ -515,10 +515,16 @@ __device__ __forceinline__ bool lane_emit(bool active, const uint32_t* pw, const
 // set only lets a duplicate through to the global probe, which answers exactly. A false merge needs
 // two distinct states of one chunk with equal high words: about (items per chunk)^2 / 2^64 per
 // chunk, 3e-8 for the whole C3 d10 search, within the visited table's own bound.
+// P::kChunkDedup enables it on unrouted levels, P::kRouteDedup on sharded (routed) levels, where a
+// duplicate also costs 16 bytes over the links and an owner probe.
 template <class P, class = void>
 struct ChunkDedup : std::false_type {};
 template <class P>
 struct ChunkDedup<P, std::void_t<decltype(P::kChunkDedup)>> : std::integral_constant<bool, P::kChunkDedup> {};
+template <class P, class = void>
+struct RouteDedup : std::false_type {};
+template <class P>
+struct RouteDedup<P, std::void_t<decltype(P::kRouteDedup)>> : std::integral_constant<bool, P::kRouteDedup> {};
 #ifndef DSL_DEDUP_SLOTS
 #define DSL_DEDUP_SLOTS 1024
 #endif
@@ -756,6 +762,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   // handler classes: messages, timers, then the events whose handler surely changes nothing
   // (NoopFilter: counted as successors and never run; they sort last and the passes stop before them)
   constexpr int NC = Classes<P>::kCount;
+  constexpr bool kDD = ROUTE ? RouteDedup<P>::value : ChunkDedup<P>::value;  // the in-chunk duplicate filter
   static_assert(P::kNodes * 256 < 32768 && P::kNetCap < 32768, "a located event fits s_ev's 16 bits");
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                           // a.PB (max) rows, stride SP
@@ -784,7 +791,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   __shared__ int16_t s_ev[kWin];  // each item's located event (locate_event code; kEvNone: none)
   __shared__ int s_stop, s_weff, s_gnext, s_tup;
   __shared__ uint64_t s_t0;
-  __shared__ unsigned long long s_dd[ChunkDedup<P>::value ? kDedupSlots : 1];
+  __shared__ unsigned long long s_dd[kDD ? kDedupSlots : 1];
   const int tid = threadIdx.x, lane = __lane_id(), wid = tid >> 6;
   const bool find = a.find != 0;
   // per-thread statistics, flushed once per workgroup (no per-wave atomics on shared words)
@@ -873,7 +880,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     else
       stage_rows_padded<NW, SP>(reinterpret_cast<const uint4*>(a.cur + p0 * NW), rows, pb);
     stage_lds(reinterpret_cast<const uint4*>(a.cur_fp + p0), reinterpret_cast<uint4*>(fps), pb);
-    if constexpr (ChunkDedup<P>::value)  // the chunk's duplicate filter starts empty (the staging barrier publishes it)
+    if constexpr (kDD)  // the chunk's duplicate filter starts empty (the staging barrier publishes it)
       for (int i = tid; i < kDedupSlots; i += kLevelBlock) s_dd[i] = 0ull;
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
@@ -1164,7 +1171,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             // a successor of this chunk seen before (ChunkDedup): the same state, not new; it was
             // probed or routed once already
             bool dup = false;
-            if constexpr (ChunkDedup<P>::value) dup = !find && chunk_seen(s_dd, f);
+            if constexpr (kDD) dup = !find && chunk_seen(s_dd, f);
             c_dup += dup ? 1u : 0u;
             if (ROUTE) dest = owner_of(f, a.W);
             bool judge = false;
@@ -1315,7 +1322,7 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     PH_MARK(10);  // end-of-window / end-of-chunk barrier waits
   }
   {  // the statistics in one workgroup reduction (one barrier pair, one atomic each)
-    constexpr int NS = ChunkDedup<P>::value ? 6 : 5;
+    constexpr int NS = kDD ? 6 : 5;
     uint32_t v[NS];
     v[0] = wave_sum(c_succ);
     v[1] = wave_sum(c_new);

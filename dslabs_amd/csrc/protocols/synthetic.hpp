@@ -36,6 +36,15 @@ struct Synthetic {
 #define DSL_SYNTH_DEDUP 0
 #endif
   static constexpr bool kChunkDedup = DSL_SYNTH_DEDUP;
+  // on sharded levels the filter would keep duplicates off the links (16 B each) and the owners'
+  // probes -- but the device's frontier order leaves few of them in a chunk (siblings are emitted
+  // by different waves and passes, interleaved with other workgroups' rows): with the filter on, C3
+  // d9 at W = 8 routed 549.7 M instead of 551.5 M records, while its k_level took 13 % longer
+  // (profiles/r06_shard_scale.txt). Off.
+#ifndef DSL_SYNTH_ROUTE_DEDUP
+#define DSL_SYNTH_ROUTE_DEDUP 0
+#endif
+  static constexpr bool kRouteDedup = DSL_SYNTH_ROUTE_DEDUP;
   static constexpr int kMsgClasses = 1;  // handler classes of messages (Poke); timers: class 1
   static constexpr int kTimerMin = 1, kTimerMax = 100;
   using Rec = uint32_t;
