@@ -3,7 +3,7 @@ dominant kernel k_level: per-launch duration, FETCH_SIZE / WRITE_SIZE (KB in roc
 traffic per launch with the gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the
 bytes of 16-byte-per-lane reads: x2), and the SQ counters. Writes one JSON object.
 
-    python tools/pmc_summary.py gpurun_out/prof_TAG > profiles/rNN_pmc_WORKLOAD_dDEPTH.json
+    python tools/pmc_summary.py gpurun_out/prof_TAG [k_levelINS_10MultiPaxosELb0E] > profiles/rNN_pmc_WORKLOAD_dDEPTH.json
 """
 import csv
 import glob
@@ -27,6 +27,26 @@ def per_dispatch(path):
     return by
 
 
+def code_object_meta(pattern):
+    """.vgpr_count / .agpr_count / spills / scratch / LDS of the kernel whose mangled name matches
+    `pattern` (e.g. k_levelINS_10MultiPaxosELb0E) in the in-tree library's code object
+    (tools/kernel_meta.py; None when the library or the LLVM tools are missing)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "dslabs_amd", "libdslabs_hip%s.so" % (
+        "_" + os.environ["DSL_LIB_VARIANT"] if os.environ.get("DSL_LIB_VARIANT") else ""))
+    try:
+        out = subprocess.run([sys.executable, os.path.join(root, "tools", "kernel_meta.py"), lib, pattern],
+                             capture_output=True, text=True, timeout=120).stdout
+    except Exception:
+        return None
+    for line in out.splitlines():
+        k = json.loads(line)
+        return {x: k[x] for x in ("kernel", "vgpr_count", "agpr_count", "vgpr_spill_count", "sgpr_spill_count",
+                                  "private_segment_fixed_size", "group_segment_fixed_size", "waves_per_simd")}
+    return None
+
+
 def main(d):
     out = {"kernel": KERNEL, "source": os.path.basename(d.rstrip("/"))}
     kt = os.path.join(d, "kt", "run_kernel_trace.csv")
@@ -35,8 +55,13 @@ def main(d):
         durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
         out["launches_traced"] = len(durs)
         out["avg_launch_ms"] = sum(durs) / max(1, len(durs))
-        out["vgpr"] = rows[0].get("VGPR_Count") if rows else None
+        # rocprofv3's columns (on gfx950 its VGPR_Count reads 64 for a 128-VGPR k_level); the
+        # code object's own metadata (tools/kernel_meta.py) is authoritative, added when the
+        # library is at hand
+        out["vgpr_rocprof"] = rows[0].get("VGPR_Count") if rows else None
         out["scratch_bytes_per_lane"] = rows[0].get("Scratch_Size") if rows else None
+        if rows and len(sys.argv) > 2:  # the instantiation (rocprofv3 -T truncates the name to k_level)
+            out["code_object"] = code_object_meta(sys.argv[2])
     tot = defaultdict(float)
     n = 0
     for f in glob.glob(os.path.join(d, "pmc_*", "run_counter_collection.csv")):
