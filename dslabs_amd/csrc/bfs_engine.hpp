@@ -123,6 +123,9 @@ struct BfsEngine : EngineBase {
     uint64_t out_item_cap = 0;
     Fp* in_fp = nullptr;
     uint64_t in_fp_cap = 0;
+    uint32_t* out_pk = nullptr;  // the regions packed for the links (12 B per record), out and in
+    uint32_t* in_pk = nullptr;
+    uint64_t out_pk_cap = 0, in_pk_cap = 0, cap_pk = 0;
     uint8_t* rep_out = nullptr;  // answers to the received fingerprints (owner side)
     uint64_t rep_out_cap = 0;
     uint8_t* rep_in = nullptr;   // answers to this shard's fingerprints, W regions of cap_fp (source side)
@@ -321,7 +324,8 @@ struct BfsEngine : EngineBase {
     for (auto& s : sh) {
       void* ptrs[] = {s.table,     s.cur,      s.next,   s.cur_fp, s.next_fp, s.terms,  s.rc,
                       s.out_key,   s.in_fp,    s.rep_out, s.rep_in, s.spill, s.ctrbuf,
-                      s.find_ctr,  s.rspill,   s.out2,    s.rep2,   s.out_item, s.out2_item, s.newl, s.nl_ctr};
+                      s.find_ctr,  s.rspill,   s.out2,    s.rep2,   s.out_item, s.out2_item, s.newl, s.nl_ctr,
+                      s.out_pk,    s.in_pk};
       for (void* q : ptrs) (void)hipFree(q);
       for (auto* q : s.hpar) (void)hipFree(q);
       for (auto* q : s.hev) (void)hipFree(q);
@@ -892,6 +896,9 @@ struct BfsEngine : EngineBase {
     DSL_TRY(grow_x(&S.out_item, &S.out_item_cap, S.cap_fp * W));
     DSL_TRY(grow_x(&S.rspill, &S.rspill_cap, std::max<uint64_t>(S.work, 1)));
     DSL_TRY(grow_x(&S.in_fp, &S.in_fp_cap, S.cap_fp * W));
+    S.cap_pk = pk_region_words(cs);
+    DSL_TRY(grow_x(&S.out_pk, &S.out_pk_cap, std::max<uint64_t>(S.cap_pk * W, 1)));
+    DSL_TRY(grow_x(&S.in_pk, &S.in_pk_cap, std::max<uint64_t>(S.cap_pk * W, 1)));
     DSL_TRY(grow_x(&S.rep_out, &S.rep_out_cap, S.cap_fp * W));
     DSL_TRY(grow_x(&S.rep_in, &S.rep_in_cap, S.cap_fp * W));
     // rows: every routed record of this shard may come back new (its own shard's included);
@@ -992,31 +999,33 @@ struct BfsEngine : EngineBase {
     Mat so(L, std::vector<uint64_t>(W, 0)), sb = so, ro = so, rb = so;
     std::vector<const uint8_t*> snd(L);
     std::vector<uint8_t*> rcv(L);
-    const size_t R = sizeof(Fp);
     if (cs) {
       for (auto& S : sh) {
         hipLaunchKernelGGL(k_route_headers, dim3(1), dim3(kMaxShards * kRouteSegs), 0, stream,
                            (const RouteCounters*)S.rc, S.out_key, S.cap_fp, cs, W,
-                           (unsigned long long*)(last ? nullptr : S.nl_ctr));
+                           (unsigned long long*)(last ? nullptr : S.nl_ctr), S.out_pk, S.cap_pk);
         DSL_HIP(hipGetLastError());
       }
-      // round A: the regions of every (source, owner) pair
+      // round A: the regions of every (source, owner) pair, packed (12 bytes per record)
       for (int l = 0; l < L; l++) {
         Shard& S = sh[l];
+        const uint64_t PB = S.cap_pk * 4;
         for (int d = 0; d < W; d++) {
-          const uint64_t n = d == S.gid ? 0 : S.cap_fp * R;
-          so[l][d] = (uint64_t)d * S.cap_fp * R;
+          const uint64_t n = d == S.gid ? 0 : PB;
+          so[l][d] = (uint64_t)d * PB;
           sb[l][d] = n;
-          ro[l][d] = (uint64_t)d * S.cap_fp * R;
+          ro[l][d] = (uint64_t)d * PB;
           rb[l][d] = n;
         }
-        snd[l] = reinterpret_cast<const uint8_t*>(S.out_key);
-        rcv[l] = reinterpret_cast<uint8_t*>(S.in_fp);
+        snd[l] = reinterpret_cast<const uint8_t*>(S.out_pk);
+        rcv[l] = reinterpret_cast<uint8_t*>(S.in_pk);
       }
       DSL_TRY(xround(snd, so, sb, rcv, ro, rb));
       for (auto& S : sh) {
         ProbeSlabArgs pa{};
         pa.in = S.in_fp;
+        pa.in_pk = S.in_pk;
+        pa.cap_pk = S.cap_pk;
         pa.self = S.out_key + (size_t)S.gid * S.cap_fp;
         pa.cap_fp = S.cap_fp;
         pa.cs = cs;
@@ -1770,6 +1779,8 @@ struct BfsEngine : EngineBase {
           a.me = S.gid;
           a.owner_filter = route && first_sharded ? 1 : 0;
           a.out_key = S.out_key;
+          a.out_pk = slab ? S.out_pk : nullptr;
+          a.cap_pk = S.cap_pk;
           a.out_item = S.out_item;
           a.cap_fp = S.cap_fp;
           a.route_cs = S.route_cs;

@@ -173,6 +173,13 @@ struct TerminalRec {
 constexpr int kRouteSegs = 32;
 constexpr int kRouteStride = 16;
 constexpr int kRouteHdr = kRouteSegs / 2;
+// The same regions as they cross the links (round A): 12-byte packed records {lo[0, 32), hi} --
+// all an owner's probe reads of a fingerprint (the home bucket and key bits of lo are below bit
+// 32, kKeyBits; the owner bits, lo's top 32, are implied by the destination) -- after a header of
+// kPkHdr records holding the 32 counts (64 words). A region is kPkWords * (kPkHdr + 32 cs) words.
+constexpr int kPkWords = 3;
+constexpr int kPkHdr = (2 * kRouteSegs + kPkWords - 1) / kPkWords;
+__host__ __device__ inline uint64_t pk_region_words(uint64_t cs) { return (uint64_t)kPkWords * (kPkHdr + kRouteSegs * cs); }
 struct RouteCounters {
   unsigned long long out[kMaxShards * kRouteSegs * kRouteStride];
 };
@@ -570,6 +577,8 @@ struct LevelArgs {
   // which stay at the source for the materialization
   Fp* out_key;
   uint64_t* out_item;
+  uint32_t* out_pk;          // the regions of the other shards packed for the links (kPkWords per record; null: none)
+  uint64_t cap_pk;           // words per packed region (pk_region_words(route_cs))
   uint64_t cap_fp;           // records per region (kRouteHdr + kRouteSegs * route_cs)
   uint64_t route_cs;         // records per sub-slab
   RouteCounters* rc;
@@ -1307,6 +1316,13 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               const uint64_t o = (uint64_t)dest * a.cap_fp + kRouteHdr + (uint64_t)sub * a.route_cs + ridx;
               a.out_key[o] = f;
               a.out_item[o] = item;
+              if (a.out_pk && dest != a.me) {  // what crosses the link: 12 bytes
+                uint32_t* pk = a.out_pk + (uint64_t)dest * a.cap_pk +
+                               (uint64_t)kPkWords * (kPkHdr + (uint64_t)sub * a.route_cs + ridx);
+                pk[0] = (uint32_t)f.lo;
+                pk[1] = (uint32_t)f.hi;
+                pk[2] = (uint32_t)(f.hi >> 32);
+              }
             } else {
               const unsigned long long x = atomicAdd(&a.ctr->route_spilled, 1ull);
               if (x < a.rspill_cap) a.rspill[x] = item;
@@ -1573,11 +1589,17 @@ __global__ void __launch_bounds__(64) k_level_record(RecordArgs a) {
 // sub-slab capacity); the owner reads it from the region it receives (k_probe_slab). Also zeroes
 // k_new_list's counter for this level (no separate fill launch).
 __global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t cap_fp, uint64_t cs, int W,
-                                unsigned long long* zero_ctr) {
+                                unsigned long long* zero_ctr, uint32_t* out_pk, uint64_t cap_pk) {
   const int t = threadIdx.x, d = t / kRouteSegs, q = t - d * kRouteSegs;
   if (t == 0 && zero_ctr) *zero_ctr = 0ull;
-  if (d < W)
-    reinterpret_cast<uint64_t*>(out_key + (uint64_t)d * cap_fp)[q] = min<uint64_t>(rc->out[rc_idx(d, q)], cs);
+  if (d < W) {
+    const uint64_t c = min<uint64_t>(rc->out[rc_idx(d, q)], cs);
+    reinterpret_cast<uint64_t*>(out_key + (uint64_t)d * cap_fp)[q] = c;
+    if (out_pk) {  // the packed region's header: the same counts, two words each
+      out_pk[(uint64_t)d * cap_pk + 2 * q] = (uint32_t)c;
+      out_pk[(uint64_t)d * cap_pk + 2 * q + 1] = (uint32_t)(c >> 32);
+    }
+  }
 }
 
 // Owner side of the fast path: W regions of cap_fp records (layout: RouteCounters), the received
@@ -1587,6 +1609,8 @@ __global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t c
 // shard's own at self_reply[...] (its source-side answer array).
 struct ProbeSlabArgs {
   const Fp* in;
+  const uint32_t* in_pk;  // the other sources' regions as received: packed (kPkWords per record); null: `in`
+  uint64_t cap_pk;
   const Fp* self;
   uint64_t cap_fp, cs;
   int32_t W, me;
@@ -1602,13 +1626,24 @@ __global__ void __launch_bounds__(kBlock) k_probe_slab(ProbeSlabArgs a) {
   __shared__ unsigned long long s_red[kBlock / 64];
   const int g = blockIdx.x, src = g / kRouteSegs, q = g - src * kRouteSegs;
   const bool self = src == a.me;
+  const bool pk = !self && a.in_pk;
   const Fp* region = self ? a.self : a.in + (uint64_t)src * a.cap_fp;
-  const uint64_t n = min<uint64_t>(reinterpret_cast<const uint64_t*>(region)[q], a.cs);
+  const uint32_t* pregion = pk ? a.in_pk + (uint64_t)src * a.cap_pk : nullptr;
+  const uint64_t n = min<uint64_t>(pk ? ((uint64_t)pregion[2 * q] | ((uint64_t)pregion[2 * q + 1] << 32))
+                                      : reinterpret_cast<const uint64_t*>(region)[q], a.cs);
   uint8_t* rep = a.reply ? (self ? a.self_reply : a.reply + (uint64_t)src * a.cap_fp) : nullptr;
-  const uint64_t base = kRouteHdr + (uint64_t)q * a.cs;
+  const uint64_t base = kRouteHdr + (uint64_t)q * a.cs;  // the answers keep the 16-byte layout's indexes
+  const uint64_t pbase = (uint64_t)kPkWords * (kPkHdr + (uint64_t)q * a.cs);
   unsigned long long c_new = 0;
   for (uint64_t j = (uint64_t)blockIdx.y * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.y * blockDim.x) {
-    const int ins = table_insert(a.table, region[base + j]);
+    Fp f;
+    if (pk) {  // lo's owner bits (above kKeyBits) are not needed by the probe
+      const uint32_t* r = pregion + pbase + (uint64_t)kPkWords * j;
+      f = Fp{(uint64_t)r[1] | ((uint64_t)r[2] << 32), (uint64_t)r[0]};
+    } else {
+      f = region[base + j];
+    }
+    const int ins = table_insert(a.table, f);
     if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
     c_new += ins == INS_NEW;
     if (rep) rep[base + j] = ins == INS_NEW ? 1 : 0;

@@ -61,8 +61,8 @@ def main():
         k = sum(lv.values())
         if depth in slabs:
             cs, last = slabs[depth]
-            region = (16 + 32 * cs) * 16  # bytes of one (source, owner) region
-            comm = region / (bw * 1e3) + round_us + (0 if last else region / 16 / (bw * 1e3) + round_us)
+            region = (22 + 32 * cs) * 12  # bytes of one (source, owner) region: 12-byte packed records (round 6)
+            comm = region / (bw * 1e3) + round_us + (0 if last else (16 + 32 * cs) / (bw * 1e3) + round_us)  # round B: a byte per record
             t = k / W + comm + sync_us
             print(f"level {depth}: sharded, kernels {k / W:.1f} + exchange {comm:.1f} + sync {sync_us} = {t:.1f} "
                   f"(one GPU: {sum(single[i].values()):.1f})")

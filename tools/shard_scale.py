@@ -45,7 +45,7 @@ def main():
                                   "expand_ms": round(st["expand_ms"], 3), "exchange_ms": round(st["exchange_ms"], 3),
                                   "sharded_levels": st["sharded_levels"], "fast_levels": st["fast_levels"],
                                   "completions": st["completions"], "exchange_rounds": st["exchange_rounds"],
-                                  "routed_records": st["exchanged"], "routed_bytes": st["exchanged"] * 16,
+                                  "routed_records": st["exchanged"], "routed_bytes": st["exchanged"] * 12,
                                   "host_syncs": st["host_syncs"], "table_slots": st["table_slots"]}), flush=True)
                 assert r.per_depth == want, (r.per_depth, want)
         finally:
