@@ -1412,6 +1412,12 @@ struct BfsEngine : EngineBase {
     t_run0 = std::chrono::steady_clock::now();
     for (int attempt = 0;; attempt++) {
       const int rc = run_once(out);
+      if (rc == DSL_ERR_COMM && comm && !comm_failed) {
+        // a transport failure (a dead or stalled peer, a caller-transport callback that failed)
+        // leaves the ranks out of step: the engine refuses every later search
+        comm_failed = true;
+        comm->abort();
+      }
       if (rc == DSL_RESTART_REKEY && attempt < 8) {
         restart_buckets = rekey_buckets;
         continue;

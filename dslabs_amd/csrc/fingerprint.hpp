@@ -109,10 +109,12 @@ DSL_HD uint64_t table_home(const Table& t, const Fp& f) { return ((f.lo & t.buck
 // atomic rate rather than latency): each slot is read with a plain load first and only an empty
 // one is CAS'd. A load can only be stale towards 0 (slots are write-once), which the CAS then
 // corrects, so the answer is the same; a state already present costs a read instead of an atomic.
-__device__ __forceinline__ int table_insert(const Table& t, const Fp& f) {
+// first > 0: the probe continues at slot home + first (the earlier slots were CAS'd and held other
+// keys; k_level's judge-overlap variant issues the home slot's CAS itself)
+__device__ __forceinline__ int table_insert(const Table& t, const Fp& f, int first = 0) {
   const uint64_t k0 = table_key0(t, f), home = table_home(t, f), nmask = t.bucket_mask * 8 + 7;
-  uint64_t i = home;
-  for (int probe = 0; probe < 8 * (kMaxDisp + 1); probe++) {
+  uint64_t i = (home + (uint64_t)first) & nmask;
+  for (int probe = first; probe < 8 * (kMaxDisp + 1); probe++) {
     const uint64_t d = ((i >> 3) - (home >> 3)) & t.bucket_mask;
     if (d > (uint64_t)kMaxDisp) break;
     const unsigned long long key = (unsigned long long)(k0 | (d << 1));

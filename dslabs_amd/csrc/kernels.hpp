@@ -1184,6 +1184,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             c_dup += dup ? 1u : 0u;
             if (ROUTE) dest = owner_of(f, a.W);
             bool judge = false;
+            bool spec = false;  // judged while the home slot's CAS is in flight (DSL_JUDGE_OVERLAP)
+            unsigned long long spec_old = 0ull, spec_key = 0ull;
             if (dup) {
             } else if (ROUTE) {
               // a sharded level routes EVERY successor, its own shard's too: the owner probes them
@@ -1198,13 +1200,25 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               judge = a.judge_routed != 0;
             } else {
               c_probe++;
-              const int ins = find ? INS_NEW : table_insert(a.table, f);
-              PH_MARK(3);  // visited-table probe / insert
-              if (ins == INS_NEW) {
-                c_new++;
+#ifdef DSL_JUDGE_OVERLAP
+              if (!find && !a.table.load_first) {
+                // the home slot's CAS is issued now and its answer used after the judge, which every
+                // probing lane runs meanwhile (its verdict counts only for a new state)
+                spec_key = table_key0(a.table, f);
+                spec_old = atomicCAS(a.table.slots + table_home(a.table, f), 0ull, spec_key);
+                spec = true;
                 judge = true;
-              } else if (ins == INS_FULL) {
-                atomicAdd(&a.ctr->err_table, 1ull);
+              } else
+#endif
+              {
+                const int ins = find ? INS_NEW : table_insert(a.table, f);
+                PH_MARK(3);  // visited-table probe / insert
+                if (ins == INS_NEW) {
+                  c_new++;
+                  judge = true;
+                } else if (ins == INS_FULL) {
+                  atomicAdd(&a.ctr->err_table, 1ull);
+                }
               }
             }
             if (judge) {
@@ -1226,7 +1240,15 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
 #else
                 const int v = judge_view<P>(view, prm, set, a.depth, &pi, a.incremental != 0);
 #endif
-                if (v == V_VALID) {
+                bool use = true;
+                if (spec) {  // the probe's answer: the home slot held nothing (new), this key, or another one
+                  const int ins = spec_old == 0ull ? INS_NEW : spec_old == spec_key ? INS_EXISTS : table_insert(a.table, f, 1);
+                  if (ins == INS_NEW) c_new++;
+                  else if (ins == INS_FULL) atomicAdd(&a.ctr->err_table, 1ull);
+                  use = ins == INS_NEW;
+                }
+                if (!use) {
+                } else if (v == V_VALID) {
                   if (route) {
                   } else if (Net<P>::size(w) + dn <= P::kNetCap) {
                     is_valid = !find;

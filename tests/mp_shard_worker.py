@@ -17,7 +17,11 @@ sys.path.insert(0, ROOT)
 def main():
     import torch.distributed as dist
     mode, out = sys.argv[1], sys.argv[2]
-    dist.init_process_group("gloo")
+    if mode == "dead_peer":  # a dead peer must surface as an error within seconds, not gloo's 30 min
+        import datetime
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=20))
+    else:
+        dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     from dslabs_amd.distributed import TorchHostComm
     # DSL_TEST_DEVICE_COLLECTIVES=1: the engine runs its RCCL branches (device-side gathers), the
@@ -52,6 +56,35 @@ def main():
         hc.alltoallv(None, send.ctypes.data_as(U8), so.ctypes.data_as(U), sb.ctypes.data_as(U),
                      recv.ctypes.data_as(U8), ro.ctypes.data_as(U), rb.ctypes.data_as(U))
         res["alltoallv"] = recv[:int(rb.sum())].tolist()
+    elif mode == "dead_peer":
+        # both ranks search C5 to depth 8, every level sharded; then rank 1 dies; rank 0's next
+        # search must fail with DSL_ERR_COMM and every later one be refused at once
+        import time
+        from dslabs_amd import RESULTS_OK, Engine, SearchSettings
+        from dslabs_amd._lib import EngineError
+        from dslabs_amd.protocols import MultiPaxos
+        proto = MultiPaxos(3, 2, "append-xy")
+        s = SearchSettings().addInvariant(RESULTS_OK).maxDepth(8)
+        s.table_log2_slots = 22
+        eng = Engine(proto, device=0, rank=rank, world_size=world, host_comm=hc, replicate_below=0)
+        r = eng.bfs(proto.initial_state(), s)
+        res["first"] = r.per_depth
+        if rank == 1:
+            with open(out, "w") as f:
+                json.dump(res, f)
+            os._exit(0)  # no goodbye to the peer
+        time.sleep(1.0)
+        for k in ("second", "third"):
+            t0 = time.perf_counter()
+            try:
+                eng.bfs(proto.initial_state(), s)
+                res[k] = "ok"
+            except EngineError as e:
+                res[k] = str(e)
+            res[k + "_s"] = round(time.perf_counter() - t0, 3)
+        with open(out, "w") as f:
+            json.dump(res, f)
+        os._exit(0)  # the process group cannot be torn down with the peer gone
     else:
         from dslabs_amd import CLIENTS_DONE, RESULTS_OK, Engine, SearchSettings
         from dslabs_amd.protocols import MultiPaxos, PingPong, SIPaxos

@@ -159,6 +159,17 @@ def test_bench_multi_gpu_branch_share_device(rep):
         assert sh["exchange_rounds"] == 2 * sh["sharded_levels"] - 1, sh
 
 
+def test_dead_peer_fails_the_search_and_refuses_later_ones():
+    """a rank that dies between searches ends the survivor's next search with
+    DSL_ERR_COMM (its transport's collective fails: here gloo's broken connection), and the engine
+    refuses every later search at once instead of running out of step with its peers."""
+    res = run_workers("dead_peer", 2, timeout=240)
+    r0 = next(r for r in res if r["rank"] == 0)
+    assert r0["first"] == MPX["mp_c5_d12"]["per_depth"][:9]
+    assert "DSL_ERR_COMM" in r0["second"] and r0["second_s"] < 60, r0
+    assert "DSL_ERR_COMM" in r0["third"] and "create a new engine" in r0["third"] and r0["third_s"] < 1, r0
+
+
 def test_rccl_engine_at_world_1():
     """make_comm / ncclCommInitRank / ncclGetVersion and the RcclComm collectives run once on a
     one-GPU box: a world-size-1 engine with its RCCL communicator (DSL_CFG_RCCL_AT_WORLD_1) runs
