@@ -513,10 +513,13 @@ struct BfsEngine : EngineBase {
   // the LDS budget of the staged rows.
   // LDS per staged parent: its row, fingerprint, node hashes (kernels.hpp k_level step 2) and offset
   // (+16 per chunk: LdsRow::image rounds the padded row image up to 16 bytes)
-  static constexpr size_t kRowLds = (size_t)LdsRow<P>::kStride * 4 + sizeof(Fp) * (1 + P::kNodes) + 4;
+  static constexpr size_t kRowLds = (size_t)LdsRow<P>::kStride * 4 + sizeof(Fp) * (1 + (DSL_NH_LDS ? P::kNodes : 0)) + 4;
   int pb_max() const {
-    const int lds_max = (int)((DSL_ROWS_LDS_KB * 1024) / kRowLds);
-    const int want = (int)((3 * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
+#ifndef DSL_PB_PASSES
+#define DSL_PB_PASSES 3
+#endif
+    const int lds_max = (int)((DSL_ROWS_LDS_BYTES) / kRowLds);
+    const int want = (int)((DSL_PB_PASSES * kLevelBlock * 16 + avg_events_x16 - 1) / std::max<uint64_t>(avg_events_x16, 1));
     return std::max(1, std::min({want, lds_max, kLevelBlock}));
   }
   // k_level workgroups resident at once on the device with `lds` bytes of dynamic LDS: the

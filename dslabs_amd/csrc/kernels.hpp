@@ -48,6 +48,14 @@ constexpr int kSegs = 32;
 #ifndef DSL_ROWS_LDS_KB
 #define DSL_ROWS_LDS_KB 24
 #endif
+#ifndef DSL_ROWS_LDS_BYTES  // the same budget in bytes (measurement builds set it between whole KB)
+#define DSL_ROWS_LDS_BYTES (DSL_ROWS_LDS_KB * 1024)
+#endif
+// 1: the parents' node hashes are computed once per chunk and kept in LDS (80 B per Multi-Paxos
+// parent); 0: every probing lane hashes its changed node's old words itself (more parents per chunk)
+#ifndef DSL_NH_LDS
+#define DSL_NH_LDS 1
+#endif
 // Row stride of the staged parents in LDS (dwords). A packed row is a multiple of 16 B, and
 // Multi-Paxos's is 160 dwords = 0 mod 32: at stride kWords every lane-per-parent access of word c
 // (node hashes, event counts, classification, the handlers' parent reads) hits bank c mod 32, a
@@ -684,7 +692,7 @@ __device__ __forceinline__ void stage_rows_dma(const uint4* src, uint32_t* dst, 
 template <int NW, int SP>
 __device__ __forceinline__ void stage_rows_padded(const uint4* src, uint32_t* dst, int pb) {
   constexpr int U = NW / 4;  // 16-byte units per row
-  constexpr int kIt = (DSL_ROWS_LDS_KB * 1024 / 16 + kLevelBlock - 1) / kLevelBlock;
+  constexpr int kIt = (DSL_ROWS_LDS_BYTES / 16 + kLevelBlock - 1) / kLevelBlock;
   const int n16 = pb * U;
   uint4 v[kIt];
 #pragma unroll
@@ -776,8 +784,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   extern __shared__ __align__(16) uint32_t lds[];
   uint32_t* rows = lds;                                           // a.PB (max) rows, stride SP
   Fp* fps = reinterpret_cast<Fp*>(rows + LdsRow<P>::image(a.PB));  // a.PB
+  constexpr int kNhPer = DSL_NH_LDS ? P::kNodes : 0;
   Fp* nh = fps + a.PB;                                     // a.PB * kNodes: the parents' node hashes
-  int* off = reinterpret_cast<int*>(nh + a.PB * P::kNodes);  // a.PB + 1
+  int* off = reinterpret_cast<int*>(nh + a.PB * kNhPer);   // a.PB + 1
   __shared__ SegTable s_segs;
   __shared__ BlockResv<kLevelBlock> s_resv;
   __shared__ uint32_t s_nodew[kLevelBlock * P::kNodeWords];
@@ -899,14 +908,15 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
     //    (parent, node); then the enabled events per parent (SearchState.events) and a workgroup
     //    exclusive scan (wave scans); the scan's barrier also publishes the hashes
 #ifndef DSL_CNT_SERIAL  // a chunk of <= 64 parents: waves 1-3 hash while wave 0 counts (+0.7 % on C5 d12)
-    if (pb <= 64) {
+    if (!DSL_NH_LDS) {
+    } else if (pb <= 64) {
       for (int x = tid - 64; x >= 0 && x < pb * P::kNodes; x += kLevelBlock - 64) {
         const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
         nh[x] = node_hash<P>(ii, rows + jj * SP + ii * P::kNodeWords);
       }
     } else
 #endif
-    for (int x = tid; x < pb * P::kNodes; x += kLevelBlock) {
+    for (int x = tid; x < pb * kNhPer; x += kLevelBlock) {
       const int jj = x / P::kNodes, ii = x - jj * P::kNodes;
       nh[x] = node_hash<P>(ii, rows + jj * SP + ii * P::kNodeWords);
     }
@@ -1166,7 +1176,8 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
               dn = delta_new_count<P>(d);
               noop = dn == 0 && same_words<P::kNodeWords>(d.nw, w + dnode * P::kNodeWords);
               if (!noop) {
-                f = delta_fingerprint_cached<P>(fp_xor(fps[j], nh[j * P::kNodes + dnode]), d);
+                if constexpr (DSL_NH_LDS) f = delta_fingerprint_cached<P>(fp_xor(fps[j], nh[j * P::kNodes + dnode]), d);
+                else f = delta_fingerprint<P>(w, fps[j], d);
                 // the changed node's words go through LDS: a view pointing at the register
                 // array would take its address and push the whole delta into scratch
 #pragma unroll
