@@ -1028,6 +1028,7 @@ struct BfsEngine : EngineBase {
         ProbeSlabArgs pa{};
         pa.in = S.in_fp;
         pa.in_pk = S.in_pk;
+        pa.self_pk = S.out_pk + (size_t)S.gid * S.cap_pk;
         pa.cap_pk = S.cap_pk;
         pa.self = S.out_key + (size_t)S.gid * S.cap_fp;
         pa.cap_fp = S.cap_fp;

@@ -1347,9 +1347,9 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
             const uint64_t item = ((p0 + j) << 20) | (uint64_t)k;
             if (ridx < a.route_cs) {
               const uint64_t o = (uint64_t)dest * a.cap_fp + kRouteHdr + (uint64_t)sub * a.route_cs + ridx;
-              a.out_key[o] = f;
               a.out_item[o] = item;
-              if (a.out_pk && dest != a.me) {  // what crosses the link: 12 bytes
+              if (!a.out_pk) a.out_key[o] = f;
+              if (a.out_pk) {  // what the owner probes (its own region's too): 12 bytes
                 uint32_t* pk = a.out_pk + (uint64_t)dest * a.cap_pk +
                                (uint64_t)kPkWords * (kPkHdr + (uint64_t)sub * a.route_cs + ridx);
                 pk[0] = (uint32_t)f.lo;
@@ -1643,6 +1643,7 @@ __global__ void k_route_headers(const RouteCounters* rc, Fp* out_key, uint64_t c
 struct ProbeSlabArgs {
   const Fp* in;
   const uint32_t* in_pk;  // the other sources' regions as received: packed (kPkWords per record); null: `in`
+  const uint32_t* self_pk;  // this shard's own region, packed (its out_pk)
   uint64_t cap_pk;
   const Fp* self;
   uint64_t cap_fp, cs;
@@ -1659,9 +1660,9 @@ __global__ void __launch_bounds__(kBlock) k_probe_slab(ProbeSlabArgs a) {
   __shared__ unsigned long long s_red[kBlock / 64];
   const int g = blockIdx.x, src = g / kRouteSegs, q = g - src * kRouteSegs;
   const bool self = src == a.me;
-  const bool pk = !self && a.in_pk;
+  const bool pk = a.in_pk != nullptr;  // packed regions: the received ones in in_pk, this shard's own in self_pk
   const Fp* region = self ? a.self : a.in + (uint64_t)src * a.cap_fp;
-  const uint32_t* pregion = pk ? a.in_pk + (uint64_t)src * a.cap_pk : nullptr;
+  const uint32_t* pregion = pk ? (self ? a.self_pk : a.in_pk + (uint64_t)src * a.cap_pk) : nullptr;
   const uint64_t n = min<uint64_t>(pk ? ((uint64_t)pregion[2 * q] | ((uint64_t)pregion[2 * q + 1] << 32))
                                       : reinterpret_cast<const uint64_t*>(region)[q], a.cs);
   uint8_t* rep = a.reply ? (self ? a.self_reply : a.reply + (uint64_t)src * a.cap_fp) : nullptr;
@@ -1786,7 +1787,7 @@ __global__ void __launch_bounds__(kBlock) k_new_list(NewListArgs a) {
 
 template <class P>
 struct MaterializeArgs {
-  const Fp* sent_key;                // this shard's routed fingerprints (regions of k_new_list's slots)
+  const Fp* sent_key;                // (unused since round 6: the fingerprint is recomputed from the parent's)
   const uint64_t* sent_item;         // ... and their (parent << 20 | event) items
   const uint64_t* list;              // the slots of the new ones (k_new_list)
   const unsigned long long* n_list;
@@ -1899,7 +1900,9 @@ __global__ void __launch_bounds__(kBlock) k_materialize(MaterializeArgs<P> a, ty
     }
     MAT_PH(2);
     if (act) {
-      f = a.sent_key[slot];
+      // the fingerprint again from the parent's (the routed records cross the links packed, and the
+      // source keeps no 16-byte copy of them)
+      f = delta_fingerprint<P>(w, a.cur_fp[parent], d);
       int pi = -1;
       uint32_t* my_nw = s_nodew + threadIdx.x * P::kNodeWords;
 #pragma unroll
