@@ -877,6 +877,15 @@ __global__ void __launch_bounds__(kLevelBlock) DSL_KLEVEL_ATTR k_level(LevelArgs
   int g = 0;
   int npass = 0;  // this workgroup's passes so far (ROUTE: its sub-slab rotates with them)
   for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+#ifndef DSL_NO_LANE_REMAT
+    // the lane indices as values opaque to the compiler, once per chunk: the per-lane addresses
+    // derived from them are recomputed where used instead of held live (and spilled) across
+    // chunks (C5 d12 scratch 36 -> 20 B/lane, C3 d10 60 -> 12 B/lane and +1.1 %:
+    // profiles/r06_remat_ab.txt)
+    int tid_c = tid, lane_c = lane;
+    asm volatile("" : "+v"(tid_c), "+v"(lane_c));
+    const int tid = tid_c, lane = lane_c, wid = tid_c >> 6;
+#endif
     if (a.budget_rt) {  // the deadline, before every chunk (one workgroup-uniform decision)
       if (tid == 0) s_tup = __builtin_amdgcn_s_memrealtime() - s_t0 > a.budget_rt ? 1 : 0;
       __syncthreads();

@@ -67,13 +67,21 @@ def test_time_limit_ends_queued_search(secs):
     s.maxTimeSecs(secs)
     e = Engine(proto)
     try:
-        for run in range(3):  # the first run also allocates the table; later ones have a queue time
+        # the queued levels' kernels load on their first launch (ms): a depth-8 search without a
+        # limit first, so that a test run alone times the same warm engine as the whole suite does
+        warm = argmap.settings(case["args"][:k] + ["--max-depth", "8"] + case["args"][k + 2:], proto, table_log2=27)
+        pd = e.bfs(proto.initial_state(), warm).per_depth
+        assert len(pd) >= 8 and pd == case["per_depth"][:len(pd)], pd
+        for run in range(4):  # the first run also allocates the table; later ones have a queue time
             r = e.bfs(proto.initial_state(), s)
             assert r.endCondition().name == "TIME_EXHAUSTED"
             # the first run allocates the 1 GiB table and the level buffers (hipMalloc, slow and
-            # variable); later runs stop right after the limit (a level past the deadline stops
-            # at its next chunk)
-            assert r.elapsed_s < secs + (2.0 if run == 0 else 0.25), (run, r.elapsed_s)
+            # variable); the second, with the whole limit for levels, reaches deeper and sizes the
+            # queue's history levels for that span (GiBs of hipMalloc, once: a 1.8 s outlier on
+            # one box); later runs allocate nothing and stop right after the limit (a level past
+            # the deadline stops at its next chunk)
+            print(f"time limit {secs}: run {run} {r.elapsed_s:.4f} s, depth {len(r.per_depth)}")
+            assert r.elapsed_s < secs + (2.5 if run < 2 else 0.25), (run, r.elapsed_s)
             n = min(len(r.per_depth), len(case["per_depth"]))
             assert r.per_depth[:n] == case["per_depth"][:n]
             if run:
