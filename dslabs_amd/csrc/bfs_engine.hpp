@@ -1847,7 +1847,9 @@ struct BfsEngine : EngineBase {
         if (queued) {  // this level's counters came back with the queue
           const unsigned char* set = hq + (size_t)q_pos * kCtrSet;
           std::memcpy(&sh[0].lc, set, sizeof(LevelCounters));
-          std::memcpy(segc[0].data(), set + kCtrSegOff, 8 * kSegs * kSegStride);
+          // only the segments' counter words (one per 128-byte line) from the pinned host buffer
+          for (int q = 0; q < kSegs; q++)
+            std::memcpy(&segc[0][(size_t)q * kSegStride], set + kCtrSegOff + (size_t)q * kSegStride * 8, 8);
         } else {
           for (int l = 0; l < L; l++) {
             Shard& S = sh[l];
@@ -2139,6 +2141,9 @@ struct BfsEngine : EngineBase {
         }
       }
     }
+    if (trace_levels)
+      fprintf(stderr, "[levels] %.4f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     // the search is over and no kernel of it is left to read the tables: zero them now, on the
     // stream, while the host assembles the result and the caller prepares the next search (whose
     // k_setup then only writes the seed); an error return above leaves table_clean false
@@ -2152,6 +2157,9 @@ struct BfsEngine : EngineBase {
         qctr_clean = true;
       }
     }
+    if (trace_levels)
+      fprintf(stderr, "[clear] %.4f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
     if (x_levels) cost_x_us = x_sum_us / (double)x_levels;
     if (q_span_adapt && L == 1) {
       uint64_t want = kQueueRowsMin;
